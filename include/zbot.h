@@ -1,0 +1,125 @@
+/*
+ * zbot.h — C ABI of libzbot_hip.so, the MI355X batched Z-Bot rollout engine.
+ *
+ * The engine replaces, for N environments at once, the ksim hot path that
+ * train.py drives:
+ *
+ *   zb_step  <- ksim RLTask.step_engine (un-vendored ksim 0.1.99, task/rl.py)
+ *               = for 20 substeps { FeetechActuators.get_stateful_ctrl
+ *                 (train.py:1242-1280) -> mjx.step (MuJoCo-MJX 3.3.4) }
+ *               -> terminations (train.py:1588-1593)
+ *               -> observations (train.py:1478-1537, run_actor/run_critic
+ *                  concatenations train.py:1624-1679)
+ *               -> per-step reward terms (train.py:1546-1586)
+ *               -> auto-reset of done envs (train.py:1471-1476)
+ *   zb_reset <- ksim MjxEngine.reset + mjx.forward (train.py:1471-1476,
+ *               FeetechActuators.get_initial_state train.py:1293-1298,
+ *               ImuOrientationObservation.initial_carry train.py:843-845)
+ *
+ * Conventions
+ *   - All device pointers are plain device addresses (e.g. torch
+ *     tensor.data_ptr()), contiguous, env-major, on the handle's device.
+ *   - `stream` is a hipStream_t passed as void* (0 = null stream). Every call
+ *     is asynchronous on that stream; no allocation, copy or synchronisation
+ *     happens inside zb_step / zb_reset (graph-capturable).
+ *   - Return value: 0 on success, negative ZB_E* on failure; the message of
+ *     the last failure on this thread is available from zb_last_error().
+ *   - Handles are not thread-safe; distinct handles are independent.
+ */
+#ifndef ZBOT_H
+#define ZBOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "zbot_layout.h"
+#include "zbot_model.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZB_OK          0
+#define ZB_EARG       -1   /* bad argument (null, size, layout mismatch) */
+#define ZB_EDEVICE    -2   /* HIP runtime error (device, alloc, copy) */
+#define ZB_ELAUNCH    -3   /* kernel launch failure */
+#define ZB_EMODEL     -4   /* model outside the engine's limits */
+
+typedef struct ZbHandle ZbHandle;
+
+/* Library / layout introspection (host only, no GPU needed). */
+int         zb_abi_version(void);
+size_t      zb_model_struct_bytes(void);
+size_t      zb_config_struct_bytes(void);
+int         zb_state_stride(void);
+int         zb_rand_stride(void);
+const char* zb_last_error(void);
+
+/* Fill `cfg` with the train.py defaults (train.py:1766-1788 + registered
+ * components). Host only. */
+void zb_default_config(ZbEnvConfig* cfg);
+
+/*
+ * Create a handle simulating `n_envs` environments whose global ids are
+ * [env_offset, env_offset + n_envs) — RNG streams are keyed by global id, so
+ * results for a given env do not depend on how envs are sharded over GPUs.
+ * Copies the model to `device`, allocates persistent state, does NOT reset
+ * (call zb_reset). Replaces ksim's mjx.put_model + engine construction.
+ */
+int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs,
+              int env_offset, int device, uint64_t seed, ZbHandle** out);
+int zb_destroy(ZbHandle* h);
+
+/*
+ * Reset environments (all when env_mask_dev is NULL, else those with
+ * env_mask_dev[e] != 0) and write their observations. Output pointers may be
+ * NULL to skip an output.
+ *   obs_actor  [n_envs, 50]   obs_critic [n_envs, 484]   obs_extra [n_envs, 96]
+ */
+int zb_reset(ZbHandle* h, const uint8_t* env_mask_dev, float* obs_actor,
+             float* obs_critic, float* obs_extra, void* stream);
+
+/*
+ * Advance every environment by one control step (n_substeps physics steps).
+ *   action       [n_envs, 20]  joint position targets, ctrl order (in)
+ *   obs_actor    [n_envs, 50]  observation of the next state (or of the reset
+ *                              state for envs that terminated)
+ *   obs_critic   [n_envs, 484]
+ *   obs_extra    [n_envs, 96]  (nullable)
+ *   reward_terms [n_envs, 12]  unscaled term values (nullable)
+ *   reward       [n_envs]      sum_i scale_i * (curriculum if by_curr) * term_i
+ *   done         [n_envs]      uint8 termination flag
+ *   curriculum_level           ksim curriculum scalar (one value for all envs)
+ */
+int zb_step(ZbHandle* h, const float* action, float* obs_actor,
+            float* obs_critic, float* obs_extra, float* reward_terms,
+            float* reward, uint8_t* done, float curriculum_level, void* stream);
+
+/* Run `n_steps` control steps back to back in ONE launch, with actions
+ * action[t][n_envs][20]; outputs of the last step only (rollout benchmark /
+ * fixed-policy rollouts). reward_sum [n_envs] (nullable) accumulates the
+ * total reward of every step. */
+int zb_rollout(ZbHandle* h, const float* actions, int n_steps,
+               float* obs_actor, float* obs_critic, float* reward_sum,
+               uint8_t* done, float curriculum_level, void* stream);
+
+/* Persistent state access: [n_envs, ZB_STATE_STRIDE] fp32 words (device).
+ * get copies out, set copies in (checkpoint / parity tests). */
+int zb_get_state(ZbHandle* h, float* state_dev, void* stream);
+int zb_set_state(ZbHandle* h, const float* state_dev, void* stream);
+/* Randomized parameters [n_envs, ZB_RAND_STRIDE] (config 5). */
+int zb_get_rand(ZbHandle* h, float* rand_dev, void* stream);
+int zb_set_rand(ZbHandle* h, const float* rand_dev, void* stream);
+
+/* Episode statistics [n_envs, ZB_NUM_STATS] accumulated by zb_step since the
+ * last clear (deterministic per-env partials for the cross-GPU reduction). */
+int zb_get_stats(ZbHandle* h, float* stats_dev, int clear, void* stream);
+
+/* Solver diagnostics: total solver iterations of the last launch summed over
+ * its substeps, per env ([n_envs] int32, device). */
+int zb_get_solver_iters(ZbHandle* h, int32_t* iters_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZBOT_H */

@@ -1,0 +1,507 @@
+"""Robot descriptor compiler: JSON robot description -> ZbModel (include/zbot_model.h).
+
+This is the build's stand-in for the part of MuJoCo's MJCF compiler that the
+reference relies on (train.py:1326-1331: `mujoco_scenes.mjcf.load_mjmodel` +
+`geom_priority[floor] = 2`). It runs once on the host, in float64, and produces:
+
+  * the kinematic tree in the index order MuJoCo would use (bodies in
+    definition order, dofs/qpos in body order);
+  * inertias of each body from its box dimensions (`box`) and mass;
+  * `qpos0` (joint zero) and the free-joint start height: the base is placed so
+    the foot soles touch the floor in the JOINT_BIASES pose (the reset pose,
+    train.py:1473) — the real MJCF's base height is unknown offline;
+  * the constants MuJoCo's `mj_setConst` derives at qpos0 and the constraint
+    model uses: `body_invweight0`, `dof_invweight0`, `stat.meaninertia`.
+
+The real Z-Bot MJCF is network-fetched by the reference (train.py:1327) and is
+unavailable here, so the default asset `assets/zbot_like.json` is a documented
+Z-Bot-like stand-in.
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import cstructs as cs
+from .constants import JOINT_BIASES
+
+ASSET_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+DEFAULT_ASSET = os.path.join(ASSET_DIR, "zbot_like.json")
+
+
+# --------------------------------------------------------------------------- #
+# small float64 rigid-body helpers (host only)
+# --------------------------------------------------------------------------- #
+def quat_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    w1, x1, y1, z1 = a
+    w2, x2, y2, z2 = b
+    return np.array(
+        [
+            w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2,
+            w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+            w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+            w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2,
+        ]
+    )
+
+
+def quat_to_mat(q: np.ndarray) -> np.ndarray:
+    w, x, y, z = q / np.linalg.norm(q)
+    return np.array(
+        [
+            [1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+            [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+            [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)],
+        ]
+    )
+
+
+def axis_angle_quat(axis: np.ndarray, angle: float) -> np.ndarray:
+    a = np.asarray(axis, dtype=np.float64)
+    a = a / np.linalg.norm(a)
+    s = math.sin(0.5 * angle)
+    return np.array([math.cos(0.5 * angle), a[0] * s, a[1] * s, a[2] * s])
+
+
+@dataclass
+class Body:
+    name: str
+    parent: int
+    pos: np.ndarray
+    quat: np.ndarray
+    mass: float
+    ipos: np.ndarray
+    inertia: np.ndarray
+    jnt_type: int = cs.JNT_NONE
+    jnt_name: str = ""
+    axis: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    jpos: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    jrange: tuple[float, float] | None = None
+    servo: dict | None = None
+    depth: int = 0
+    dofadr: int = -1
+    dofnum: int = 0
+    qposadr: int = -1
+    lastdof: int = -1
+
+
+@dataclass
+class CompiledModel:
+    """Host-side view of the compiled model (float64) plus the packed ZbModel."""
+
+    desc: dict
+    bodies: list[Body]
+    nq: int
+    nv: int
+    nu: int
+    qpos0: np.ndarray
+    dof_body: np.ndarray
+    dof_parent: np.ndarray
+    joint_names: list[str]
+    geom_names: list[str]
+    site_names: list[str]
+    cmodel: cs.ZbModel
+
+    @property
+    def body_names(self) -> list[str]:
+        return [b.name for b in self.bodies]
+
+    def reset_qpos(self) -> np.ndarray:
+        """qpos of the reset pose: base at qpos0, joints at JOINT_BIASES (train.py:1473)."""
+        q = self.qpos0.copy()
+        q[7:] = [b for _, b, _ in JOINT_BIASES]
+        return q
+
+
+# --------------------------------------------------------------------------- #
+# kinematics / dynamics in float64 (used only to derive model constants)
+# --------------------------------------------------------------------------- #
+def _kinematics(bodies: list[Body], qpos: np.ndarray) -> tuple[list[np.ndarray], list[np.ndarray]]:
+    xpos = [np.zeros(3) for _ in bodies]
+    xmat = [np.eye(3) for _ in bodies]
+    xquat = [np.array([1.0, 0, 0, 0]) for _ in bodies]
+    for i, b in enumerate(bodies):
+        if i == 0:
+            continue
+        p = b.parent
+        if b.jnt_type == cs.JNT_FREE:
+            xpos[i] = qpos[b.qposadr : b.qposadr + 3].copy()
+            xquat[i] = qpos[b.qposadr + 3 : b.qposadr + 7] / np.linalg.norm(qpos[b.qposadr + 3 : b.qposadr + 7])
+        else:
+            xpos[i] = xpos[p] + xmat[p] @ b.pos
+            xquat[i] = quat_mul(xquat[p], b.quat)
+            if b.jnt_type == cs.JNT_HINGE:
+                anchor = xpos[i] + quat_to_mat(xquat[i]) @ b.jpos
+                xquat[i] = quat_mul(xquat[i], axis_angle_quat(b.axis, qpos[b.qposadr]))
+                xpos[i] = anchor - quat_to_mat(xquat[i]) @ b.jpos
+        xmat[i] = quat_to_mat(xquat[i])
+    return xpos, xmat
+
+
+def _point_jacobian(bodies: list[Body], xpos, xmat, nv: int, dof_body, body: int, point: np.ndarray):
+    """Translational/rotational world Jacobians of a point fixed to `body`."""
+    jp = np.zeros((3, nv))
+    jr = np.zeros((3, nv))
+    b = body
+    while b > 0:
+        bd = bodies[b]
+        if bd.jnt_type == cs.JNT_FREE:
+            for k in range(3):
+                jp[:, bd.dofadr + k] = np.eye(3)[k]
+                axis = xmat[b][:, k]
+                jr[:, bd.dofadr + 3 + k] = axis
+                jp[:, bd.dofadr + 3 + k] = np.cross(axis, point - xpos[b])
+        elif bd.jnt_type == cs.JNT_HINGE:
+            axis = xmat[b] @ bd.axis
+            anchor = xpos[b] + xmat[b] @ bd.jpos
+            jr[:, bd.dofadr] = axis
+            jp[:, bd.dofadr] = np.cross(axis, point - anchor)
+        b = bd.parent
+    return jp, jr
+
+
+def mass_matrix(bodies: list[Body], qpos: np.ndarray, nv: int, dof_body, armature: np.ndarray) -> np.ndarray:
+    xpos, xmat = _kinematics(bodies, qpos)
+    M = np.diag(armature.astype(np.float64))
+    for i, b in enumerate(bodies):
+        if i == 0 or b.mass <= 0:
+            continue
+        com = xpos[i] + xmat[i] @ b.ipos
+        jp, jr = _point_jacobian(bodies, xpos, xmat, nv, dof_body, i, com)
+        Ri = xmat[i] @ quat_to_mat(np.array([1.0, 0, 0, 0]))
+        Iw = Ri @ np.diag(b.inertia) @ Ri.T
+        M += b.mass * jp.T @ jp + jr.T @ Iw @ jr
+    return M
+
+
+# --------------------------------------------------------------------------- #
+def _box_inertia(mass: float, box: list[float]) -> np.ndarray:
+    lx, ly, lz = box
+    return mass / 12.0 * np.array([ly * ly + lz * lz, lx * lx + lz * lz, lx * lx + ly * ly])
+
+
+def load_description(path: str | None = None) -> dict:
+    with open(path or DEFAULT_ASSET) as f:
+        return json.load(f)
+
+
+def compile_model(desc: dict | str | None = None) -> CompiledModel:
+    """Compile a JSON robot description into a ZbModel (+ host float64 view)."""
+    if desc is None or isinstance(desc, str):
+        desc = load_description(desc)
+
+    # ---- bodies -----------------------------------------------------------
+    bodies: list[Body] = [Body("world", -1, np.zeros(3), np.array([1.0, 0, 0, 0]), 0.0, np.zeros(3), np.zeros(3))]
+    names = {"world": 0}
+    servo_classes = desc.get("servo_classes", {})
+    auto_z = False
+    for bd in desc["bodies"]:
+        if bd["parent"] not in names:
+            raise ValueError(f"body {bd['name']}: parent {bd['parent']} must be defined before it")
+        pos = list(bd["pos"])
+        if pos[2] == "auto":
+            auto_z = True
+            pos[2] = 0.0
+        b = Body(
+            name=bd["name"],
+            parent=names[bd["parent"]],
+            pos=np.array(pos, dtype=np.float64),
+            quat=np.array(bd.get("quat", [1.0, 0.0, 0.0, 0.0]), dtype=np.float64),
+            mass=float(bd["mass"]),
+            ipos=np.array(bd.get("ipos", [0.0, 0.0, 0.0]), dtype=np.float64),
+            inertia=np.array(bd["inertia"], dtype=np.float64)
+            if "inertia" in bd
+            else _box_inertia(float(bd["mass"]), bd["box"]),
+        )
+        j = bd.get("joint")
+        if j is not None:
+            b.jnt_name = j["name"]
+            if j["type"] == "free":
+                if b.parent != 0:
+                    raise ValueError("free joint only allowed on a child of the world")
+                b.jnt_type = cs.JNT_FREE
+            elif j["type"] == "hinge":
+                b.jnt_type = cs.JNT_HINGE
+                b.axis = np.array(j["axis"], dtype=np.float64)
+                b.axis /= np.linalg.norm(b.axis)
+                b.jpos = np.array(j.get("pos", [0.0, 0.0, 0.0]), dtype=np.float64)
+                b.jrange = tuple(j["range"]) if "range" in j else None
+                b.servo = servo_classes[j["servo"]] if "servo" in j else None
+            else:
+                raise ValueError(f"unsupported joint type {j['type']}")
+        names[b.name] = len(bodies)
+        bodies.append(b)
+
+    nbody = len(bodies)
+    if nbody > cs.MAX_BODY:
+        raise ValueError(f"nbody={nbody} > {cs.MAX_BODY}")
+
+    # ---- dofs / qpos ----------------------------------------------------------
+    nq = nv = 0
+    dof_body: list[int] = []
+    dof_parent: list[int] = []
+    for i, b in enumerate(bodies):
+        if i == 0:
+            continue
+        b.depth = bodies[b.parent].depth + 1
+        parent_last = bodies[b.parent].lastdof
+        if b.jnt_type == cs.JNT_FREE:
+            b.dofadr, b.dofnum, b.qposadr = nv, 6, nq
+            for k in range(6):
+                dof_body.append(i)
+                dof_parent.append(parent_last if k == 0 else nv + k - 1)
+            nv += 6
+            nq += 7
+        elif b.jnt_type == cs.JNT_HINGE:
+            b.dofadr, b.dofnum, b.qposadr = nv, 1, nq
+            dof_body.append(i)
+            dof_parent.append(parent_last)
+            nv += 1
+            nq += 1
+        b.lastdof = b.dofadr + b.dofnum - 1 if b.dofnum else parent_last
+    if nv > cs.MAX_DOF or nq > cs.MAX_QPOS:
+        raise ValueError(f"nv={nv}/nq={nq} exceed limits")
+
+    dof_depth = np.zeros(nv, dtype=np.int64)
+    for d in range(nv):
+        dof_depth[d] = 0 if dof_parent[d] < 0 else dof_depth[dof_parent[d]] + 1
+    max_depth = int(dof_depth.max()) + 1
+    if max_depth > cs.MAX_DEPTH:
+        raise ValueError(f"dof chain depth {max_depth} > {cs.MAX_DEPTH}")
+    dof_anc = -np.ones((nv, cs.MAX_DEPTH), dtype=np.int64)
+    for d in range(nv):
+        a = d
+        while a >= 0:
+            dof_anc[d, dof_depth[a]] = a
+            a = dof_parent[a]
+
+    hinge_bodies = [b for b in bodies if b.jnt_type == cs.JNT_HINGE]
+    joint_names = [b.jnt_name for b in hinge_bodies]
+    nu = len(hinge_bodies)
+    bias_names = [n for n, _, _ in JOINT_BIASES]
+    if joint_names != bias_names:
+        raise ValueError(
+            "hinge joints must be defined in JOINT_BIASES order (train.py:61-82) so that "
+            "ctrl order == qpos[7:] order (train.py:1252-1253, 1358-1359)"
+        )
+
+    armature = np.zeros(nv)
+    damping = np.zeros(nv)
+    frictionloss = np.zeros(nv)
+    for b in hinge_bodies:
+        s = b.servo or {}
+        armature[b.dofadr] = s.get("armature", 0.0)
+        damping[b.dofadr] = s.get("damping", 0.0)
+        frictionloss[b.dofadr] = s.get("frictionloss", 0.0)
+
+    # ---- qpos0 and base height ---------------------------------------------------
+    qpos0 = np.zeros(nq)
+    root = bodies[1]
+    if root.jnt_type == cs.JNT_FREE:
+        qpos0[0:3] = root.pos
+        qpos0[3:7] = root.quat / np.linalg.norm(root.quat)
+
+    geoms = desc.get("geoms", [])
+    geom_names = [g["name"] for g in geoms]
+    if len(geoms) > cs.MAX_GEOM:
+        raise ValueError("too many collision geoms")
+
+    if auto_z:
+        q = qpos0.copy()
+        q[7:] = [v for _, v, _ in JOINT_BIASES]
+        xpos, xmat = _kinematics(bodies, q)
+        zmin = math.inf
+        for g in geoms:
+            bi = names[g["body"]]
+            size = np.array(g["size"])
+            gpos = xpos[bi] + xmat[bi] @ np.array(g.get("pos", [0, 0, 0]))
+            gmat = xmat[bi] @ quat_to_mat(np.array(g.get("quat", [1.0, 0, 0, 0])))
+            for sx in (-1, 1):
+                for sy in (-1, 1):
+                    for sz in (-1, 1):
+                        c = gpos + gmat @ (size * np.array([sx, sy, sz]))
+                        zmin = min(zmin, c[2])
+        qpos0[2] = -zmin + float(desc.get("base_clearance", 0.0))
+        root.pos[2] = qpos0[2]
+
+    # ---- mj_setConst equivalents at qpos0 ---------------------------------------
+    M0 = mass_matrix(bodies, qpos0, nv, dof_body, armature)
+    Minv = np.linalg.inv(M0)
+    xpos0, xmat0 = _kinematics(bodies, qpos0)
+    body_invweight = np.zeros((nbody, 2))
+    for i in range(1, nbody):
+        com = xpos0[i] + xmat0[i] @ bodies[i].ipos
+        jp, jr = _point_jacobian(bodies, xpos0, xmat0, nv, dof_body, i, com)
+        J = np.vstack([jp, jr])
+        A = J @ Minv @ J.T
+        body_invweight[i, 0] = np.trace(A[:3, :3]) / 3.0
+        body_invweight[i, 1] = np.trace(A[3:, 3:]) / 3.0
+    dof_invweight = np.diag(Minv).copy()
+    if root.jnt_type == cs.JNT_FREE:  # MuJoCo averages free-joint dofs (trans / rot)
+        dof_invweight[0:3] = dof_invweight[0:3].mean()
+        dof_invweight[3:6] = dof_invweight[3:6].mean()
+    meaninertia = float(np.trace(M0) / nv)
+
+    # ---- pack ZbModel ------------------------------------------------------------
+    m = cs.ZbModel()
+    m.magic = cs.MODEL_MAGIC
+    m.version = cs.MODEL_VERSION
+    m.struct_bytes = C_sizeof(cs.ZbModel)
+    m.nbody, m.nq, m.nv, m.nu = nbody, nq, nv, nu
+    m.ngeom = len(geoms)
+    m.max_depth = max_depth
+    opt = desc.get("option", {})
+    g = opt.get("gravity", [0.0, 0.0, -9.81])
+    for k in range(3):
+        m.gravity[k] = g[k]
+    m.timestep = opt.get("timestep", 0.001)
+    m.meaninertia = meaninertia
+
+    for i, b in enumerate(bodies):
+        m.body_parent[i] = b.parent
+        m.body_depth[i] = b.depth
+        m.body_jnttype[i] = b.jnt_type
+        m.body_dofadr[i] = b.dofadr
+        m.body_dofnum[i] = b.dofnum
+        m.body_qposadr[i] = b.qposadr
+        m.body_lastdof[i] = b.lastdof
+        for k in range(3):
+            m.body_pos[i][k] = b.pos[k]
+            m.body_ipos[i][k] = b.ipos[k]
+            m.body_inertia[i][k] = b.inertia[k]
+            m.jnt_axis[i][k] = b.axis[k]
+            m.jnt_pos[i][k] = b.jpos[k]
+        for k in range(4):
+            m.body_quat[i][k] = b.quat[k]
+        m.body_iquat[i][0] = 1.0
+        m.body_mass[i][0] = b.mass
+        m.body_invweight0[i][0] = body_invweight[i, 0]
+        m.body_invweight0[i][1] = body_invweight[i, 1]
+    # subtree masses
+    sub = np.array([b.mass for b in bodies])
+    for i in range(nbody - 1, 0, -1):
+        sub[bodies[i].parent] += sub[i]
+    for i in range(nbody):
+        m.body_mass[i][1] = sub[i]
+
+    for d in range(nv):
+        m.dof_body[d] = dof_body[d]
+        m.dof_parent[d] = dof_parent[d]
+        m.dof_depth[d] = int(dof_depth[d])
+        for e in range(cs.MAX_DEPTH):
+            m.dof_anc[d][e] = int(dof_anc[d, e])
+        m.dof_armature[d] = armature[d]
+        m.dof_damping[d] = damping[d]
+        m.dof_frictionloss[d] = frictionloss[d]
+        m.dof_invweight0[d] = dof_invweight[d]
+        m.dof_qposadr[d] = -1
+    for d in range(nv, cs.MAX_DOF):
+        m.dof_body[d] = -1
+        m.dof_parent[d] = -1
+        for e in range(cs.MAX_DEPTH):
+            m.dof_anc[d][e] = -1
+    for b in hinge_bodies:
+        m.dof_qposadr[b.dofadr] = b.qposadr
+        if b.jrange is not None:
+            m.dof_limited[b.dofadr] = 1
+            m.dof_range[b.dofadr][0] = b.jrange[0]
+            m.dof_range[b.dofadr][1] = b.jrange[1]
+    jc = desc.get("joint_constraint", {})
+    sr = jc.get("solref", [0.02, 1.0])
+    si = jc.get("solimp", [0.9, 0.95, 0.001, 0.5, 2.0])
+    for k in range(2):
+        m.dof_solref[k] = sr[k]
+    for k in range(5):
+        m.dof_solimp[k] = si[k]
+    for k in range(nq):
+        m.qpos0[k] = qpos0[k]
+
+    for a, b in enumerate(hinge_bodies):
+        s = b.servo or {}
+        m.act_dof[a] = b.dofadr
+        m.act_gear[a] = 1.0
+        mt = s.get("max_torque", 1e6)
+        m.act_ctrlrange[a][0] = -mt
+        m.act_ctrlrange[a][1] = mt
+        m.fe_kp[a] = s.get("kp", 0.0)
+        m.fe_kd[a] = s.get("kd", 0.0)
+        m.fe_error_gain[a] = s.get("error_gain", 1.0)
+        m.fe_max_pwm[a] = s.get("max_pwm", 1.0)
+        m.fe_vin[a] = s.get("vin", 12.0)
+        m.fe_kt[a] = s.get("kt", 1.0)
+        m.fe_R[a] = s.get("R", 1.0)
+        m.fe_vmax[a] = s.get("vmax", 5.0)
+        m.fe_amax[a] = s.get("amax", 17.45)
+        m.fe_max_torque[a] = mt
+        m.fe_max_velocity[a] = s.get("max_velocity", 5.0)
+        m.joint_bias[a] = JOINT_BIASES[a][1]
+        m.joint_weight[a] = JOINT_BIASES[a][2]
+
+    for gi, gd in enumerate(geoms):
+        if gd.get("type", "box") != "box":
+            raise ValueError("only box collision geoms are supported")
+        m.geom_body[gi] = names[gd["body"]]
+        gp = gd.get("pos", [0, 0, 0])
+        gq = gd.get("quat", [1.0, 0, 0, 0])
+        for k in range(3):
+            m.geom_pos[gi][k] = gp[k]
+            m.geom_size[gi][k] = gd["size"][k]
+        for k in range(4):
+            m.geom_quat[gi][k] = gq[k]
+    fl = desc.get("floor", {})
+    for k, v in enumerate(fl.get("friction", [1.0, 0.005, 0.0001])):
+        m.floor_friction[k] = v
+    for k, v in enumerate(fl.get("solref", [0.02, 1.0])):
+        m.floor_solref[k] = v
+    for k, v in enumerate(fl.get("solimp", [0.9, 0.95, 0.001, 0.5, 2.0])):
+        m.floor_solimp[k] = v
+    m.floor_margin = fl.get("margin", 0.0)
+
+    sites = desc.get("sites", [])
+    site_names = [s["name"] for s in sites]
+    m.nsite = len(sites)
+    for si_, sd in enumerate(sites):
+        m.site_body[si_] = names[sd["body"]]
+        sp = sd.get("pos", [0, 0, 0])
+        sq = sd.get("quat", [1.0, 0, 0, 0])
+        for k in range(3):
+            m.site_pos[si_][k] = sp[k]
+        for k in range(4):
+            m.site_quat[si_][k] = sq[k]
+    m.site_imu = site_names.index("imu_site")
+    m.site_left_foot = site_names.index("left_foot")
+    m.site_right_foot = site_names.index("right_foot")
+    m.body_base = 1
+    m.body_left_foot = names["Left_Foot"]
+    m.body_right_foot = names["Right_Foot"]
+    m.geom_left_foot = geom_names.index(sites[m.site_left_foot]["touch_geom"])
+    m.geom_right_foot = geom_names.index(sites[m.site_right_foot]["touch_geom"])
+
+    if nu != cs.NJ or nbody != cs.NBODY_TASK:
+        raise ValueError(f"the Z-Bot task layout needs nu=20, nbody=26 (got nu={nu}, nbody={nbody})")
+
+    return CompiledModel(
+        desc=desc,
+        bodies=bodies,
+        nq=nq,
+        nv=nv,
+        nu=nu,
+        qpos0=qpos0,
+        dof_body=np.array(dof_body),
+        dof_parent=np.array(dof_parent),
+        joint_names=joint_names,
+        geom_names=geom_names,
+        site_names=site_names,
+        cmodel=m,
+    )
+
+
+def C_sizeof(t: type) -> int:  # noqa: N802
+    import ctypes
+
+    return ctypes.sizeof(t)

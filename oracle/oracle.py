@@ -1,0 +1,144 @@
+"""ctypes wrapper of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; the product path (zbot_amd.engine) never does.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBS: dict[str, C.CDLL] = {}
+
+
+def build(force: bool = False) -> None:
+    """Compile the oracle libraries with the committed Makefile."""
+    targets = [os.path.join(HERE, "liboracle_zbot.so"), os.path.join(HERE, "liboracle_zbot_f64.so")]
+    if force or not all(os.path.exists(t) for t in targets):
+        subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def lib(precision: str = "f32") -> C.CDLL:
+    name = "liboracle_zbot.so" if precision == "f32" else "liboracle_zbot_f64.so"
+    if name in _LIBS:
+        return _LIBS[name]
+    path = os.path.join(HERE, name)
+    if not os.path.exists(path):
+        build()
+    L = C.CDLL(path)
+    fp = C.POINTER(C.c_float)
+    u8p = C.POINTER(C.c_uint8)
+    i32p = C.POINTER(C.c_int32)
+    L.zbo_threefry2x32.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)]
+    L.zbo_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint64, fp, fp, u8p, fp, fp, fp]
+    L.zbo_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint64, fp, fp, fp, fp, fp, fp, fp, fp,
+                           u8p, C.c_float, fp, i32p]
+    L.zbo_forward_debug.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp,
+                                    C.POINTER(C.c_int), fp]
+    L.zbo_simulate.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, C.c_int]
+    L.zbo_trapezoidal_step.argtypes = [fp, fp, fp, C.c_float, fp, fp, C.c_int, fp, fp]
+    L.zbo_rotate_quat_by_quat.argtypes = [fp, fp, C.c_int, fp]
+    L.zbo_synthetic_actions.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_uint32, C.c_float, fp]
+    L.zbo_field_offset.argtypes = [C.c_int, C.c_char_p]
+    L.zbo_field_offset.restype = C.c_long
+    L.zbo_struct_bytes.argtypes = [C.c_int]
+    L.zbo_struct_bytes.restype = C.c_size_t
+    _LIBS[name] = L
+    return L
+
+
+def _p(a: np.ndarray | None, t=C.c_float):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def threefry2x32(k0: int, k1: int, c0: int, c1: int) -> tuple[int, int]:
+    out = (C.c_uint32 * 2)()
+    lib().zbo_threefry2x32(k0 & 0xFFFFFFFF, k1 & 0xFFFFFFFF, c0 & 0xFFFFFFFF, c1 & 0xFFFFFFFF, out)
+    return out[0], out[1]
+
+
+def synthetic_actions(cmodel, seed: int, n: int, env_offset: int, t: int, std: float = 0.05) -> np.ndarray:
+    a = np.zeros((n, 20), dtype=np.float32)
+    lib().zbo_synthetic_actions(C.byref(cmodel), seed, n, env_offset, t, std, _p(a))
+    return a
+
+
+class OracleEnv:
+    """N environments simulated by the CPU oracle, same state layout as the engine."""
+
+    def __init__(self, cmodel, cfg, n_envs: int, env_offset: int = 0, seed: int = 0, precision: str = "f32"):
+        from zbot_amd import cstructs as cs  # noqa: PLC0415
+
+        self.cs = cs
+        self.L = lib(precision)
+        self.model = cmodel
+        self.cfg = cfg
+        self.n = n_envs
+        self.env_offset = env_offset
+        self.seed = seed
+        self.state = np.zeros((n_envs, cs.STATE_STRIDE), dtype=np.float32)
+        self.rand = np.zeros((n_envs, cs.RAND_STRIDE), dtype=np.float32)
+        self.stats = np.zeros((n_envs, cs.NUM_STATS), dtype=np.float32)
+        self.iters = np.zeros(n_envs, dtype=np.int32)
+
+    def reset(self, mask: np.ndarray | None = None):
+        cs = self.cs
+        oa = np.zeros((self.n, cs.OBS_ACTOR), dtype=np.float32)
+        oc = np.zeros((self.n, cs.OBS_CRITIC), dtype=np.float32)
+        ox = np.zeros((self.n, cs.OBS_EXTRA), dtype=np.float32)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        rc = self.L.zbo_reset(C.byref(self.model), C.byref(self.cfg), self.n, self.env_offset, self.seed,
+                              _p(self.state), _p(self.rand), _p(m, C.c_uint8), _p(oa), _p(oc), _p(ox))
+        assert rc == 0
+        return oa, oc, ox
+
+    def step(self, action: np.ndarray, curriculum: float = 1.0):
+        cs = self.cs
+        action = np.ascontiguousarray(action, dtype=np.float32)
+        assert action.shape == (self.n, cs.NJ)
+        oa = np.zeros((self.n, cs.OBS_ACTOR), dtype=np.float32)
+        oc = np.zeros((self.n, cs.OBS_CRITIC), dtype=np.float32)
+        ox = np.zeros((self.n, cs.OBS_EXTRA), dtype=np.float32)
+        terms = np.zeros((self.n, cs.NUM_TERMS), dtype=np.float32)
+        rew = np.zeros(self.n, dtype=np.float32)
+        done = np.zeros(self.n, dtype=np.uint8)
+        rc = self.L.zbo_step(C.byref(self.model), C.byref(self.cfg), self.n, self.env_offset, self.seed,
+                             _p(self.state), _p(self.rand), _p(action), _p(oa), _p(oc), _p(ox), _p(terms), _p(rew),
+                             _p(done, C.c_uint8), curriculum, _p(self.stats), _p(self.iters, C.c_int32))
+        assert rc == 0
+        return dict(obs_actor=oa, obs_critic=oc, obs_extra=ox, reward_terms=terms, reward=rew, done=done)
+
+
+def forward_debug(cmodel, cfg, qpos, qvel, ctrl=None, precision: str = "f32") -> dict:
+    nv, nb = cmodel.nv, cmodel.nbody
+    qpos = np.ascontiguousarray(qpos, dtype=np.float32)
+    qvel = np.ascontiguousarray(qvel, dtype=np.float32)
+    ctrl = None if ctrl is None else np.ascontiguousarray(ctrl, dtype=np.float32)
+    out = dict(
+        qM=np.zeros((nv, nv), np.float32), qfrc_bias=np.zeros(nv, np.float32), qacc_smooth=np.zeros(nv, np.float32),
+        qacc=np.zeros(nv, np.float32), xpos=np.zeros((nb, 3), np.float32), cinert=np.zeros((nb, 10), np.float32),
+        cvel=np.zeros((nb, 6), np.float32), touch=np.zeros(2, np.float32),
+    )
+    nn = (C.c_int * 2)()
+    lib(precision).zbo_forward_debug(C.byref(cmodel), C.byref(cfg), _p(qpos), _p(qvel), _p(ctrl), _p(out["qM"]),
+                                     _p(out["qfrc_bias"]), _p(out["qacc_smooth"]), _p(out["qacc"]), _p(out["xpos"]),
+                                     _p(out["cinert"]), _p(out["cvel"]), nn, _p(out["touch"]))
+    out["nefc"], out["ncon"] = nn[0], nn[1]
+    return out
+
+
+def simulate(cmodel, cfg, qpos, qvel, nsteps: int, ctrl=None, qaccw=None, precision: str = "f32"):
+    qpos = np.array(qpos, dtype=np.float32)
+    qvel = np.array(qvel, dtype=np.float32)
+    qaccw = np.zeros(cmodel.nv, np.float32) if qaccw is None else np.array(qaccw, dtype=np.float32)
+    ctrl = None if ctrl is None else np.ascontiguousarray(ctrl, dtype=np.float32)
+    lib(precision).zbo_simulate(C.byref(cmodel), C.byref(cfg), _p(qpos), _p(qvel), _p(qaccw), _p(ctrl), nsteps)
+    return qpos, qvel, qaccw
