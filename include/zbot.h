@@ -119,6 +119,14 @@ int zb_get_stats(ZbHandle* h, float* stats_dev, int clear, void* stream);
  * its substeps, per env ([n_envs] int32, device). */
 int zb_get_solver_iters(ZbHandle* h, int32_t* iters_dev, void* stream);
 
+/* Diagnostic: one forward pass (no integration) on the qpos/qvel stored in
+ * state_dev [n_envs, ZB_STATE_STRIDE] with ctrl_dev [n_envs, 20] (nullable ->
+ * zero ctrl); dumps M, bias, qacc_smooth, qacc, xpos, cinert, cvel and sensor
+ * values into dbg_dev [n_envs, 1760] (layout: csrc/zb_internal.h ZB_DBG_*).
+ * Used by the parity tests to localise differences to one pipeline stage. */
+int zb_debug_forward(ZbHandle* h, float* state_dev, const float* ctrl_dev,
+                     float* dbg_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,318 @@
+/*
+ * zb_capi.cpp — C ABI of libzbot_hip.so (declared in include/zbot.h).
+ *
+ * Host-side handle management: validates the compiled model against the
+ * engine's limits, owns the persistent per-env device buffers, and launches
+ * the kernels of zb_engine.hip asynchronously on the caller's stream. Nothing
+ * here allocates, copies or synchronises inside zb_step / zb_reset.
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "zb_internal.h"
+
+#define ZB_ABI_VERSION 1
+
+struct ZbHandle {
+  int device;
+  int n;
+  int env_offset;
+  uint64_t seed;
+  ZbModel hmodel;
+  ZbEnvConfig cfg;
+  ZbModel* dmodel;
+  float* state;
+  float* rnd;
+  float* stats;
+  int32_t* iters;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIPCHK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess) return fail(ZB_EDEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+static int use_device(const ZbHandle* h) {
+  int cur = -1;
+  HIPCHK(hipGetDevice(&cur));
+  if (cur != h->device) HIPCHK(hipSetDevice(h->device));
+  return ZB_OK;
+}
+
+extern "C" {
+
+int zb_abi_version(void) { return ZB_ABI_VERSION; }
+size_t zb_model_struct_bytes(void) { return sizeof(ZbModel); }
+size_t zb_config_struct_bytes(void) { return sizeof(ZbEnvConfig); }
+int zb_state_stride(void) { return ZB_STATE_STRIDE; }
+int zb_rand_stride(void) { return ZB_RAND_STRIDE; }
+const char* zb_last_error(void) { return g_err.c_str(); }
+
+void zb_default_config(ZbEnvConfig* c) {
+  if (!c) return;
+  memset(c, 0, sizeof *c);
+  const double PI = 3.14159265358979323846;
+  c->struct_bytes = (int32_t)sizeof(ZbEnvConfig);
+  c->flags = ZB_F_OBS_NOISE | ZB_F_AUTORESET;
+  c->n_substeps = 20;
+  c->iterations = 8;
+  c->ls_iterations = 8;
+  c->dt = 0.001f;
+  c->ctrl_dt = 0.02f;
+  c->tolerance = 1e-8f;
+  c->ls_tolerance = 0.01f;
+  c->imu_noise_std = (float)(PI / 180.0);
+  c->acc_noise_std = 0.5f;
+  c->reset_qvel_scale = 0.01f;
+  c->max_episode_sec = 80.f;
+  c->lag_range[0] = 0.f; c->lag_range[1] = 0.1f;
+  c->bad_z[0] = 0.05f; c->bad_z[1] = 0.5f;
+  c->max_tilt_rad = (float)(60.0 * PI / 180.0);
+  c->push_linvel[0] = 0.1f; c->push_linvel[1] = 0.1f; c->push_linvel[2] = 0.05f;
+  c->push_interval[0] = 2.f; c->push_interval[1] = 4.f;
+  c->push_vel_range[0] = 0.05f; c->push_vel_range[1] = 0.15f;
+  const float scales[ZB_NUM_TERMS] = {1.0f, 1.0f, 5.0f, 0.3f, -2.0f, 0.3f, 2.5f, 0.3f, -0.5f, -0.5f, -0.05f, -2.0f};
+  const int by_cur[ZB_NUM_TERMS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1};
+  for (int i = 0; i < ZB_NUM_TERMS; i++) {
+    c->reward_scale[i] = scales[i];
+    c->reward_by_curriculum[i] = by_cur[i];
+  }
+  c->feet_airtime_touchdown_penalty = 0.3f;
+  c->naive_forward_clip_max = 0.2f;
+  c->feet_orient_error_scale = 0.25f;
+  c->feet_too_close_threshold = 0.12f;
+  c->touch_threshold = 0.1f;
+  c->stay_alive_balance = 10.f;
+  c->rand_mass[0] = 0.95f; c->rand_mass[1] = 1.15f;
+  c->rand_armature[0] = 1.0f; c->rand_armature[1] = 1.05f;
+  c->rand_damping[0] = 0.95f; c->rand_damping[1] = 1.05f;
+  c->rand_friction[0] = 0.5f; c->rand_friction[1] = 1.5f;
+  c->rand_qpos0[0] = (float)(-2.0 * PI / 180.0); c->rand_qpos0[1] = (float)(2.0 * PI / 180.0);
+  c->rand_floor_mu[0] = 0.3f; c->rand_floor_mu[1] = 1.5f;
+  c->rand_imu_tilt_std = (float)(5.0 * PI / 180.0);
+  c->rand_imu_yaw_std = (float)(1.0 * PI / 180.0);
+  c->rand_imu_pos_std = 0.005f;
+}
+
+static int check_model(const ZbModel* m) {
+  if (m->magic != ZB_MODEL_MAGIC) return fail(ZB_EARG, "model magic mismatch");
+  if (m->version != ZB_MODEL_VERSION) return fail(ZB_EARG, "model version %d != %d", m->version, ZB_MODEL_VERSION);
+  if (m->struct_bytes != (int32_t)sizeof(ZbModel))
+    return fail(ZB_EARG, "model struct_bytes %d != %zu (layout mismatch)", m->struct_bytes, sizeof(ZbModel));
+  if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
+    return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
+  if (m->ngeom * ZB_CON_PER_GEOM * 4 > 32)
+    return fail(ZB_EMODEL, "ngeom=%d: contact rows exceed the 32-lane team", m->ngeom);
+  if (m->max_depth > ZB_MAX_DEPTH) return fail(ZB_EMODEL, "dof depth %d > %d", m->max_depth, ZB_MAX_DEPTH);
+  if (m->nu != ZB_NJ || m->nbody != ZB_NBODY_TASK)
+    return fail(ZB_EMODEL, "task layout needs nu=%d nbody=%d (got %d, %d)", ZB_NJ, ZB_NBODY_TASK, m->nu, m->nbody);
+  if (m->body_jnttype[1] != ZB_JNT_FREE) return fail(ZB_EMODEL, "body 1 must carry the free joint");
+  int maxbd = 0;
+  for (int b = 0; b < m->nbody; b++) {
+    if (m->body_depth[b] > maxbd) maxbd = m->body_depth[b];
+    int nch = 0;
+    for (int c = 1; c < m->nbody; c++)
+      if (m->body_parent[c] == b) nch++;
+    if (nch > 8) return fail(ZB_EMODEL, "body %d has %d children (max 8)", b, nch);
+  }
+  if (maxbd > 15) return fail(ZB_EMODEL, "body depth %d > 15", maxbd);
+  return ZB_OK;
+}
+
+static int check_cfg(const ZbEnvConfig* c) {
+  if (c->struct_bytes != (int32_t)sizeof(ZbEnvConfig))
+    return fail(ZB_EARG, "config struct_bytes %d != %zu", c->struct_bytes, sizeof(ZbEnvConfig));
+  if (c->n_substeps < 1 || c->iterations < 0 || c->ls_iterations < 0 || !(c->dt > 0.f))
+    return fail(ZB_EARG, "invalid solver/timestep configuration");
+  return ZB_OK;
+}
+
+int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_offset, int device, uint64_t seed,
+              ZbHandle** out) {
+  if (!model || !cfg || !out || n_envs < 0 || env_offset < 0) return fail(ZB_EARG, "zb_create: bad argument");
+  *out = nullptr;
+  int rc = check_model(model);
+  if (rc) return rc;
+  rc = check_cfg(cfg);
+  if (rc) return rc;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(ZB_EDEVICE, "device %d not available (%d devices)", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  ZbHandle* h = new ZbHandle();
+  h->device = device;
+  h->n = n_envs;
+  h->env_offset = env_offset;
+  h->seed = seed;
+  h->hmodel = *model;
+  h->cfg = *cfg;
+  size_t n = (size_t)(n_envs > 0 ? n_envs : 1);
+  hipError_t e = hipMalloc(&h->dmodel, sizeof(ZbModel));
+  if (e == hipSuccess) e = hipMalloc(&h->state, n * ZB_STATE_STRIDE * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&h->rnd, n * ZB_RAND_STRIDE * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&h->stats, n * ZB_NUM_STATS * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&h->iters, n * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemcpy(h->dmodel, model, sizeof(ZbModel), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(h->state, 0, n * ZB_STATE_STRIDE * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(h->rnd, 0, n * ZB_RAND_STRIDE * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(h->stats, 0, n * ZB_NUM_STATS * sizeof(float));
+  if (e == hipSuccess) e = hipMemset(h->iters, 0, n * sizeof(int32_t));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    zb_destroy(h);
+    return fail(ZB_EDEVICE, "zb_create: %s", hipGetErrorString(e));
+  }
+  *out = h;
+  return ZB_OK;
+}
+
+int zb_destroy(ZbHandle* h) {
+  if (!h) return ZB_OK;
+  (void)hipSetDevice(h->device);
+  if (h->dmodel) (void)hipFree(h->dmodel);
+  if (h->state) (void)hipFree(h->state);
+  if (h->rnd) (void)hipFree(h->rnd);
+  if (h->stats) (void)hipFree(h->stats);
+  if (h->iters) (void)hipFree(h->iters);
+  delete h;
+  return ZB_OK;
+}
+
+static zb::StepArgs base_args(ZbHandle* h) {
+  zb::StepArgs a;
+  memset(&a, 0, sizeof a);
+  a.model = h->dmodel;
+  a.cfg = h->cfg;
+  a.n_envs = h->n;
+  a.env_offset = h->env_offset;
+  a.seed = h->seed;
+  a.state = h->state;
+  a.rnd = h->rnd;
+  a.stats = h->stats;
+  a.iters = h->iters;
+  a.nsteps = 1;
+  a.curriculum = 1.f;
+  return a;
+}
+
+int zb_reset(ZbHandle* h, const uint8_t* env_mask_dev, float* obs_actor, float* obs_critic, float* obs_extra,
+             void* stream) {
+  if (!h) return fail(ZB_EARG, "zb_reset: null handle");
+  int rc = use_device(h);
+  if (rc) return rc;
+  zb::StepArgs a = base_args(h);
+  a.reset_mask = env_mask_dev;
+  a.obs_actor = obs_actor;
+  a.obs_critic = obs_critic;
+  a.obs_extra = obs_extra;
+  hipError_t e = zb::launch_reset(a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_reset launch: %s", hipGetErrorString(e));
+  return ZB_OK;
+}
+
+int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_critic, float* obs_extra,
+            float* reward_terms, float* reward, uint8_t* done, float curriculum_level, void* stream) {
+  if (!h || !action) return fail(ZB_EARG, "zb_step: null handle or action");
+  if (!(curriculum_level == curriculum_level)) return fail(ZB_EARG, "zb_step: curriculum is NaN");
+  int rc = use_device(h);
+  if (rc) return rc;
+  zb::StepArgs a = base_args(h);
+  a.action = action;
+  a.obs_actor = obs_actor;
+  a.obs_critic = obs_critic;
+  a.obs_extra = obs_extra;
+  a.reward_terms = reward_terms;
+  a.reward = reward;
+  a.done = done;
+  a.curriculum = curriculum_level;
+  hipError_t e = zb::launch_step(a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_step launch: %s", hipGetErrorString(e));
+  return ZB_OK;
+}
+
+int zb_rollout(ZbHandle* h, const float* actions, int n_steps, float* obs_actor, float* obs_critic, float* reward_sum,
+               uint8_t* done, float curriculum_level, void* stream) {
+  if (!h || !actions || n_steps < 1) return fail(ZB_EARG, "zb_rollout: bad argument");
+  int rc = use_device(h);
+  if (rc) return rc;
+  zb::StepArgs a = base_args(h);
+  a.action = actions;
+  a.nsteps = n_steps;
+  a.obs_actor = obs_actor;
+  a.obs_critic = obs_critic;
+  a.reward = reward_sum;
+  a.done = done;
+  a.curriculum = curriculum_level;
+  hipError_t e = zb::launch_step(a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_rollout launch: %s", hipGetErrorString(e));
+  return ZB_OK;
+}
+
+static int copy_rows(ZbHandle* h, void* dst, const void* src, size_t bytes, void* stream) {
+  if (!h || !dst || !src) return fail(ZB_EARG, "null pointer");
+  int rc = use_device(h);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return ZB_OK;
+}
+
+int zb_get_state(ZbHandle* h, float* state_dev, void* stream) {
+  if (!h) return fail(ZB_EARG, "null handle");
+  return copy_rows(h, state_dev, h->state, (size_t)h->n * ZB_STATE_STRIDE * sizeof(float), stream);
+}
+int zb_set_state(ZbHandle* h, const float* state_dev, void* stream) {
+  if (!h) return fail(ZB_EARG, "null handle");
+  return copy_rows(h, h->state, state_dev, (size_t)h->n * ZB_STATE_STRIDE * sizeof(float), stream);
+}
+int zb_get_rand(ZbHandle* h, float* rand_dev, void* stream) {
+  if (!h) return fail(ZB_EARG, "null handle");
+  return copy_rows(h, rand_dev, h->rnd, (size_t)h->n * ZB_RAND_STRIDE * sizeof(float), stream);
+}
+int zb_set_rand(ZbHandle* h, const float* rand_dev, void* stream) {
+  if (!h) return fail(ZB_EARG, "null handle");
+  return copy_rows(h, h->rnd, rand_dev, (size_t)h->n * ZB_RAND_STRIDE * sizeof(float), stream);
+}
+int zb_get_stats(ZbHandle* h, float* stats_dev, int clear, void* stream) {
+  if (!h) return fail(ZB_EARG, "null handle");
+  int rc = copy_rows(h, stats_dev, h->stats, (size_t)h->n * ZB_NUM_STATS * sizeof(float), stream);
+  if (rc) return rc;
+  if (clear) HIPCHK(hipMemsetAsync(h->stats, 0, (size_t)h->n * ZB_NUM_STATS * sizeof(float), (hipStream_t)stream));
+  return ZB_OK;
+}
+int zb_get_solver_iters(ZbHandle* h, int32_t* iters_dev, void* stream) {
+  if (!h) return fail(ZB_EARG, "null handle");
+  return copy_rows(h, iters_dev, h->iters, (size_t)h->n * sizeof(int32_t), stream);
+}
+
+int zb_debug_forward(ZbHandle* h, float* state_dev, const float* ctrl_dev, float* dbg_dev, void* stream) {
+  if (!h || !state_dev || !dbg_dev) return fail(ZB_EARG, "zb_debug_forward: null pointer");
+  int rc = use_device(h);
+  if (rc) return rc;
+  zb::StepArgs a = base_args(h);
+  a.state = state_dev;
+  a.action = ctrl_dev;
+  a.dbg = dbg_dev;
+  hipError_t e = zb::launch_debug_forward(a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_debug_forward launch: %s", hipGetErrorString(e));
+  return ZB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,1873 @@
+/*
+ * zb_engine.hip — MI355X (gfx950) batched Z-Bot env.step()/reset() engine.
+ *
+ * Replaces, per environment, ksim's step_engine over MuJoCo-MJX:
+ *   20 x [FeetechActuators.get_stateful_ctrl (train.py:1242-1280) -> mj_step]
+ *   -> terminations (train.py:1588-1593) -> reward terms (train.py:1546-1586)
+ *   -> observations (train.py:1478-1537, 1624-1679) -> auto-reset (train.py:1471-1476)
+ *
+ * Execution model:
+ *   - one TEAM of 32 lanes simulates one environment; a 64-lane wavefront
+ *     holds two teams; a workgroup is exactly one wavefront, so "team sync"
+ *     is a single-wave barrier (LDS ordering only, no cross-wave traffic);
+ *   - lane l plays three roles: body l (kinematics, inertias, velocities),
+ *     dof l (mass-matrix row, factor row, accelerations) and constraint row l
+ *     (the 32 pyramid edges of the 8 sole/floor contacts);
+ *   - the dof tree is stored "depth-indexed": row j of M / L holds the
+ *     entries (j, anc_e(j)) for e = 0..depth(j) (MuJoCo's sparse tree layout,
+ *     mj_factorM), so every row fits 12 registers/LDS words;
+ *   - all 20 substeps of a control step, the Newton solve, sensors, rewards,
+ *     observations and auto-reset run inside ONE launch; HBM traffic is one
+ *     read and one write of the env's state row plus its outputs.
+ *
+ * Numerics: fp32 like the reference (JAX x64 off). Team reductions are xor
+ * butterflies, so every lane of a team holds the bit-identical sum and all
+ * team-uniform decisions agree. Results are deterministic run to run and
+ * independent of how envs are sharded (RNG keyed by global env id).
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "zb_internal.h"
+
+namespace zb {
+
+constexpr int TEAM = 32;
+constexpr int NTEAM = 64 / TEAM;
+constexpr int CAP = ZB_MAX_DEPTH; /* 12 */
+constexpr float MINVAL = 1e-15f;
+constexpr float MINIMP = 0.0001f;
+constexpr float MAXIMP = 0.9999f;
+constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0); /* train.py:1113-1116 */
+
+enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3 };
+
+/* per-environment LDS working set (8.6 KB) */
+struct EnvL {
+  float cdof[32][6];
+  float cdofdot[32][6];
+  float M[32][CAP];
+  float L[32][CAP];
+  float J[32][CAP];
+  float sub[32][10];
+  float vec[4][32];
+  float rowDA[32];
+  float rowF[32];
+  float Dk[32];
+  int rowlist[32];
+};
+
+/* ----------------------------- team primitives ----------------------------- */
+__device__ __forceinline__ float tsh(float v, int src) { return __shfl(v, src, TEAM); }
+__device__ __forceinline__ int tshi(int v, int src) { return __shfl(v, src, TEAM); }
+__device__ __forceinline__ float tsum(float v) {
+#pragma unroll
+  for (int o = TEAM / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, TEAM);
+  return v;
+}
+__device__ __forceinline__ float tmaxf(float v) {
+#pragma unroll
+  for (int o = TEAM / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, TEAM));
+  return v;
+}
+__device__ __forceinline__ int tmaxi(int v) {
+#pragma unroll
+  for (int o = TEAM / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, TEAM));
+  return v;
+}
+__device__ __forceinline__ void tsync() { __syncthreads(); }
+
+/* ------------------------------- small math -------------------------------- */
+__device__ __forceinline__ void cross3(float r[3], const float a[3], const float b[3]) {
+  float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ float dot3(const float a[3], const float b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+__device__ __forceinline__ void quat_mul(float r[4], const float a[4], const float b[4]) {
+  float w = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float x = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float y = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float z = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = w; r[1] = x; r[2] = y; r[3] = z;
+}
+__device__ __forceinline__ void quat_normalize(float q[4]) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  float s = 1.0f / n;
+  q[0] *= s; q[1] *= s; q[2] *= s; q[3] *= s;
+}
+__device__ __forceinline__ void quat2mat(float m[9], const float q[4]) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  m[0] = 1 - 2 * (y * y + z * z); m[1] = 2 * (x * y - w * z); m[2] = 2 * (x * z + w * y);
+  m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
+  m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void mulmv3(float r[3], const float m[9], const float v[3]) {
+  float t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
+  float t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
+  float t2 = m[6] * v[0] + m[7] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mulmtv3(float r[3], const float m[9], const float v[3]) {
+  float t0 = m[0] * v[0] + m[3] * v[1] + m[6] * v[2];
+  float t1 = m[1] * v[0] + m[4] * v[1] + m[7] * v[2];
+  float t2 = m[2] * v[0] + m[5] * v[1] + m[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mulmm3(float r[9], const float a[9], const float b[9]) {
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+}
+__device__ __forceinline__ void axis_angle_quat(float q[4], const float ax[3], float angle) {
+  float s, c;
+  sincosf(0.5f * angle, &s, &c);
+  q[0] = c; q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
+}
+__device__ __forceinline__ void cross_motion(float r[6], const float v[6], const float u[6]) {
+  float a[3], b[3], c[3];
+  cross3(a, v, u);
+  cross3(b, v, u + 3);
+  cross3(c, v + 3, u);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+__device__ __forceinline__ void cross_force(float r[6], const float v[6], const float f[6]) {
+  float a[3], b[3], c[3];
+  cross3(a, v, f);
+  cross3(b, v + 3, f + 3);
+  cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+__device__ __forceinline__ void mul_inert_vec(float r[6], const float i[10], const float v[6]) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+__device__ __forceinline__ float dot6(const float a[6], const float b[6]) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
+
+/* ------------------------ RNG: threefry2x32-20 (Random123) ------------------ */
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ void threefry2x32(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t& o0,
+                                             uint32_t& o1) {
+  const uint32_t ks2 = 0x1BD11BDAu ^ k0 ^ k1;
+  uint32_t x0 = c0 + k0, x1 = c1 + k1;
+#define TF_R(r) { x0 += x1; x1 = rotl32(x1, r); x1 ^= x0; }
+  TF_R(13) TF_R(15) TF_R(26) TF_R(6)  x0 += k1;  x1 += ks2 + 1u;
+  TF_R(17) TF_R(29) TF_R(16) TF_R(24) x0 += ks2; x1 += k0 + 2u;
+  TF_R(13) TF_R(15) TF_R(26) TF_R(6)  x0 += k0;  x1 += k1 + 3u;
+  TF_R(17) TF_R(29) TF_R(16) TF_R(24) x0 += k1;  x1 += ks2 + 4u;
+  TF_R(13) TF_R(15) TF_R(26) TF_R(6)  x0 += ks2; x1 += k0 + 5u;
+#undef TF_R
+  o0 = x0; o1 = x1;
+}
+#define P_OBS 1u
+#define P_PUSH 2u
+#define P_RESET 3u
+#define P_RAND 4u
+__device__ __forceinline__ void rng_bits(uint64_t seed, uint32_t purpose, uint32_t k, uint32_t env, uint32_t ctr,
+                                         uint32_t& a, uint32_t& b) {
+  threefry2x32((uint32_t)seed ^ (purpose * 0x9E3779B9u), (uint32_t)(seed >> 32) ^ (k * 0x85EBCA6Bu), env, ctr, a, b);
+}
+__device__ __forceinline__ float u01(uint32_t b) { return (float)(b >> 8) * (1.0f / 16777216.0f); }
+__device__ __forceinline__ void uniform2(uint64_t seed, uint32_t p, uint32_t k, uint32_t env, uint32_t ctr, float& u0,
+                                         float& u1) {
+  uint32_t a, b;
+  rng_bits(seed, p, k, env, ctr, a, b);
+  u0 = u01(a);
+  u1 = u01(b);
+}
+__device__ __forceinline__ void normal2(uint64_t seed, uint32_t p, uint32_t k, uint32_t env, uint32_t ctr, float& z0,
+                                        float& z1) {
+  uint32_t a, b;
+  rng_bits(seed, p, k, env, ctr, a, b);
+  float u1 = 1.0f - u01(a), u2 = u01(b);
+  float r = sqrtf(-2.0f * logf(u1));
+  float s, c;
+  sincosf(6.283185307179586f * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+/* --------------------------------- contexts -------------------------------- */
+struct Ctx {
+  const ZbModel* m;
+  const ZbEnvConfig* cfg;
+  EnvL* L;
+  uint64_t seed;
+  uint32_t env;
+  int l;
+  int nb, nv, nu, ngeom, maxbd, maxdd;
+  /* lane as body */
+  int bpar, bdep, bjt, bdofadr, blast, nch;
+  uint32_t ch0, ch1;
+  uint64_t lvlch; /* per body depth: max #children among bodies at that depth (4 bits each) */
+  /* lane as dof */
+  int ddep, dbody, qadr, act;
+  uint32_t anc0, anc1, anc2;
+  uint32_t desc; /* strict descendants of dof l */
+};
+
+__device__ __forceinline__ int ancof(const Ctx& c, int e) {
+  uint32_t w = e < 4 ? c.anc0 : (e < 8 ? c.anc1 : c.anc2);
+  return (int)((w >> ((e & 3) * 8)) & 0xffu);
+}
+__device__ __forceinline__ int anc_packed(uint32_t a0, uint32_t a1, uint32_t a2, int e) {
+  uint32_t w = e < 4 ? a0 : (e < 8 ? a1 : a2);
+  return (int)((w >> ((e & 3) * 8)) & 0xffu);
+}
+__device__ __forceinline__ int childof(const Ctx& c, int k) {
+  uint32_t w = k < 4 ? c.ch0 : c.ch1;
+  return (int)((w >> ((k & 3) * 8)) & 0xffu);
+}
+
+/* per-env replicated scalars */
+struct EnvS {
+  float bp[3], bq[4];
+  float ema[4], lag, air[2], push_timer, touch[2], feet_dist, ep_ret, prev_cont[2];
+  uint32_t ep_steps, rng_step, episode, nanflag;
+  float floor_mu, imu_q[4], imu_p[3];
+};
+/* per-lane persistent registers */
+struct LaneS {
+  float q, v, w;        /* dof lane: hinge angle, qvel, qacc_warmstart */
+  float q0;             /* joint zero (hinge) */
+  float pp, pv, ptau;   /* planner (actuated dof lane) */
+  float tgt;            /* action target */
+  float arm, damp, floss; /* effective dof params */
+  float mscale;         /* body lane mass scale */
+  float ctrl;           /* actuator ctrl of this dof lane */
+  float qacc;           /* last constrained qacc */
+  float actforce;       /* actuator force (gear*clamped ctrl) */
+};
+/* per-substep body outputs */
+struct BodyK {
+  float xp[3], xq[4], R[9];
+  float ci[10], cv[6];
+};
+struct Sensors {
+  float fq[4], gyro[3], acc[3], touch[2], force[6];
+};
+/* constraint rows held by the lane */
+struct Rows {
+  /* contact row (lane = row) */
+  bool ex;
+  uint32_t ka0, ka1, ka2; int kdep; int kd;
+  float aref, D, jar, Jv, f;
+  int act;
+  float dir[3], pos[3];
+  int geom;
+  /* dof rows: frictionloss, lower, upper limit */
+  bool hf, hlo, hhi;
+  float af, Df, Rf, fl, jf, ff; int actf;
+  float alo, Dlo, jlo, flo; int actlo;
+  float ahi, Dhi, jhi, fhi; int acthi;
+  int nrow;
+};
+
+/* ------------------------------- kinematics -------------------------------- */
+__device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B) {
+  const ZbModel* m = c.m;
+  /* relative hinge angle of this body's joint, from its dof lane */
+  float qrel_dof = ls.q - ls.q0;
+  float ang = tsh(qrel_dof, c.bdofadr < 0 ? 0 : c.bdofadr);
+  B.xp[0] = B.xp[1] = B.xp[2] = 0.f;
+  B.xq[0] = 1.f; B.xq[1] = B.xq[2] = B.xq[3] = 0.f;
+  int par = c.bpar < 0 ? 0 : c.bpar;
+  for (int d = 1; d <= c.maxbd; d++) {
+    float pxp[3], pxq[4];
+#pragma unroll
+    for (int k = 0; k < 3; k++) pxp[k] = tsh(B.xp[k], par);
+#pragma unroll
+    for (int k = 0; k < 4; k++) pxq[k] = tsh(B.xq[k], par);
+    if (c.bdep == d) {
+      const int b = c.l;
+      if (c.bjt == ZB_JNT_FREE) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) B.xp[k] = s.bp[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) B.xq[k] = s.bq[k];
+        quat_normalize(B.xq);
+      } else {
+        float pR[9], t[3];
+        quat2mat(pR, pxq);
+        float bpos[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]};
+        float bqt[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]};
+        mulmv3(t, pR, bpos);
+        float xp[3] = {pxp[0] + t[0], pxp[1] + t[1], pxp[2] + t[2]}, xq[4];
+        quat_mul(xq, pxq, bqt);
+        if (c.bjt == ZB_JNT_HINGE) {
+          float R[9], jp[3] = {m->jnt_pos[b][0], m->jnt_pos[b][1], m->jnt_pos[b][2]};
+          float ax[3] = {m->jnt_axis[b][0], m->jnt_axis[b][1], m->jnt_axis[b][2]};
+          quat2mat(R, xq);
+          mulmv3(t, R, jp);
+          float anchor[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
+          float ql[4], qn[4];
+          axis_angle_quat(ql, ax, ang);
+          quat_mul(qn, xq, ql);
+          quat_normalize(qn);
+          quat2mat(R, qn);
+          mulmv3(t, R, jp);
+#pragma unroll
+          for (int k = 0; k < 3; k++) xp[k] = anchor[k] - t[k];
+#pragma unroll
+          for (int k = 0; k < 4; k++) xq[k] = qn[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) B.xp[k] = xp[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) B.xq[k] = xq[k];
+      }
+    }
+  }
+  quat2mat(B.R, B.xq);
+}
+
+/* subtree sum of K-vectors over the body tree: out (lane b) = sum over subtree(b).
+ * Uses c.L->sub as the exchange buffer; result also left in sub[b]. */
+template <int K>
+__device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
+  EnvL* L = c.L;
+  for (int d = c.maxbd; d >= 1; d--) {
+    int nmax = (int)((c.lvlch >> (4 * d)) & 0xfull);
+    if (c.bdep == d) {
+      for (int k = 0; k < nmax; k++) {
+        if (k < c.nch) {
+          int ch = childof(c, k);
+#pragma unroll
+          for (int i = 0; i < K; i++) v[i] += L->sub[ch][i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < K; i++) L->sub[c.l][i] = v[i];
+    }
+    tsync();
+  }
+}
+
+/* ------------------------------ mass matrix -------------------------------- */
+/* com, cinert (lane b), cdof (lane j -> LDS), crb, M rows (LDS + return) */
+__device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B, float cm[3]) {
+  const ZbModel* m = c.m;
+  EnvL* L = c.L;
+  const int b = c.l;
+  const bool isbody = b >= 1 && b < c.nb;
+  float mass = isbody ? m->body_mass[b][0] * ls.mscale : 0.f;
+  float xipos[3], Ri[9];
+  {
+    float ip[3] = {m->body_ipos[isbody ? b : 0][0], m->body_ipos[isbody ? b : 0][1], m->body_ipos[isbody ? b : 0][2]}, t[3];
+    mulmv3(t, B.R, ip);
+#pragma unroll
+    for (int k = 0; k < 3; k++) xipos[k] = B.xp[k] + t[k];
+    float iq[4] = {m->body_iquat[isbody ? b : 0][0], m->body_iquat[isbody ? b : 0][1],
+                   m->body_iquat[isbody ? b : 0][2], m->body_iquat[isbody ? b : 0][3]}, iR[9];
+    quat2mat(iR, iq);
+    mulmm3(Ri, B.R, iR);
+  }
+  float mt = tsum(mass);
+#pragma unroll
+  for (int k = 0; k < 3; k++) cm[k] = tsum(mass * xipos[k]) / mt;
+  /* cinert: inertia about cm in world orientation (mju_inertCom) */
+  {
+    float in[3] = {0.f, 0.f, 0.f};
+    if (isbody) {
+      in[0] = m->body_inertia[b][0] * ls.mscale;
+      in[1] = m->body_inertia[b][1] * ls.mscale;
+      in[2] = m->body_inertia[b][2] * ls.mscale;
+    }
+    float dif[3] = {xipos[0] - cm[0], xipos[1] - cm[1], xipos[2] - cm[2]};
+    float I[9];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int bb = 0; bb < 3; bb++)
+        I[3 * a + bb] = Ri[3 * a] * in[0] * Ri[3 * bb] + Ri[3 * a + 1] * in[1] * Ri[3 * bb + 1] +
+                        Ri[3 * a + 2] * in[2] * Ri[3 * bb + 2];
+    float dd = dot3(dif, dif);
+    B.ci[0] = I[0] + mass * (dd - dif[0] * dif[0]);
+    B.ci[1] = I[4] + mass * (dd - dif[1] * dif[1]);
+    B.ci[2] = I[8] + mass * (dd - dif[2] * dif[2]);
+    B.ci[3] = I[1] - mass * dif[0] * dif[1];
+    B.ci[4] = I[2] - mass * dif[0] * dif[2];
+    B.ci[5] = I[5] - mass * dif[1] * dif[2];
+    B.ci[6] = mass * dif[0];
+    B.ci[7] = mass * dif[1];
+    B.ci[8] = mass * dif[2];
+    B.ci[9] = mass;
+  }
+  /* cdof (lane j): fetch body frame of dof's body */
+  {
+    const int j = c.l;
+    int bj = c.dbody < 0 ? 0 : c.dbody;
+    float R[9], xp[3];
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], bj);
+#pragma unroll
+    for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], bj);
+    if (j < c.nv) {
+      float cd[6];
+      int jt = m->body_jnttype[bj];
+      if (jt == ZB_JNT_FREE) {
+        int k = j - m->body_dofadr[bj];
+        if (k < 3) {
+          cd[0] = cd[1] = cd[2] = 0.f;
+          cd[3] = k == 0 ? 1.f : 0.f; cd[4] = k == 1 ? 1.f : 0.f; cd[5] = k == 2 ? 1.f : 0.f;
+        } else {
+          float ax[3] = {R[k - 3], R[3 + k - 3], R[6 + k - 3]};
+          float off[3] = {cm[0] - xp[0], cm[1] - xp[1], cm[2] - xp[2]};
+          cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+          cross3(cd + 3, ax, off);
+        }
+      } else {
+        float jp[3] = {m->jnt_pos[bj][0], m->jnt_pos[bj][1], m->jnt_pos[bj][2]};
+        float ja[3] = {m->jnt_axis[bj][0], m->jnt_axis[bj][1], m->jnt_axis[bj][2]};
+        float t[3], ax[3];
+        mulmv3(t, R, jp);
+        mulmv3(ax, R, ja);
+        float off[3] = {cm[0] - (xp[0] + t[0]), cm[1] - (xp[1] + t[1]), cm[2] - (xp[2] + t[2])};
+        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+        cross3(cd + 3, ax, off);
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) L->cdof[j][k] = cd[k];
+    }
+  }
+  /* crb = subtree sums of cinert */
+  float crb[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) crb[k] = B.ci[k];
+  tsync();
+  subtree_sum<10>(c, crb);
+  /* M rows: M(j, anc_e(j)) = cdof_anc . (crb_body(j) * cdof_j) */
+  {
+    const int j = c.l;
+    if (j < c.nv) {
+      float cr[10], cd[6], F[6];
+#pragma unroll
+      for (int k = 0; k < 10; k++) cr[k] = L->sub[c.dbody][k];
+#pragma unroll
+      for (int k = 0; k < 6; k++) cd[k] = L->cdof[j][k];
+      mul_inert_vec(F, cr, cd);
+#pragma unroll
+      for (int e = 0; e < CAP; e++) {
+        float v = 0.f;
+        if (e <= c.ddep) {
+          int a = ancof(c, e);
+          float ca[6];
+#pragma unroll
+          for (int k = 0; k < 6; k++) ca[k] = L->cdof[a][k];
+          v = dot6(ca, F);
+          if (e == c.ddep) v += ls.arm;
+        }
+        L->M[j][e] = v;
+      }
+    }
+  }
+  tsync();
+}
+
+/* ---------------------- sparse L'DL factor + solves ------------------------ */
+/* factor rows X (lane j, depth-indexed) in place; writes L rows to LDS L[][]
+ * and the diagonal to LDS Dk[]; returns 1/D_j */
+__device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP]) {
+  EnvL* L = c.L;
+  const int j = c.l;
+  for (int k = c.nv - 1; k >= 0; k--) {
+    const int dk = c.m->dof_depth[k];
+    if (j == k) {
+      float Dkv = 0.f;
+#pragma unroll
+      for (int e = 0; e < CAP; e++)
+        if (e == dk) Dkv = X[e];
+      Dkv = fmaxf(Dkv, MINVAL);
+      float inv = 1.0f / Dkv;
+#pragma unroll
+      for (int e = 0; e < CAP; e++) {
+        if (e < dk) X[e] = X[e] * inv;
+        L->L[k][e] = X[e];
+      }
+      L->Dk[k] = Dkv;
+    }
+    tsync();
+    if ((c.desc >> k) & 1u) {
+      float Dkv = L->Dk[k];
+      float lk = L->L[k][c.ddep];  /* L(k, j) */
+      float t = lk * Dkv;           /* = M(k, j) after Schur updates */
+#pragma unroll
+      for (int e = 0; e < CAP; e++)
+        if (e <= c.ddep) X[e] -= t * L->L[k][e];
+    }
+  }
+  float D = 1.f;
+#pragma unroll
+  for (int e = 0; e < CAP; e++)
+    if (e == c.ddep) D = X[e];
+  D = fmaxf(D, MINVAL);
+  tsync();
+  return 1.0f / D;
+}
+
+/* x <- (L'DL)^-1 x, x held by dof lanes */
+__device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
+  EnvL* L = c.L;
+  for (int k = c.nv - 1; k >= 0; k--) {
+    float xk = tsh(x, k);
+    if ((c.desc >> k) & 1u) x -= L->L[k][c.ddep] * xk;
+  }
+  x *= Dinv;
+  for (int e = 0; e < c.maxdd - 1; e++) {
+    int a = e <= c.ddep ? ancof(c, e) : 0;
+    float xa = tsh(x, a);
+    if (e < c.ddep) x -= L->L[c.l][e] * xa;
+  }
+  return x;
+}
+
+/* y = M x (M rows in LDS), x in dof lanes; uses vec[slot] */
+__device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
+  EnvL* L = c.L;
+  const int j = c.l;
+  if (j < 32) L->vec[slot][j] = x;
+  tsync();
+  float y = 0.f;
+  if (j < c.nv) {
+#pragma unroll
+    for (int e = 0; e < CAP; e++)
+      if (e <= c.ddep) y += L->M[j][e] * L->vec[slot][ancof(c, e)];
+    uint32_t dm = c.desc;
+    while (dm) {
+      int k = __ffs(dm) - 1;
+      dm &= dm - 1;
+      y += L->M[k][c.ddep] * L->vec[slot][k];
+    }
+  }
+  tsync();
+  return y;
+}
+
+/* chain gather: sum_e Jc[e] * vec[slot][anc_e] for a contact row */
+__device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) {
+  float v = 0.f;
+#pragma unroll
+  for (int e = 0; e < CAP; e++)
+    if (e <= r.kdep) v += c.L->J[c.l][e] * c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
+  return v;
+}
+
+/* ----------------------------------- RNE ----------------------------------- */
+/* cvel (lane b), cdofdot (LDS). Requires vec[V_QVEL]. */
+__device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
+  const ZbModel* m = c.m;
+  EnvL* L = c.L;
+  const int j = c.l;
+  if (j < c.nv) {
+    int bj = c.dbody;
+    int jt = m->body_jnttype[bj];
+    int k0 = j - m->body_dofadr[bj];
+    int cap = c.ddep;                       /* hinge: before own contribution */
+    if (jt == ZB_JNT_FREE) cap = c.ddep - k0 + 3; /* free rot: after the translations */
+    float acc[6] = {0, 0, 0, 0, 0, 0}, before[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < CAP; e++) {
+      if (e == cap) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) before[k] = acc[k];
+      }
+      if (e <= c.ddep) {
+        int a = ancof(c, e);
+        float qv = L->vec[V_QVEL][a];
+#pragma unroll
+        for (int k = 0; k < 6; k++) acc[k] += L->cdof[a][k] * qv;
+      }
+    }
+    float cdd[6] = {0, 0, 0, 0, 0, 0};
+    if (!(jt == ZB_JNT_FREE && k0 < 3)) {
+      float cd[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) cd[k] = L->cdof[j][k];
+      cross_motion(cdd, before, cd);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      L->cdofdot[j][k] = cdd[k];
+      L->sub[j][k] = acc[k];
+    }
+  }
+  tsync();
+#pragma unroll
+  for (int k = 0; k < 6; k++) B.cv[k] = 0.f;
+  if (c.l < c.nb && c.blast >= 0) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) B.cv[k] = L->sub[c.blast][k];
+  }
+  tsync();
+}
+
+/* cacc per body (lane b) with or without qacc (vec[V_QACC]) */
+__device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc) {
+  const ZbModel* m = c.m;
+  EnvL* L = c.L;
+  const int j = c.l;
+  if (j < c.nv) {
+    float acc[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
+#pragma unroll
+    for (int e = 0; e < CAP; e++) {
+      if (e <= c.ddep) {
+        int a = ancof(c, e);
+        float qv = L->vec[V_QVEL][a];
+#pragma unroll
+        for (int k = 0; k < 6; k++) acc[k] += L->cdofdot[a][k] * qv;
+        if (with_acc) {
+          float qa = L->vec[V_QACC][a];
+#pragma unroll
+          for (int k = 0; k < 6; k++) acc[k] += L->cdof[a][k] * qa;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) L->sub[j][k] = acc[k];
+  }
+  tsync();
+  ca[0] = ca[1] = ca[2] = 0.f;
+  ca[3] = -m->gravity[0]; ca[4] = -m->gravity[1]; ca[5] = -m->gravity[2];
+  if (c.l < c.nb && c.blast >= 0) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) ca[k] = L->sub[c.blast][k];
+  }
+  tsync();
+}
+
+/* body force cfrc (lane b) -> subtree sums in sub[] ; returns dof projection cdof_j . sub[body(j)] */
+__device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const float ca[6], const float fext[6]) {
+  EnvL* L = c.L;
+  float f[6];
+  if (c.l >= 1 && c.l < c.nb) {
+    float f1[6], t[6], f2[6];
+    mul_inert_vec(f1, B.ci, ca);
+    mul_inert_vec(t, B.ci, B.cv);
+    cross_force(f2, B.cv, t);
+#pragma unroll
+    for (int k = 0; k < 6; k++) f[k] = f1[k] + f2[k] - fext[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; k++) f[k] = 0.f;
+  }
+  subtree_sum<6>(c, f);
+  float r = 0.f;
+  if (c.l < c.nv) {
+    float cd[6], fs[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      cd[k] = L->cdof[c.l][k];
+      fs[k] = L->sub[c.dbody][k];
+    }
+    r = dot6(cd, fs);
+  }
+  tsync();
+  return r;
+}
+
+/* --------------------------- constraint model ------------------------------ */
+__device__ __forceinline__ float impedance(const float* si, float xabs) {
+  float dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
+  float imp;
+  if (width <= MINVAL || xabs >= width) {
+    imp = dmax;
+  } else {
+    float x = xabs / width, y;
+    if (power == 1.f) y = x;
+    else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
+    else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
+    imp = dmin + y * (dmax - dmin);
+  }
+  return fminf(fmaxf(imp, MINIMP), MAXIMP);
+}
+__device__ __forceinline__ void row_params(const float* solref, const float* solimp, float pos, float dA, float vel,
+                                           float dt, float& D, float& R, float& aref) {
+  float tc = fmaxf(solref[0], 2.f * dt), dr = solref[1], dmax = solimp[1];
+  float bb = 2.f / (dmax * tc);
+  float kk = 1.f / (dmax * dmax * tc * tc * dr * dr);
+  float imp = impedance(solimp, fabsf(pos));
+  R = fmaxf((1.f - imp) / imp * dA, MINVAL);
+  D = 1.f / R;
+  aref = -bb * vel - kk * imp * pos;
+}
+
+/* collision + contact rows (lane r) + dof rows (lane j) */
+__device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
+                                 Rows& r) {
+  const ZbModel* m = c.m;
+  const ZbEnvConfig* cfg = c.cfg;
+  EnvL* L = c.L;
+  const int l = c.l;
+  /* ---- contact rows: lane = 16*geom + 4*corner + edge ---- */
+  const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
+  const bool gvalid = g < c.ngeom;
+  const int gb = gvalid ? m->geom_body[g] : 0;
+  float R[9], xp[3];
+#pragma unroll
+  for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], gb);
+#pragma unroll
+  for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
+  int kd = gvalid ? m->body_lastdof[gb] : 0;
+  if (kd < 0) kd = 0;
+  r.ka0 = (uint32_t)tshi((int)c.anc0, kd);
+  r.ka1 = (uint32_t)tshi((int)c.anc1, kd);
+  r.ka2 = (uint32_t)tshi((int)c.anc2, kd);
+  r.kdep = tshi(c.ddep, kd);
+  r.kd = kd;
+  r.ex = false;
+  r.geom = g;
+  r.act = 0;
+  r.f = 0.f;
+  r.jar = 0.f;
+  r.Jv = 0.f;
+  r.D = 0.f;
+  r.aref = 0.f;
+  float Jc[CAP];
+#pragma unroll
+  for (int e = 0; e < CAP; e++) Jc[e] = 0.f;
+  if (gvalid) {
+    float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]}, t[3];
+    float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]}, gR0[9], gR[9];
+    mulmv3(t, R, gp);
+    float gpos[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
+    quat2mat(gR0, gq);
+    mulmm3(gR, R, gR0);
+    float loc[3] = {(corner & 1) ? m->geom_size[g][0] : -m->geom_size[g][0],
+                    (corner & 2) ? m->geom_size[g][1] : -m->geom_size[g][1], -m->geom_size[g][2]};
+    mulmv3(t, gR, loc);
+    float p[3] = {gpos[0] + t[0], gpos[1] + t[1], gpos[2] + t[2]};
+    float dist = p[2];
+    if (dist < m->floor_margin) {
+      r.ex = true;
+      r.pos[0] = p[0]; r.pos[1] = p[1]; r.pos[2] = p[2] - 0.5f * dist;
+      float mu = m->floor_friction[0] * s.floor_mu;
+      float sg = (edge & 1) ? -mu : mu;
+      /* frame of mju_makeFrame(+z): t1 = +y, t2 = -x */
+      if (edge < 2) { r.dir[0] = 0.f; r.dir[1] = sg; r.dir[2] = 1.f; }
+      else { r.dir[0] = -sg; r.dir[1] = 0.f; r.dir[2] = 1.f; }
+      float off[3] = {r.pos[0] - cm[0], r.pos[1] - cm[1], r.pos[2] - cm[2]}, sa[3];
+      cross3(sa, off, r.dir);
+      float vel = 0.f;
+#pragma unroll
+      for (int e = 0; e < CAP; e++) {
+        if (e <= r.kdep) {
+          int a = anc_packed(r.ka0, r.ka1, r.ka2, e);
+          float v = sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
+                    r.dir[0] * L->cdof[a][3] + r.dir[1] * L->cdof[a][4] + r.dir[2] * L->cdof[a][5];
+          Jc[e] = v;
+          vel += v * L->vec[V_QVEL][a];
+        }
+      }
+      float dA = m->body_invweight0[gb][0] * (1.f + mu * mu);
+      float Rr;
+      row_params(m->floor_solref, m->floor_solimp, dist, dA, vel, cfg->dt, r.D, Rr, r.aref);
+    }
+  }
+  /* compaction list of existing contact rows */
+  uint64_t bal = __ballot(r.ex);
+  uint32_t tb = (uint32_t)(bal >> ((threadIdx.x & 63) & ~(TEAM - 1)));
+  if (TEAM < 64) tb &= 0xffffffffu;
+  r.nrow = __popc(tb);
+  if (r.ex) {
+    int idx = __popc(tb & ((1u << l) - 1u));
+    L->rowlist[idx] = l;
+#pragma unroll
+    for (int e = 0; e < CAP; e++) L->J[l][e] = Jc[e];
+  }
+  /* ---- dof rows (lane j) ---- */
+  r.hf = r.hlo = r.hhi = false;
+  r.actf = r.actlo = r.acthi = 0;
+  r.ff = r.flo = r.fhi = 0.f;
+  r.jf = r.jlo = r.jhi = 0.f;
+  r.Df = r.Dlo = r.Dhi = 0.f;
+  r.af = r.alo = r.ahi = 0.f;
+  r.Rf = 0.f;
+  r.fl = 0.f;
+  if (l < c.nv) {
+    float v = ls.v;
+    float dA = m->dof_invweight0[l];
+    if (ls.floss > 0.f) {
+      r.hf = true;
+      r.fl = ls.floss;
+      row_params(m->dof_solref, m->dof_solimp, 0.f, dA, v, cfg->dt, r.Df, r.Rf, r.af);
+    }
+    if (m->dof_limited[l]) {
+      float dlo = ls.q - m->dof_range[l][0], dhi = m->dof_range[l][1] - ls.q, Rt;
+      if (dlo < 0.f) {
+        r.hlo = true;
+        row_params(m->dof_solref, m->dof_solimp, dlo, dA, v, cfg->dt, r.Dlo, Rt, r.alo);
+      }
+      if (dhi < 0.f) {
+        r.hhi = true;
+        row_params(m->dof_solref, m->dof_solimp, dhi, dA, -v, cfg->dt, r.Dhi, Rt, r.ahi);
+      }
+    }
+  }
+  tsync();
+}
+
+/* ------------------------------ Newton solver ------------------------------ */
+__device__ __forceinline__ float eval_fric(float jar, float D, float R, float fl, float& force, int& act) {
+  float Rf = R * fl;
+  if (jar <= -Rf) { force = fl; act = 0; return -fl * (0.5f * Rf + jar); }
+  if (jar >= Rf) { force = -fl; act = 0; return fl * (jar - 0.5f * Rf); }
+  force = -D * jar; act = 1; return 0.5f * D * jar * jar;
+}
+__device__ __forceinline__ float eval_one(float jar, float D, float& force, int& act) {
+  if (jar < 0.f) { force = -D * jar; act = 1; return 0.5f * D * jar * jar; }
+  force = 0.f; act = 0; return 0.f;
+}
+
+/* row costs at given jar values (no state change) */
+__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jlo_, float jhi_) {
+  float cost = 0.f, f;
+  int a;
+  if (r.ex) cost += eval_one(jc, r.D, f, a);
+  if (r.hf) cost += eval_fric(jf_, r.Df, r.Rf, r.fl, f, a);
+  if (r.hlo) cost += eval_one(jlo_, r.Dlo, f, a);
+  if (r.hhi) cost += eval_one(jhi_, r.Dhi, f, a);
+  return cost;
+}
+
+/* forces/activity at current jar, qfrc_constraint, grad, total cost */
+__device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float qacc, float qs, float fs, float Ma, float& grad) {
+  EnvL* L = c.L;
+  float cost = 0.f;
+  if (c.l < c.nv) cost += 0.5f * (Ma - fs) * (qacc - qs);
+  if (r.ex) cost += eval_one(r.jar, r.D, r.f, r.act);
+  if (r.hf) cost += eval_fric(r.jf, r.Df, r.Rf, r.fl, r.ff, r.actf);
+  if (r.hlo) cost += eval_one(r.jlo, r.Dlo, r.flo, r.actlo);
+  if (r.hhi) cost += eval_one(r.jhi, r.Dhi, r.fhi, r.acthi);
+  if (r.ex) {
+    L->rowF[c.l] = r.f;
+    L->rowDA[c.l] = r.act ? r.D : 0.f;
+  }
+  tsync();
+  float qc = 0.f;
+  if (c.l < c.nv) {
+    for (int i = 0; i < r.nrow; i++) {
+      int row = L->rowlist[i];
+      float fr = L->rowF[row];
+      /* is this dof on the row's chain? rows of one geom share a chain */
+      if (fr != 0.f) {
+        int g = row >> 4;
+        int kdr = c.m->body_lastdof[c.m->geom_body[g]];
+        if (kdr == c.l || ((c.desc >> kdr) & 1u)) qc += L->J[row][c.ddep] * fr;
+      }
+    }
+    if (r.hf) qc += r.ff;
+    if (r.hlo) qc += r.flo;
+    if (r.hhi) qc -= r.fhi;
+  }
+  grad = Ma - fs - qc;
+  return tsum(cost);
+}
+
+/* H = M + J' D_active J rows (depth-indexed), then factor -> Dinv */
+__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
+  EnvL* L = c.L;
+  float H[CAP];
+#pragma unroll
+  for (int e = 0; e < CAP; e++) H[e] = (c.l < c.nv) ? L->M[c.l][e] : 0.f;
+  if (c.l < c.nv) {
+    for (int i = 0; i < r.nrow; i++) {
+      int row = L->rowlist[i];
+      float da = L->rowDA[row];
+      if (da != 0.f) {
+        int g = row >> 4;
+        int kdr = c.m->body_lastdof[c.m->geom_body[g]];
+        if (kdr == c.l || ((c.desc >> kdr) & 1u)) {
+          float jj = da * L->J[row][c.ddep];
+#pragma unroll
+          for (int e = 0; e < CAP; e++)
+            if (e <= c.ddep) H[e] += jj * L->J[row][e];
+        }
+      }
+    }
+    float dd = 0.f;
+    if (r.hf && r.actf) dd += r.Df;
+    if (r.hlo && r.actlo) dd += r.Dlo;
+    if (r.hhi && r.acthi) dd += r.Dhi;
+#pragma unroll
+    for (int e = 0; e < CAP; e++)
+      if (e == c.ddep) H[e] += dd;
+  }
+  tsync();
+  return factor_ldl(c, H);
+}
+
+/* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
+__device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float& Mv) {
+  const ZbEnvConfig* cfg = c.cfg;
+  EnvL* L = c.L;
+  Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
+  r.Jv = r.ex ? row_dot(c, r, V_TMP) : 0.f;
+  tsync();
+  float c1 = tsum(c.l < c.nv ? search * (Ma - fs) : 0.f);
+  float c2 = tsum(c.l < c.nv ? search * Mv : 0.f);
+  auto eval = [&](float alpha, float& d1, float& d2) {
+    float g1 = 0.f, g2 = 0.f;
+    if (r.ex && r.Jv != 0.f) {
+      float x = r.jar + alpha * r.Jv;
+      if (x < 0.f) { g1 += r.D * x * r.Jv; g2 += r.D * r.Jv * r.Jv; }
+    }
+    if (c.l < c.nv && search != 0.f) {
+      float jv = search;
+      if (r.hf) {
+        float x = r.jf + alpha * jv, Rf = r.Rf * r.fl;
+        if (x <= -Rf) g1 -= r.fl * jv;
+        else if (x >= Rf) g1 += r.fl * jv;
+        else { g1 += r.Df * x * jv; g2 += r.Df * jv * jv; }
+      }
+      if (r.hlo) {
+        float x = r.jlo + alpha * jv;
+        if (x < 0.f) { g1 += r.Dlo * x * jv; g2 += r.Dlo * jv * jv; }
+      }
+      if (r.hhi) {
+        float x = r.jhi - alpha * jv;
+        if (x < 0.f) { g1 += r.Dhi * x * (-jv); g2 += r.Dhi * jv * jv; }
+      }
+    }
+    d1 = c1 + alpha * c2 + tsum(g1);
+    d2 = c2 + tsum(g2);
+  };
+  float d1, d2;
+  eval(0.f, d1, d2);
+  if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
+  float gtol = cfg->ls_tolerance * (-d1);
+  float lo = 0.f, hi = -1.f;
+  float alpha = -d1 / d2;
+  for (int it = 0; it < cfg->ls_iterations; it++) {
+    eval(alpha, d1, d2);
+    if (fabsf(d1) <= gtol) break;
+    if (d1 < 0.f) lo = alpha; else hi = alpha;
+    float an = alpha - d1 / d2;
+    if (!(an > lo) || (hi >= 0.f && !(an < hi))) an = 0.5f * (lo + (hi >= 0.f ? hi : 2.f * alpha));
+    alpha = an;
+  }
+  return alpha;
+}
+
+/* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
+__device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters) {
+  const ZbEnvConfig* cfg = c.cfg;
+  const ZbModel* m = c.m;
+  EnvL* L = c.L;
+  /* warmstart selection */
+  float x = w;
+  float Ma = mul_m(c, x, V_TMP);
+  if (c.l < 32) { L->vec[V_TMP][c.l] = x; L->vec[V_TMP2][c.l] = qs; }
+  tsync();
+  float jw = r.ex ? row_dot(c, r, V_TMP) - r.aref : 0.f;
+  float js = r.ex ? row_dot(c, r, V_TMP2) - r.aref : 0.f;
+  tsync();
+  float cw = tsum((c.l < c.nv ? 0.5f * (Ma - fs) * (x - qs) : 0.f) +
+                  rows_cost(c, r, jw, x - r.af, x - r.alo, -x - r.ahi));
+  float cs = tsum(rows_cost(c, r, js, qs - r.af, qs - r.alo, -qs - r.ahi));
+  if (cw > cs) {
+    x = qs;
+    Ma = mul_m(c, x, V_TMP);
+    r.jar = js;
+  } else {
+    r.jar = jw;
+  }
+  r.jf = x - r.af;
+  r.jlo = x - r.alo;
+  r.jhi = -x - r.ahi;
+  float scale = 1.0f / (m->meaninertia * (float)(c.nv > 1 ? c.nv : 1));
+  float grad;
+  float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
+  float Dinv = hessian_factor(c, r);
+  float search = -solve_ldl(c, grad, Dinv);
+  int it = 0;
+  while (it < cfg->iterations) {
+    float Mv;
+    float alpha = line_search(c, r, search, Ma, fs, Mv);
+    if (alpha == 0.f) break;
+    x += alpha * search;
+    Ma += alpha * Mv;
+    r.jar += alpha * r.Jv;
+    r.jf += alpha * search;
+    r.jlo += alpha * search;
+    r.jhi -= alpha * search;
+    float oldcost = cost;
+    cost = update_constraint(c, r, x, qs, fs, Ma, grad);
+    Dinv = hessian_factor(c, r);
+    float mg = solve_ldl(c, grad, Dinv);
+    it++;
+    float improvement = scale * (oldcost - cost);
+    float gradient = scale * sqrtf(tsum(c.l < c.nv ? grad * grad : 0.f));
+    if (improvement < cfg->tolerance || gradient < cfg->tolerance) break;
+    search = -mg;
+  }
+  iters += it;
+  return x;
+}
+
+/* ----------------------------- Feetech actuator ---------------------------- */
+/* trapezoidal_step (train.py:1137-1196) + duty/torque (train.py:1260-1269) */
+__device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
+  const ZbModel* m = c.m;
+  if (c.act < 0) { ls.ctrl = 0.f; return; }
+  const int a = c.act;
+  const float dt = c.cfg->dt;
+  float pos = ls.pp, vel = ls.pv, tgt = ls.tgt;
+  float err = tgt - pos;
+  bool in_db = fabsf(err) <= DEADBAND;
+  float db_vel = vel * 0.8f;
+  float db_pos = pos + db_vel * dt;
+  float tdir = (float)((err > 0.f) - (err < 0.f));
+  float amax = m->fe_amax[a], vmax = m->fe_vmax[a];
+  float stop = fabsf(vel * vel) / (2.f * amax);
+  float vdir = (float)((vel > 0.f) - (vel < 0.f));
+  bool towards = vdir * tdir >= 0.f;
+  bool accel = towards && fabsf(err) > stop;
+  float acc = accel ? tdir * amax : -vdir * amax;
+  if (fabsf(vel) < 1e-6f) acc = tdir * amax;
+  float pv = vel + acc * dt;
+  pv = fminf(fmaxf(pv, -vmax), vmax);
+  float pp = pos + pv * dt;
+  float npos = in_db ? db_pos : pp, nvel = in_db ? db_vel : pv;
+  float perr = npos - ls.q, verr = nvel - ls.v;
+  float duty = m->fe_kp[a] * m->fe_error_gain[a] * perr + m->fe_kd[a] * verr;
+  duty = fminf(fmaxf(duty, -m->fe_max_pwm[a]), m->fe_max_pwm[a]);
+  float tau = duty * m->fe_vin[a] * m->fe_kt[a] / m->fe_R[a];
+  ls.pp = npos;
+  ls.pv = nvel;
+  ls.ptau = tau;
+  ls.ctrl = tau;
+}
+
+/* ------------------------------- full forward ------------------------------ */
+/* mj_forward (+ sensors if requested). Leaves qacc in ls.qacc, kinematics in B. */
+__device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
+                                        Sensors& sen, int& iters) {
+  const ZbModel* m = c.m;
+  EnvL* L = c.L;
+  kinematics(c, s, ls, B);
+  float cm[3];
+  com_crb_m(c, s, ls, B, cm);
+  /* factor M (copy of rows) */
+  float X[CAP];
+#pragma unroll
+  for (int e = 0; e < CAP; e++) X[e] = (c.l < c.nv) ? L->M[c.l][e] : 0.f;
+  float DinvM = factor_ldl(c, X);
+  /* velocities */
+  if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < c.nv ? ls.v : 0.f;
+  tsync();
+  com_vel(c, B);
+  float ca[6], zero6[6] = {0, 0, 0, 0, 0, 0};
+  com_acc(c, ca, false);
+  float bias = rne_project(c, B, ca, zero6);
+  /* actuation + passive -> qfrc_smooth, qacc_smooth */
+  float act = 0.f;
+  if (c.act >= 0) {
+    float ct = fminf(fmaxf(ls.ctrl, m->act_ctrlrange[c.act][0]), m->act_ctrlrange[c.act][1]);
+    ls.actforce = m->act_gear[c.act] * ct;
+    act = m->act_gear[c.act] * ls.actforce;
+  } else {
+    ls.actforce = 0.f;
+  }
+  float fs = (c.l < c.nv) ? (-ls.damp * ls.v - bias + act) : 0.f;
+  float qs = solve_ldl(c, fs, DinvM);
+  /* constraints */
+  make_constraints(c, s, ls, B, cm, r);
+  int nrows = tmaxi(r.nrow + (r.hf || r.hlo || r.hhi ? 1 : 0));
+  float qacc;
+  if (nrows == 0) {
+    qacc = qs;
+  } else {
+    qacc = solve_newton(c, r, qs, fs, ls.w, iters);
+  }
+  ls.qacc = (c.l < c.nv) ? qacc : 0.f;
+  if (!with_sensors) return;
+  /* ------------------- sensors (mj_rnePostConstraint etc.) ------------------ */
+  if (c.l < 32) L->vec[V_QACC][c.l] = ls.qacc;
+  tsync();
+  /* contact forces per geom -> cfrc_ext on the geom body, touch */
+  float fext[6] = {0, 0, 0, 0, 0, 0};
+  sen.touch[0] = sen.touch[1] = 0.f;
+  for (int g = 0; g < c.ngeom; g++) {
+    bool mine = r.ex && r.geom == g;
+    float F[3] = {0, 0, 0}, tq[3] = {0, 0, 0};
+    float fn = 0.f;
+    if (mine) {
+      F[0] = r.f * r.dir[0]; F[1] = r.f * r.dir[1]; F[2] = r.f * r.dir[2];
+      float off[3] = {r.pos[0] - cm[0], r.pos[1] - cm[1], r.pos[2] - cm[2]};
+      cross3(tq, off, F);
+      fn = r.f;
+    }
+    float ext[6] = {tsum(tq[0]), tsum(tq[1]), tsum(tq[2]), tsum(F[0]), tsum(F[1]), tsum(F[2])};
+    float fnt = tsum(fn);
+    if (c.l == m->geom_body[g]) {
+#pragma unroll
+      for (int k = 0; k < 6; k++) fext[k] += ext[k];
+    }
+    if (g == m->geom_left_foot) sen.touch[0] = fnt;
+    if (g == m->geom_right_foot) sen.touch[1] = fnt;
+  }
+  float cacc[6];
+  com_acc(c, cacc, true);
+  /* cfrc_int subtree sums (in sub[]) */
+  (void)rne_project(c, B, cacc, fext);
+  /* imu site: framequat, gyro, accelerometer */
+  {
+    int sb = m->site_body[m->site_imu];
+    float xq[4], xp[3], R[9], cv[6], cc[6];
+#pragma unroll
+    for (int k = 0; k < 4; k++) xq[k] = tsh(B.xq[k], sb);
+#pragma unroll
+    for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], sb);
+#pragma unroll
+    for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], sb);
+#pragma unroll
+    for (int k = 0; k < 6; k++) { cv[k] = tsh(B.cv[k], sb); cc[k] = tsh(cacc[k], sb); }
+    float sq[4];
+    quat_mul(sq, xq, s.imu_q);
+#pragma unroll
+    for (int k = 0; k < 4; k++) sen.fq[k] = sq[k];
+    float sR[9], t[3];
+    quat2mat(sR, sq);
+    mulmv3(t, R, s.imu_p);
+    float sp[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
+    float dif[3] = {sp[0] - cm[0], sp[1] - cm[1], sp[2] - cm[2]};
+    mulmtv3(sen.gyro, sR, cv);
+    float v[3], a[3];
+    cross3(t, cv, dif);
+    for (int k = 0; k < 3; k++) v[k] = cv[3 + k] + t[k];
+    cross3(t, cc, dif);
+    for (int k = 0; k < 3; k++) a[k] = cc[3 + k] + t[k];
+    cross3(t, cv, v);
+    for (int k = 0; k < 3; k++) a[k] += t[k];
+    mulmtv3(sen.acc, sR, a);
+  }
+  /* foot force sensors: cfrc_int of the site body, site frame */
+  {
+    int fs_[2] = {m->site_left_foot, m->site_right_foot};
+    for (int side = 0; side < 2; side++) {
+      int ss = fs_[side], sb = m->site_body[ss];
+      float F[3] = {L->sub[sb][3], L->sub[sb][4], L->sub[sb][5]};
+      float xq[4], sq[4], sR[9];
+#pragma unroll
+      for (int k = 0; k < 4; k++) xq[k] = tsh(B.xq[k], sb);
+      float sqm[4] = {m->site_quat[ss][0], m->site_quat[ss][1], m->site_quat[ss][2], m->site_quat[ss][3]};
+      quat_mul(sq, xq, sqm);
+      quat2mat(sR, sq);
+      mulmtv3(&sen.force[3 * side], sR, F);
+    }
+  }
+  tsync();
+}
+
+/* ------------------------------ Euler integrate ----------------------------- */
+__device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls) {
+  const float dt = c.cfg->dt;
+  float vn = ls.v + dt * ls.qacc;
+  float v0 = tsh(vn, 0), v1 = tsh(vn, 1), v2 = tsh(vn, 2), w0 = tsh(vn, 3), w1 = tsh(vn, 4), w2 = tsh(vn, 5);
+  if (c.l < c.nv) {
+    ls.w = ls.qacc; /* mj_advance: qacc_warmstart */
+    ls.v = vn;
+    if (c.qadr >= 0) ls.q += dt * vn;
+  }
+  /* free joint (root): world-frame translation, body-frame rotation */
+  if (c.m->body_jnttype[1] == ZB_JNT_FREE) {
+    s.bp[0] += dt * v0; s.bp[1] += dt * v1; s.bp[2] += dt * v2;
+    float w[3] = {w0, w1, w2};
+    float nw = sqrtf(dot3(w, w));
+    if (nw > MINVAL) {
+      float ax[3] = {w[0] / nw, w[1] / nw, w[2] / nw}, qr[4], qn[4];
+      axis_angle_quat(qr, ax, nw * dt);
+      quat_mul(qn, s.bq, qr);
+#pragma unroll
+      for (int k = 0; k < 4; k++) s.bq[k] = qn[k];
+    }
+    quat_normalize(s.bq);
+  }
+}
+
+/* --------------------------- env-level (ksim) logic ------------------------- */
+__device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, const float* rnd) {
+  const ZbModel* m = c.m;
+  const bool rz = (c.cfg->flags & ZB_F_RANDOMIZE) && rnd;
+  const int l = c.l;
+  ls.mscale = (rz && l < c.nb) ? rnd[ZB_R_MASS + l] : 1.f;
+  ls.arm = ls.damp = ls.floss = 0.f;
+  ls.q0 = 0.f;
+  if (l < c.nv) {
+    ls.arm = m->dof_armature[l] * (rz ? rnd[ZB_R_ARMATURE + l] : 1.f);
+    ls.damp = m->dof_damping[l] * (rz ? rnd[ZB_R_DAMPING + l] : 1.f);
+    ls.floss = m->dof_frictionloss[l] * (rz ? rnd[ZB_R_FRICTION + l] : 1.f);
+    if (c.qadr >= 0) ls.q0 = m->qpos0[c.qadr] + ((rz && c.act >= 0) ? rnd[ZB_R_QPOS0 + c.act] : 0.f);
+  }
+  s.floor_mu = rz ? rnd[ZB_R_FLOOR_MU] : 1.f;
+  int si = m->site_imu;
+  float sq[4] = {m->site_quat[si][0], m->site_quat[si][1], m->site_quat[si][2], m->site_quat[si][3]};
+#pragma unroll
+  for (int k = 0; k < 3; k++) s.imu_p[k] = m->site_pos[si][k] + (rz ? rnd[ZB_R_IMU_POS + k] : 0.f);
+  if (rz) {
+    float rq[4] = {rnd[ZB_R_IMU_QUAT], rnd[ZB_R_IMU_QUAT + 1], rnd[ZB_R_IMU_QUAT + 2], rnd[ZB_R_IMU_QUAT + 3]}, o[4];
+    quat_mul(o, sq, rq);
+#pragma unroll
+    for (int k = 0; k < 4; k++) sq[k] = o[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) s.imu_q[k] = sq[k];
+}
+
+/* randomizer sampling (must match oracle/zb_oracle.c sample_rand) */
+__device__ __forceinline__ void sample_rand(const Ctx& c, uint32_t episode, float* rnd) {
+  const ZbEnvConfig* cfg = c.cfg;
+  const int l = c.l;
+  for (int k = l; k < 75; k += TEAM) {
+    float u0, u1;
+    uniform2(c.seed, P_RAND, (uint32_t)k, c.env, episode, u0, u1);
+    float lo, hi;
+    int base;
+    if (k < 16) { lo = cfg->rand_mass[0]; hi = cfg->rand_mass[1]; base = ZB_R_MASS + 2 * k; }
+    else if (k < 32) { lo = cfg->rand_armature[0]; hi = cfg->rand_armature[1]; base = ZB_R_ARMATURE + 2 * (k - 16); }
+    else if (k < 48) { lo = cfg->rand_damping[0]; hi = cfg->rand_damping[1]; base = ZB_R_DAMPING + 2 * (k - 32); }
+    else if (k < 64) { lo = cfg->rand_friction[0]; hi = cfg->rand_friction[1]; base = ZB_R_FRICTION + 2 * (k - 48); }
+    else if (k < 74) { lo = cfg->rand_qpos0[0]; hi = cfg->rand_qpos0[1]; base = ZB_R_QPOS0 + 2 * (k - 64); }
+    else { lo = cfg->rand_floor_mu[0]; hi = cfg->rand_floor_mu[1]; base = ZB_R_FLOOR_MU; }
+    rnd[base] = lo + (hi - lo) * u0;
+    if (k < 74) rnd[base + 1] = lo + (hi - lo) * u1;
+  }
+  if (l == 0) {
+    float z00, z01, z10, z11, z20, z21;
+    normal2(c.seed, P_RAND, 75u, c.env, episode, z00, z01);
+    normal2(c.seed, P_RAND, 76u, c.env, episode, z10, z11);
+    normal2(c.seed, P_RAND, 77u, c.env, episode, z20, z21);
+    float rv[3] = {cfg->rand_imu_tilt_std * z00, cfg->rand_imu_tilt_std * z01, cfg->rand_imu_yaw_std * z10};
+    float ang = sqrtf(dot3(rv, rv)), q[4] = {1.f, 0.f, 0.f, 0.f};
+    if (ang > MINVAL) {
+      float ax[3] = {rv[0] / ang, rv[1] / ang, rv[2] / ang};
+      axis_angle_quat(q, ax, ang);
+    }
+    for (int k = 0; k < 4; k++) rnd[ZB_R_IMU_QUAT + k] = q[k];
+    rnd[ZB_R_IMU_POS + 0] = cfg->rand_imu_pos_std * z11;
+    rnd[ZB_R_IMU_POS + 1] = cfg->rand_imu_pos_std * z20;
+    rnd[ZB_R_IMU_POS + 2] = cfg->rand_imu_pos_std * z21;
+    for (int k = ZB_R_END; k < ZB_RAND_STRIDE; k++) rnd[k] = 0.f;
+  }
+}
+
+/* rotate_quat_by_quat (train.py:751-787) */
+__device__ __forceinline__ void rotate_quat_by_quat(const float q_[4], const float r_[4], bool inverse, float out[4]) {
+  const float eps = 1e-6f;
+  float n1 = sqrtf(q_[0] * q_[0] + q_[1] * q_[1] + q_[2] * q_[2] + q_[3] * q_[3]) + eps;
+  float n2 = sqrtf(r_[0] * r_[0] + r_[1] * r_[1] + r_[2] * r_[2] + r_[3] * r_[3]) + eps;
+  float a[4] = {r_[0] / n2, r_[1] / n2, r_[2] / n2, r_[3] / n2};
+  float b[4] = {q_[0] / n1, q_[1] / n1, q_[2] / n1, q_[3] / n1};
+  if (inverse) { a[1] = -a[1]; a[2] = -a[2]; a[3] = -a[3]; }
+  float r[4];
+  quat_mul(r, a, b);
+  float n = sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3]) + eps;
+  for (int k = 0; k < 4; k++) out[k] = r[k] / n;
+}
+
+/* observation assembly + obs-derived carries (train.py:1478-1537, 1624-1679) */
+__device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, const Sensors& sen, float* oa,
+                        float* oc, float* ox) {
+  const ZbModel* m = c.m;
+  const ZbEnvConfig* cfg = c.cfg;
+  const int l = c.l;
+  /* ImuOrientationObservation (heading command 0) */
+  float hq[4] = {1.f, 0.f, 0.f, 0.f}, bq[4];
+  rotate_quat_by_quat(sen.fq, hq, true, bq);
+  if (bq[0] < 0.f) for (int k = 0; k < 4; k++) bq[k] = -bq[k];
+  float imu[4];
+  for (int k = 0; k < 4; k++) {
+    float x = s.ema[k] * s.lag + bq[k] * (1.f - s.lag);
+    s.ema[k] = x;
+    imu[k] = x;
+  }
+  float acc[3] = {sen.acc[0], sen.acc[1], sen.acc[2]};
+  if (cfg->flags & ZB_F_OBS_NOISE) {
+    float z0 = 0.f, z1 = 0.f;
+    if (l < 4) normal2(c.seed, P_OBS, (uint32_t)l, c.env, s.rng_step, z0, z1);
+    float a0 = tsh(z0, 0), a1 = tsh(z1, 0), b0 = tsh(z0, 1), b1 = tsh(z1, 1);
+    float c0 = tsh(z0, 2), c1 = tsh(z1, 2), d0 = tsh(z0, 3);
+    imu[0] += cfg->imu_noise_std * a0; imu[1] += cfg->imu_noise_std * a1;
+    imu[2] += cfg->imu_noise_std * b0; imu[3] += cfg->imu_noise_std * b1;
+    acc[0] += cfg->acc_noise_std * c0; acc[1] += cfg->acc_noise_std * c1; acc[2] += cfg->acc_noise_std * d0;
+  }
+  /* feet positions in the robot frame (train.py:451-465) */
+  float bqn[4] = {s.bq[0], s.bq[1], s.bq[2], s.bq[3]}, bm[9];
+  quat_normalize(bqn);
+  quat2mat(bm, bqn);
+  float fpos[2][3];
+  {
+    int sides[2] = {m->site_left_foot, m->site_right_foot};
+    for (int sd = 0; sd < 2; sd++) {
+      int ss = sides[sd], sb = m->site_body[ss];
+      float xp[3], R[9], t[3];
+      for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], sb);
+      for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], sb);
+      float sp[3] = {m->site_pos[ss][0], m->site_pos[ss][1], m->site_pos[ss][2]};
+      mulmv3(t, R, sp);
+      float w[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
+      mulmtv3(fpos[sd], bm, w);
+    }
+  }
+  float dfx = fpos[0][0] - fpos[1][0], dfy = fpos[0][1] - fpos[1][1], dfz = fpos[0][2] - fpos[1][2];
+  s.feet_dist = sqrtf(dfx * dfx + dfy * dfy + dfz * dfz);
+  s.touch[0] = sen.touch[0];
+  s.touch[1] = sen.touch[1];
+  /* joint-space values of actuated dof lanes, fetched by output index */
+  const int jl = l < ZB_NJ ? m->act_dof[l] : 0;
+  const float qa = tsh(ls.q, jl), va = tsh(ls.v, jl), fa = tsh(ls.actforce, jl), ta = tsh(ls.ptau, jl);
+  const float acca = tsh(ls.qacc, jl);
+  float xb = tsh(B.xp[2], 1);
+  if (oa) {
+    if (l < ZB_NJ) {
+      oa[l] = qa;
+      oa[ZB_NJ + l] = va;
+    }
+    if (l < 4) oa[40 + l] = imu[l];
+    if (l >= 4 && l < 10) oa[40 + l] = 0.f;
+  }
+  if (oc) {
+    if (l < ZB_NJ) {
+      oc[l] = qa;
+      oc[ZB_NJ + l] = va / 10.f;
+      oc[457 + l] = fa / 100.f;
+    }
+    if (l >= 1 && l < c.nb) {
+      for (int k = 0; k < 10; k++) oc[40 + (l - 1) * 10 + k] = B.ci[k];
+      for (int k = 0; k < 6; k++) oc[290 + (l - 1) * 6 + k] = B.cv[k];
+    }
+    if (l < 3) oc[440 + l] = acc[l];
+    if (l < 3) oc[443 + l] = sen.gyro[l];
+    if (l < 4) oc[446 + l] = imu[l];
+    if (l < ZB_NUM_CMD) oc[450 + l] = 0.f;
+    if (l < 3) oc[477 + l] = s.bp[l];
+    if (l < 4) oc[480 + l] = s.bq[l];
+  }
+  if (ox) {
+    if (l < 6) {
+      ox[ZB_X_BASE_LINVEL + l] = ls.v;   /* qvel[0:6] (lin then ang) */
+      ox[ZB_X_BASE_LINACC + l] = ls.qacc; /* qacc[0:6] (lin then ang) */
+    }
+    if (l == 0) {
+      ox[ZB_X_BASE_HEIGHT] = xb;
+      ox[ZB_X_TOUCH] = sen.touch[0];
+      ox[ZB_X_TOUCH + 1] = sen.touch[1];
+#pragma unroll
+      for (int k = 0; k < 6; k++) ox[ZB_X_FORCE + k] = sen.force[k];
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        ox[ZB_X_FEET_POS + k] = fpos[0][k];
+        ox[ZB_X_FEET_POS + 3 + k] = fpos[1][k];
+      }
+    }
+    if (l < ZB_NJ) {
+      ox[ZB_X_FEETECH_TAU + l] = ta;
+      ox[ZB_X_ACT_ACC + l] = acca;
+    }
+    for (int i = ZB_X_END + l; i < ZB_OBS_EXTRA; i += TEAM) ox[i] = 0.f;
+  }
+}
+
+/* xax.quat_to_euler roll & pitch */
+__device__ __forceinline__ void quat_roll_pitch(const float q_[4], float& roll, float& pitch) {
+  float q[4] = {q_[0], q_[1], q_[2], q_[3]};
+  quat_normalize(q);
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  roll = atan2f(2.f * (w * x + y * z), 1.f - 2.f * (x * x + y * y));
+  float sp = fminf(fmaxf(2.f * (w * y - z * x), -1.f), 1.f);
+  pitch = asinf(sp);
+}
+
+/* terminations + reward terms (train.py:1546-1593) ; returns done */
+__device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, float cur, float* terms_out,
+                        float& total, bool& fail) {
+  const ZbModel* m = c.m;
+  const ZbEnvConfig* cfg = c.cfg;
+  const int l = c.l;
+  float z = s.bp[2];
+  float bq[4] = {s.bq[0], s.bq[1], s.bq[2], s.bq[3]};
+  quat_normalize(bq);
+  float upz = 1.f - 2.f * (bq[1] * bq[1] + bq[2] * bq[2]);
+  uint32_t steps = s.ep_steps + 1u;
+  fail = (z < cfg->bad_z[0]) || (z > cfg->bad_z[1]) || (upz < cosf(cfg->max_tilt_rad)) || !(z == z);
+  bool trunc = (float)steps * cfg->ctrl_dt >= cfg->max_episode_sec;
+  bool done = fail || trunc;
+  float t[ZB_NUM_TERMS];
+  t[ZB_T_STAY_ALIVE] = fail ? -1.f : 1.f / cfg->stay_alive_balance;
+  float xq1[4];
+  for (int k = 0; k < 4; k++) xq1[k] = tsh(B.xq[k], 1);
+  t[ZB_T_UPRIGHT] = 1.f - 2.f * (xq1[1] * xq1[1] + xq1[2] * xq1[2]);
+  float v0 = tsh(ls.v, 0), v1 = tsh(ls.v, 1), v2 = tsh(ls.v, 2);
+  t[ZB_T_NAIVE_FORWARD] = fminf(v0, cfg->naive_forward_clip_max);
+  t[ZB_T_FWD_ORIENT] = 1.f - 2.f * (xq1[2] * xq1[2] + xq1[3] * xq1[3]);
+  {
+    float bm[9], vb[3], vw[3] = {v0, v1, v2};
+    quat2mat(bm, bq);
+    mulmtv3(vb, bm, vw);
+    t[ZB_T_LINVEL_Y] = fabsf(vb[1]);
+  }
+  bool lc = s.touch[0] > cfg->touch_threshold, rc = s.touch[1] > cfg->touch_threshold;
+  t[ZB_T_SINGLE_FOOT] = (lc != rc) ? 1.f : 0.f;
+  {
+    bool cont[2] = {lc, rc};
+    float rr = 0.f;
+    for (int sd = 0; sd < 2; sd++) {
+      float air_prev = s.air[sd];
+      bool prev = s.prev_cont[sd] > 0.5f;
+      bool td = cont[sd] && !prev;
+      rr += (air_prev - cfg->feet_airtime_touchdown_penalty) * (td ? 1.f : 0.f);
+      s.air[sd] = (cont[sd] || done) ? 0.f : air_prev + cfg->ctrl_dt;
+      s.prev_cont[sd] = cont[sd] ? 1.f : 0.f;
+    }
+    t[ZB_T_FEET_AIRTIME] = rr;
+  }
+  {
+    float ql[4], qr[4];
+    for (int k = 0; k < 4; k++) {
+      ql[k] = tsh(B.xq[k], m->body_left_foot);
+      qr[k] = tsh(B.xq[k], m->body_right_foot);
+    }
+    float rl, pl, rrr, pr;
+    quat_roll_pitch(ql, rl, pl);
+    quat_roll_pitch(qr, rrr, pr);
+    float err = fabsf(rl) + fabsf(pl) + fabsf(rrr) + fabsf(pr);
+    t[ZB_T_FEET_ORIENT] = expf(-err / cfg->feet_orient_error_scale);
+  }
+  t[ZB_T_FEET_TOO_CLOSE] = s.feet_dist < cfg->feet_too_close_threshold ? 1.f : 0.f;
+  {
+    /* joint deviation penalties; group masks over ctrl index (train.py:584-640) */
+    const uint32_t straight = (1u << 7) | (1u << 6) | (1u << 1) | (1u << 0);
+    const uint32_t ankle = (1u << 9) | (1u << 10) | (1u << 11) | (1u << 3) | (1u << 4) | (1u << 5);
+    const uint32_t arm = 0xFF000u;
+    float p1 = 0.f, p2 = 0.f, p3 = 0.f;
+    if (c.act >= 0) {
+      float e = ls.q - m->joint_bias[c.act];
+      float w = m->joint_weight[c.act] * e * e;
+      if ((straight >> c.act) & 1u) p1 = w;
+      if ((ankle >> c.act) & 1u) p2 = w;
+      if ((arm >> c.act) & 1u) p3 = w;
+    }
+    t[ZB_T_STRAIGHT_LEG] = tsum(p1);
+    t[ZB_T_ANKLE_KNEE] = tsum(p2);
+    t[ZB_T_ARM_POSE] = tsum(p3);
+  }
+  total = 0.f;
+  for (int i = 0; i < ZB_NUM_TERMS; i++) {
+    float sc = cfg->reward_scale[i] * (cfg->reward_by_curriculum[i] ? cur : 1.f);
+    total += sc * t[i];
+  }
+  if (terms_out && l < ZB_NUM_TERMS) {
+    float v = 0.f;
+    for (int i = 0; i < ZB_NUM_TERMS; i++)
+      if (i == l) v = t[i];
+    terms_out[l] = v;
+  }
+  s.ep_steps = steps;
+  s.ep_ret += total;
+  return done;
+}
+
+/* ------------------------------ state I/O ---------------------------------- */
+__device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, const float* st) {
+  const int l = c.l;
+  for (int k = 0; k < 3; k++) s.bp[k] = st[ZB_S_QPOS + k];
+  for (int k = 0; k < 4; k++) s.bq[k] = st[ZB_S_QPOS + 3 + k];
+  for (int k = 0; k < 4; k++) s.ema[k] = st[ZB_S_IMU_EMA + k];
+  s.lag = st[ZB_S_IMU_LAG];
+  s.air[0] = st[ZB_S_AIRTIME]; s.air[1] = st[ZB_S_AIRTIME + 1];
+  s.push_timer = st[ZB_S_PUSH_TIMER];
+  s.touch[0] = st[ZB_S_TOUCH]; s.touch[1] = st[ZB_S_TOUCH + 1];
+  s.feet_dist = st[ZB_S_FEET_DIST];
+  s.ep_ret = st[ZB_S_EP_RETURN];
+  s.ep_steps = fbits(st[ZB_S_EP_STEPS]);
+  s.rng_step = fbits(st[ZB_S_RNG_STEP]);
+  s.prev_cont[0] = st[ZB_S_PREV_CONT]; s.prev_cont[1] = st[ZB_S_PREV_CONT + 1];
+  s.episode = fbits(st[ZB_S_EPISODE]);
+  s.nanflag = fbits(st[ZB_S_NAN]);
+  ls.q = ls.v = ls.w = 0.f;
+  ls.pp = ls.pv = ls.ptau = 0.f;
+  if (l < c.nv) {
+    ls.v = st[ZB_S_QVEL + l];
+    ls.w = st[ZB_S_QACCW + l];
+    if (c.qadr >= 0) ls.q = st[ZB_S_QPOS + c.qadr];
+  }
+  if (c.act >= 0) {
+    ls.pp = st[ZB_S_PLAN_POS + c.act];
+    ls.pv = st[ZB_S_PLAN_VEL + c.act];
+    ls.ptau = st[ZB_S_PLAN_TAU + c.act];
+  }
+  ls.ctrl = 0.f;
+  ls.qacc = 0.f;
+  ls.actforce = 0.f;
+}
+
+__device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const LaneS& ls, float* st) {
+  const int l = c.l;
+  if (l < c.nv) {
+    st[ZB_S_QVEL + l] = ls.v;
+    st[ZB_S_QACCW + l] = ls.w;
+    if (c.qadr >= 0) st[ZB_S_QPOS + c.qadr] = ls.q;
+  }
+  if (c.act >= 0) {
+    st[ZB_S_PLAN_POS + c.act] = ls.pp;
+    st[ZB_S_PLAN_VEL + c.act] = ls.pv;
+    st[ZB_S_PLAN_TAU + c.act] = ls.ptau;
+  }
+  if (l == 0) {
+    for (int k = 0; k < 3; k++) st[ZB_S_QPOS + k] = s.bp[k];
+    for (int k = 0; k < 4; k++) st[ZB_S_QPOS + 3 + k] = s.bq[k];
+    for (int k = 0; k < 4; k++) st[ZB_S_IMU_EMA + k] = s.ema[k];
+    st[ZB_S_IMU_LAG] = s.lag;
+    st[ZB_S_AIRTIME] = s.air[0]; st[ZB_S_AIRTIME + 1] = s.air[1];
+    st[ZB_S_PUSH_TIMER] = s.push_timer;
+    st[ZB_S_TOUCH] = s.touch[0]; st[ZB_S_TOUCH + 1] = s.touch[1];
+    st[ZB_S_FEET_DIST] = s.feet_dist;
+    st[ZB_S_EP_RETURN] = s.ep_ret;
+    st[ZB_S_EP_STEPS] = bitsf(s.ep_steps);
+    st[ZB_S_RNG_STEP] = bitsf(s.rng_step);
+    st[ZB_S_PREV_CONT] = s.prev_cont[0]; st[ZB_S_PREV_CONT + 1] = s.prev_cont[1];
+    st[ZB_S_EPISODE] = bitsf(s.episode);
+    st[ZB_S_NAN] = bitsf(s.nanflag);
+  }
+}
+
+/* ksim reset (train.py:1471-1476); the caller then runs mjx.forward (forward()) */
+__device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, float* rnd) {
+  const ZbModel* m = c.m;
+  const ZbEnvConfig* cfg = c.cfg;
+  const int l = c.l;
+  uint32_t episode = s.episode;
+  if ((cfg->flags & ZB_F_RANDOMIZE) && rnd) {
+    sample_rand(c, episode, rnd);
+    tsync();
+    __threadfence_block();
+  }
+  load_params(c, s, ls, rnd);
+  for (int k = 0; k < 3; k++) s.bp[k] = m->qpos0[k];
+  for (int k = 0; k < 4; k++) s.bq[k] = m->qpos0[3 + k];
+  ls.v = 0.f;
+  ls.w = 0.f;
+  if (c.act >= 0) {
+    int qa = c.qadr;
+    ls.q = m->joint_bias[c.act] + (ls.q0 - m->qpos0[qa]);
+    float u0, u1;
+    uniform2(c.seed, P_RESET, (uint32_t)(c.act / 2), c.env, episode, u0, u1);
+    float u = (c.act & 1) ? u1 : u0;
+    ls.v = cfg->reset_qvel_scale * (2.f * u - 1.f);
+  } else if (l < c.nv && c.qadr >= 0) {
+    ls.q = m->qpos0[c.qadr];
+  }
+  {
+    float u0, u1;
+    uniform2(c.seed, P_RESET, 15u, c.env, episode, u0, u1);
+    s.lag = cfg->lag_range[0] + (cfg->lag_range[1] - cfg->lag_range[0]) * u0;
+    s.push_timer = cfg->push_interval[0] + (cfg->push_interval[1] - cfg->push_interval[0]) * u1;
+  }
+  for (int k = 0; k < 4; k++) s.ema[k] = 0.f;
+  ls.pp = ls.q;
+  ls.pv = ls.v;
+  ls.ptau = 0.f;
+  ls.ctrl = 0.f;
+  s.ep_ret = 0.f;
+  s.ep_steps = 0u;
+  s.episode = episode + 1u;
+}
+
+/* push event (train.py:1459-1468) */
+__device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, float cur) {
+  const ZbEnvConfig* cfg = c.cfg;
+  float timer = s.push_timer - cfg->ctrl_dt;
+  if (timer <= 0.f) {
+    float u0, u1, w0, w1;
+    uniform2(c.seed, P_PUSH, 0u, c.env, s.rng_step, u0, u1);
+    uniform2(c.seed, P_PUSH, 1u, c.env, s.rng_step, w0, w1);
+    float mag = (cfg->push_vel_range[0] + (cfg->push_vel_range[1] - cfg->push_vel_range[0]) * w1) / cfg->push_vel_range[1];
+    if (c.l == 0) ls.v += cur * mag * cfg->push_linvel[0] * (2.f * u0 - 1.f);
+    if (c.l == 1) ls.v += cur * mag * cfg->push_linvel[1] * (2.f * u1 - 1.f);
+    if (c.l == 2) ls.v += cur * mag * cfg->push_linvel[2] * (2.f * w0 - 1.f);
+    timer = cfg->push_interval[0] + (cfg->push_interval[1] - cfg->push_interval[0]) * w1;
+  }
+  s.push_timer = timer;
+}
+
+/* ---------------------------- per-team context ------------------------------ */
+__device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvConfig* cfg, EnvL* L, uint64_t seed, uint32_t env) {
+  c.m = m;
+  c.cfg = cfg;
+  c.L = L;
+  c.seed = seed;
+  c.env = env;
+  const int l = threadIdx.x & (TEAM - 1);
+  c.l = l;
+  c.nb = m->nbody;
+  c.nv = m->nv;
+  c.nu = m->nu;
+  c.ngeom = m->ngeom;
+  c.maxdd = m->max_depth;
+  /* body role */
+  const bool isb = l < c.nb;
+  c.bpar = isb ? m->body_parent[l] : 0;
+  c.bdep = isb ? m->body_depth[l] : 1000;
+  c.bjt = isb ? m->body_jnttype[l] : ZB_JNT_NONE;
+  c.bdofadr = isb ? m->body_dofadr[l] : -1;
+  c.blast = isb ? m->body_lastdof[l] : -1;
+  c.maxbd = tmaxi(isb ? c.bdep : 0);
+  int nch = 0;
+  uint32_t ch0 = 0, ch1 = 0;
+  for (int b = 1; b < c.nb; b++) {
+    if (isb && m->body_parent[b] == l && nch < 8) {
+      if (nch < 4) ch0 |= (uint32_t)b << (8 * nch);
+      else ch1 |= (uint32_t)b << (8 * (nch - 4));
+      nch++;
+    }
+  }
+  c.nch = nch;
+  c.ch0 = ch0;
+  c.ch1 = ch1;
+  uint64_t lv = 0;
+  for (int d = 0; d <= c.maxbd && d < 16; d++) {
+    int mx = tmaxi(c.bdep == d ? nch : 0);
+    lv |= (uint64_t)(mx & 0xf) << (4 * d);
+  }
+  c.lvlch = lv;
+  /* dof role */
+  const bool isd = l < c.nv;
+  c.ddep = isd ? m->dof_depth[l] : 0;
+  c.dbody = isd ? m->dof_body[l] : 0;
+  c.qadr = isd ? m->dof_qposadr[l] : -1;
+  c.act = -1;
+  for (int a = 0; a < c.nu; a++)
+    if (isd && m->act_dof[a] == l) c.act = a;
+  uint32_t a0 = 0, a1 = 0, a2 = 0;
+  for (int e = 0; e < CAP; e++) {
+    int a = isd ? m->dof_anc[l][e] : -1;
+    uint32_t v = (uint32_t)(a < 0 ? 0 : a) & 0xffu;
+    if (e < 4) a0 |= v << (8 * e);
+    else if (e < 8) a1 |= v << (8 * (e - 4));
+    else a2 |= v << (8 * (e - 8));
+  }
+  c.anc0 = a0;
+  c.anc1 = a1;
+  c.anc2 = a2;
+  uint32_t desc = 0;
+  for (int k = 0; k < c.nv; k++) {
+    int dk = m->dof_depth[k];
+    if (isd && k != l && dk > c.ddep && m->dof_anc[k][c.ddep] == l) desc |= 1u << k;
+  }
+  c.desc = desc;
+}
+
+/* ---------------------------------- kernels --------------------------------- */
+template <bool ROLLOUT>
+__global__ __launch_bounds__(64) void step_kernel(StepArgs a) {
+  __shared__ EnvL lds[NTEAM];
+  const int team = threadIdx.x / TEAM;
+  const int e = blockIdx.x * NTEAM + team;
+  if (e >= a.n_envs) return;
+  const ZbModel* m = a.model;
+  const ZbEnvConfig* cfg = &a.cfg;
+  Ctx c;
+  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
+  float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
+  EnvS s;
+  LaneS ls;
+  load_state(c, s, ls, st);
+  load_params(c, s, ls, rnd);
+  BodyK B;
+  Rows r;
+  Sensors sen;
+  int iters = 0;
+  float rsum = 0.f;
+  bool done = false;
+  const int nsteps = ROLLOUT ? a.nsteps : 1;
+  for (int t = 0; t < nsteps; t++) {
+    const bool last_t = t == nsteps - 1;
+    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + e) * ZB_NJ + c.act];
+    if (cfg->flags & ZB_F_PUSH) push_event(c, s, ls, a.curriculum);
+    float total = 0.f;
+    int ss = 0;
+    bool resetting = false;
+    /* 20 substeps; when the env terminates, one more pass of the same code path
+       runs the reset forward (mjx.forward after MjxEngine.reset) */
+    while (true) {
+      if (!resetting) feetech(c, ls);
+      forward(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, iters);
+      if (resetting) break;
+      integrate(c, s, ls);
+      if (++ss < cfg->n_substeps) continue;
+      {
+        bool bad = (c.l < c.nv) && !(isfinite(ls.q) && isfinite(ls.v));
+        if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
+      }
+      bool fail;
+      float* terms = (a.reward_terms && !ROLLOUT) ? a.reward_terms + (size_t)e * ZB_NUM_TERMS : nullptr;
+      done = rewards(c, s, ls, B, a.curriculum, terms, total, fail);
+      rsum += total;
+      if (a.stats && c.l == 0) {
+        float* sp = a.stats + (size_t)e * ZB_NUM_STATS;
+        sp[ZB_ST_REWARD] += total;
+        if (done) {
+          sp[ZB_ST_RETURN] += s.ep_ret;
+          sp[ZB_ST_LENGTH] += (float)s.ep_steps;
+          sp[ZB_ST_DONE] += 1.f;
+        }
+      }
+      if (!(done && (cfg->flags & ZB_F_AUTORESET))) break;
+      reset_prepare(c, s, ls, rnd);
+      resetting = true;
+    }
+    if (last_t) {
+      observe(c, s, ls, B, sen, a.obs_actor ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
+              a.obs_critic ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
+              a.obs_extra ? a.obs_extra + (size_t)e * ZB_OBS_EXTRA : nullptr);
+    } else {
+      observe(c, s, ls, B, sen, nullptr, nullptr, nullptr);
+    }
+    s.rng_step += 1u;
+    if (c.l == 0 && last_t) {
+      if (a.reward) a.reward[e] = ROLLOUT ? rsum : total;
+      if (a.done) a.done[e] = done ? 1 : 0;
+    }
+  }
+  if (a.iters && c.l == 0) a.iters[e] = iters;
+  store_state(c, s, ls, st);
+}
+
+__global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
+  __shared__ EnvL lds[NTEAM];
+  const int team = threadIdx.x / TEAM;
+  const int e = blockIdx.x * NTEAM + team;
+  if (e >= a.n_envs) return;
+  if (a.reset_mask && !a.reset_mask[e]) return;
+  const ZbModel* m = a.model;
+  const ZbEnvConfig* cfg = &a.cfg;
+  Ctx c;
+  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
+  float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
+  EnvS s;
+  LaneS ls;
+  load_state(c, s, ls, st);
+  BodyK B;
+  Rows r;
+  Sensors sen;
+  int it = 0;
+  reset_prepare(c, s, ls, rnd);
+  forward(c, s, ls, B, r, true, sen, it);
+  observe(c, s, ls, B, sen, a.obs_actor ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
+          a.obs_critic ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
+          a.obs_extra ? a.obs_extra + (size_t)e * ZB_OBS_EXTRA : nullptr);
+  store_state(c, s, ls, st);
+}
+
+/* single forward on the stored (qpos, qvel), ctrl = action row; dumps internals */
+__global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
+  __shared__ EnvL lds[NTEAM];
+  const int team = threadIdx.x / TEAM;
+  const int e = blockIdx.x * NTEAM + team;
+  if (e >= a.n_envs) return;
+  const ZbModel* m = a.model;
+  const ZbEnvConfig* cfg = &a.cfg;
+  Ctx c;
+  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
+  EnvS s;
+  LaneS ls;
+  load_state(c, s, ls, st);
+  load_params(c, s, ls, nullptr);
+  ls.ctrl = (c.act >= 0 && a.action) ? a.action[(size_t)e * ZB_NJ + c.act] : 0.f;
+  BodyK B;
+  Rows r;
+  Sensors sen;
+  int it = 0;
+  forward(c, s, ls, B, r, true, sen, it);
+  float* d = a.dbg + (size_t)e * ZB_DBG_STRIDE;
+  const int l = c.l;
+  EnvL* L = c.L;
+  /* dense M from depth-indexed rows */
+  for (int i = l; i < c.nv * c.nv; i += TEAM) d[ZB_DBG_QM + i] = 0.f;
+  __threadfence_block();
+  tsync();
+  if (l < c.nv) {
+    for (int ee = 0; ee <= c.ddep; ee++) {
+      int aa = ancof(c, ee);
+      float v = L->M[l][ee];
+      d[ZB_DBG_QM + l * c.nv + aa] = v;
+      d[ZB_DBG_QM + aa * c.nv + l] = v;
+    }
+    d[ZB_DBG_QACC + l] = ls.qacc;
+  }
+  /* recompute smooth quantities for the dump is avoided: store qacc only; the
+     bias/qacc_smooth slots are filled by a second, constraint-free pass below */
+  if (l < c.nb) {
+    for (int k = 0; k < 3; k++) d[ZB_DBG_XPOS + 3 * l + k] = B.xp[k];
+    for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = B.ci[k];
+    for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
+  }
+  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (r.hf ? 1 : 0) + (r.hlo ? 1 : 0) + (r.hhi ? 1 : 0)));
+  if (l == 0) {
+    d[ZB_DBG_MISC + 0] = (float)nefc;
+    d[ZB_DBG_MISC + 1] = (float)(r.nrow / 4);
+    d[ZB_DBG_MISC + 2] = sen.touch[0];
+    d[ZB_DBG_MISC + 3] = sen.touch[1];
+    for (int k = 0; k < 4; k++) d[ZB_DBG_MISC + 4 + k] = sen.fq[k];
+    for (int k = 0; k < 3; k++) d[ZB_DBG_MISC + 8 + k] = sen.gyro[k];
+    for (int k = 0; k < 3; k++) d[ZB_DBG_MISC + 11 + k] = sen.acc[k];
+  }
+  /* smooth dynamics: qfrc_bias and qacc_smooth recomputed on the same state */
+  {
+    float X[CAP];
+    for (int ee = 0; ee < CAP; ee++) X[ee] = (l < c.nv) ? L->M[l][ee] : 0.f;
+    float Dinv = factor_ldl(c, X);
+    if (l < 32) L->vec[V_QVEL][l] = l < c.nv ? ls.v : 0.f;
+    tsync();
+    com_vel(c, B);
+    float ca[6], z6[6] = {0, 0, 0, 0, 0, 0};
+    com_acc(c, ca, false);
+    float bias = rne_project(c, B, ca, z6);
+    float act = c.act >= 0 ? m->act_gear[c.act] * ls.actforce : 0.f;
+    float fs = (l < c.nv) ? (-ls.damp * ls.v - bias + act) : 0.f;
+    float qs = solve_ldl(c, fs, Dinv);
+    if (l < c.nv) {
+      d[ZB_DBG_BIAS + l] = bias;
+      d[ZB_DBG_QACCS + l] = qs;
+    }
+  }
+}
+
+hipError_t launch_step(const StepArgs& a, hipStream_t s) {
+  if (a.n_envs <= 0) return hipSuccess;
+  dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
+  if (a.nsteps > 1)
+    hipLaunchKernelGGL(step_kernel<true>, grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL(step_kernel<false>, grid, block, 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_reset(const StepArgs& a, hipStream_t s) {
+  if (a.n_envs <= 0) return hipSuccess;
+  dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
+  hipLaunchKernelGGL(reset_kernel, grid, block, 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s) {
+  if (a.n_envs <= 0) return hipSuccess;
+  dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
+  hipLaunchKernelGGL(debug_forward_kernel, grid, block, 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace zb

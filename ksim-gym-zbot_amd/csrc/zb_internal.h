@@ -1,0 +1,55 @@
+/*
+ * zb_internal.h — declarations shared by the HIP engine (zb_engine.hip) and
+ * the C-ABI host code (zb_capi.cpp). Not part of the public ABI.
+ */
+#ifndef ZB_INTERNAL_H
+#define ZB_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zbot.h"
+
+/* debug forward dump layout (zb_debug_forward), fp32 words per env */
+#define ZB_DBG_QM      0     /* [nv*nv] dense symmetric mass matrix */
+#define ZB_DBG_BIAS    1024  /* [nv] qfrc_bias */
+#define ZB_DBG_QACCS   1056  /* [nv] qacc_smooth */
+#define ZB_DBG_QACC    1088  /* [nv] constrained qacc */
+#define ZB_DBG_XPOS    1120  /* [nbody*3] */
+#define ZB_DBG_CINERT  1216  /* [nbody*10] */
+#define ZB_DBG_CVEL    1536  /* [nbody*6] */
+#define ZB_DBG_MISC    1728  /* nefc, ncon, touch_l, touch_r, imu quat(4), gyro(3), acc(3) */
+#define ZB_DBG_STRIDE  1760
+
+namespace zb {
+
+struct StepArgs {
+  const ZbModel* model;     /* device copy */
+  ZbEnvConfig cfg;
+  int n_envs;
+  int env_offset;
+  uint64_t seed;
+  float* state;             /* [n, ZB_STATE_STRIDE] */
+  float* rnd;               /* [n, ZB_RAND_STRIDE] */
+  const float* action;      /* [nsteps, n, 20] */
+  int nsteps;
+  float* obs_actor;
+  float* obs_critic;
+  float* obs_extra;
+  float* reward_terms;
+  float* reward;            /* per step reward (nsteps==1) or reward sum (rollout) */
+  uint8_t* done;
+  float curriculum;
+  float* stats;             /* [n, ZB_NUM_STATS] */
+  int32_t* iters;           /* [n] */
+  const uint8_t* reset_mask;
+  float* dbg;               /* [n, ZB_DBG_STRIDE] */
+};
+
+hipError_t launch_step(const StepArgs& a, hipStream_t s);
+hipError_t launch_reset(const StepArgs& a, hipStream_t s);
+hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s);
+
+}  // namespace zb
+
+#endif

@@ -1,0 +1,194 @@
+"""ctypes binding of libzbot_hip.so over PyTorch-ROCm device tensors.
+
+This is the product path: every call goes to the HIP engine. There is no CPU
+fallback — when the library or a GPU is missing, construction raises.
+The C ABI is documented in include/zbot.h.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import cstructs as cs
+
+LIB_NAME = "libzbot_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+CSRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+
+_lib: C.CDLL | None = None
+
+
+class ZbError(RuntimeError):
+    pass
+
+
+def build_library(force: bool = False) -> str:
+    """Compile libzbot_hip.so in-tree for gfx950 (hipcc; no GPU needed)."""
+    import subprocess  # noqa: PLC0415
+
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-C", CSRC_DIR, "-s"], check=True)
+    return LIB_PATH
+
+
+def load_library() -> C.CDLL:
+    """Load the engine library; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ZbError(f"{LIB_PATH} not found: build it with `make -C {CSRC_DIR}` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.zb_abi_version.restype = C.c_int
+    L.zb_model_struct_bytes.restype = C.c_size_t
+    L.zb_config_struct_bytes.restype = C.c_size_t
+    L.zb_state_stride.restype = C.c_int
+    L.zb_rand_stride.restype = C.c_int
+    L.zb_last_error.restype = C.c_char_p
+    L.zb_default_config.argtypes = [C.POINTER(cs.ZbEnvConfig)]
+    L.zb_create.argtypes = [C.POINTER(cs.ZbModel), C.POINTER(cs.ZbEnvConfig), C.c_int, C.c_int, C.c_int, C.c_uint64,
+                            C.POINTER(vp)]
+    L.zb_destroy.argtypes = [vp]
+    L.zb_reset.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.zb_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp]
+    L.zb_rollout.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, C.c_float, vp]
+    for f in ("zb_get_state", "zb_set_state", "zb_get_rand", "zb_set_rand", "zb_get_solver_iters"):
+        getattr(L, f).argtypes = [vp, vp, vp]
+    L.zb_get_stats.argtypes = [vp, vp, C.c_int, vp]
+    L.zb_debug_forward.argtypes = [vp, vp, vp, vp, vp]
+    for f in ("zb_create", "zb_destroy", "zb_reset", "zb_step", "zb_rollout", "zb_get_state", "zb_set_state",
+              "zb_get_rand", "zb_set_rand", "zb_get_stats", "zb_get_solver_iters", "zb_debug_forward"):
+        getattr(L, f).restype = C.c_int
+    if L.zb_model_struct_bytes() != C.sizeof(cs.ZbModel):
+        raise ZbError("ZbModel layout mismatch between cstructs.py and the library")
+    if L.zb_config_struct_bytes() != C.sizeof(cs.ZbEnvConfig):
+        raise ZbError("ZbEnvConfig layout mismatch between cstructs.py and the library")
+    _lib = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise ZbError(f"libzbot_hip error {rc}: {load_library().zb_last_error().decode()}")
+
+
+def _ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+DBG_STRIDE = 1760
+DBG = dict(qM=0, bias=1024, qacc_smooth=1056, qacc=1088, xpos=1120, cinert=1216, cvel=1536, misc=1728)
+
+
+class HipEngine:
+    """N Z-Bot environments on one GPU (one handle)."""
+
+    def __init__(self, model, cfg: cs.ZbEnvConfig, n_envs: int, env_offset: int = 0, device: int = 0,
+                 seed: int = 0):
+        import torch  # noqa: PLC0415
+
+        if not torch.cuda.is_available():
+            raise ZbError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.torch = torch
+        self.L = load_library()
+        self.cmodel = model.cmodel if hasattr(model, "cmodel") else model
+        self.cfg = cfg
+        self.n = n_envs
+        self.env_offset = env_offset
+        self.device = torch.device("cuda", device)
+        self.seed = seed
+        h = C.c_void_p()
+        _check(self.L.zb_create(C.byref(self.cmodel), C.byref(cfg), n_envs, env_offset, device, seed, C.byref(h)))
+        self.h = h
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.obs_actor = torch.zeros(n_envs, cs.OBS_ACTOR, **f32)
+        self.obs_critic = torch.zeros(n_envs, cs.OBS_CRITIC, **f32)
+        self.obs_extra = torch.zeros(n_envs, cs.OBS_EXTRA, **f32)
+        self.reward_terms = torch.zeros(n_envs, cs.NUM_TERMS, **f32)
+        self.reward = torch.zeros(n_envs, **f32)
+        self.done = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.L.zb_destroy(h)
+            except Exception:  # noqa: BLE001
+                pass
+            self.h = None
+
+    def _stream(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def outputs(self) -> dict:
+        return dict(obs_actor=self.obs_actor, obs_critic=self.obs_critic, obs_extra=self.obs_extra,
+                    reward_terms=self.reward_terms, reward=self.reward, done=self.done)
+
+    def reset(self, mask=None, extras: bool = True) -> dict:
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
+        _check(self.L.zb_reset(self.h, _ptr(m), _ptr(self.obs_actor), _ptr(self.obs_critic),
+                               _ptr(self.obs_extra) if extras else None, self._stream()))
+        return self.outputs()
+
+    def step(self, action, curriculum: float = 1.0, extras: bool = True, terms: bool = True) -> dict:
+        a = action
+        if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if tuple(a.shape) != (self.n, cs.NJ):
+            raise ZbError(f"action must be [{self.n}, {cs.NJ}], got {tuple(a.shape)}")
+        _check(self.L.zb_step(self.h, _ptr(a), _ptr(self.obs_actor), _ptr(self.obs_critic),
+                              _ptr(self.obs_extra) if extras else None, _ptr(self.reward_terms) if terms else None,
+                              _ptr(self.reward), _ptr(self.done), float(curriculum), self._stream()))
+        return self.outputs()
+
+    def rollout(self, actions, curriculum: float = 1.0, reward_sum=None) -> dict:
+        a = actions.to(device=self.device, dtype=self.torch.float32).contiguous()
+        T = a.shape[0]
+        if tuple(a.shape) != (T, self.n, cs.NJ):
+            raise ZbError("actions must be [T, n_envs, 20]")
+        _check(self.L.zb_rollout(self.h, _ptr(a), T, _ptr(self.obs_actor), _ptr(self.obs_critic), _ptr(reward_sum),
+                                 _ptr(self.done), float(curriculum), self._stream()))
+        return self.outputs()
+
+    def get_state(self):
+        out = self.torch.empty(self.n, cs.STATE_STRIDE, dtype=self.torch.float32, device=self.device)
+        _check(self.L.zb_get_state(self.h, _ptr(out), self._stream()))
+        return out
+
+    def set_state(self, state) -> None:
+        s = state.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if tuple(s.shape) != (self.n, cs.STATE_STRIDE):
+            raise ZbError("state must be [n_envs, ZB_STATE_STRIDE]")
+        _check(self.L.zb_set_state(self.h, _ptr(s), self._stream()))
+        self.torch.cuda.current_stream(self.device).synchronize()
+
+    def get_rand(self):
+        out = self.torch.empty(self.n, cs.RAND_STRIDE, dtype=self.torch.float32, device=self.device)
+        _check(self.L.zb_get_rand(self.h, _ptr(out), self._stream()))
+        return out
+
+    def set_rand(self, rand) -> None:
+        r = rand.to(device=self.device, dtype=self.torch.float32).contiguous()
+        _check(self.L.zb_set_rand(self.h, _ptr(r), self._stream()))
+        self.torch.cuda.current_stream(self.device).synchronize()
+
+    def get_stats(self, clear: bool = False):
+        out = self.torch.empty(self.n, cs.NUM_STATS, dtype=self.torch.float32, device=self.device)
+        _check(self.L.zb_get_stats(self.h, _ptr(out), int(clear), self._stream()))
+        return out
+
+    def solver_iters(self):
+        out = self.torch.empty(self.n, dtype=self.torch.int32, device=self.device)
+        _check(self.L.zb_get_solver_iters(self.h, _ptr(out), self._stream()))
+        return out
+
+    def debug_forward(self, state, ctrl=None):
+        s = state.to(device=self.device, dtype=self.torch.float32).contiguous()
+        c = None if ctrl is None else ctrl.to(device=self.device, dtype=self.torch.float32).contiguous()
+        out = self.torch.zeros(self.n, DBG_STRIDE, dtype=self.torch.float32, device=self.device)
+        _check(self.L.zb_debug_forward(self.h, _ptr(s), _ptr(c), _ptr(out), self._stream()))
+        return out
