@@ -1,0 +1,202 @@
+"""Benchmark: env-steps/s of the fused HIP Z-Bot env.step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--config c2|c3|c5]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+A "step" is one zb_step over all E envs of a GPU (20 physics substeps each,
+Newton solver 8 / 8 line-search iterations, observations, rewards, auto-reset)
+— the hot path of ksim's step_engine for train.py's ZbotWalkingTask
+(SURVEY.md §3.2). Inputs are synthetic (actions = JOINT_BIASES + 0.05 N(0,1),
+generated on the GPU before timing); the state is resident in HBM. Prints ONE
+JSON line on rank 0 (contract: see the repository brief / DESIGN.md §Bench).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
+
+METRIC = "env-steps/sec at N envs per GPU, 1/2/4/8 MI355X; % HBM roofline"
+
+CONFIGS = {
+    "c2": dict(envs=8192, push=False, randomize=False, name="C2: 8192 envs/GPU, flat-floor stand, 256-step rollout"),
+    "c3": dict(envs=32768, push=True, randomize=False, name="C3: 32768 envs/GPU, push-perturbation curriculum"),
+    "c5": dict(envs=16384, push=False, randomize=True, name="C5: 16384 envs/GPU, per-env domain randomization"),
+}
+
+
+def cpu_baseline(cm, cfg, budget_s: float, n_envs: int = 256) -> dict:
+    """Time the CPU oracle (fp32 C, OpenMP over envs) on a bounded sample."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # noqa: PLC0415  (cpu_baseline leg: the oracle is the CPU twin being timed)
+
+    env = O.OracleEnv(cm.cmodel, cfg, n_envs, seed=0)
+    env.reset()
+    acts = [O.synthetic_actions(cm.cmodel, 0, n_envs, 0, t) for t in range(4)]
+    env.step(acts[0])  # warm-up (thread pool)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        env.step(acts[steps % 4])
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {
+        "value": n_envs * steps / el,
+        "unit": "env-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n_envs} envs x {steps} env-steps of the same C2 workload on the oracle "
+                  f"(fp32 C restatement, OpenMP {threads} threads), {el:.1f} s",
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default: the config's)")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-baseline-sec", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+    from zbot_amd import compile_model, default_config  # noqa: PLC0415
+    from zbot_amd import cstructs as cs  # noqa: PLC0415
+    from zbot_amd.constants import JOINT_BIASES  # noqa: PLC0415
+    from zbot_amd.engine import HipEngine  # noqa: PLC0415
+    from zbot_amd.metrics import HBM_PEAK_GBS, bytes_per_env_step  # noqa: PLC0415
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    conf = CONFIGS[args.config]
+    n = args.envs or conf["envs"]
+    cm = compile_model()
+    cfg = default_config(push=conf["push"], randomize=conf["randomize"])
+    eng = HipEngine(cm, cfg, n, env_offset=rank * n, device=local_rank, seed=args.seed)
+
+    # synthetic policy outputs, generated before timing (policy is out of scope)
+    T = args.warmup + args.steps
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    bias = torch.tensor([b for _, b, _ in JOINT_BIASES], device=dev)
+    acts = bias + 0.05 * torch.randn(min(T, 64), n, cs.NJ, device=dev, generator=g)
+
+    eng.reset()
+    for t in range(args.warmup):
+        eng.step(acts[t % acts.shape[0]], extras=False)
+    eng.get_stats(clear=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for t in range(args.steps):
+        ev[t][0].record(stream)
+        eng.step(acts[(args.warmup + t) % acts.shape[0]], extras=False)
+        ev[t][1].record(stream)
+    # per-rollout episode statistics: per-GPU partials summed in fixed env order,
+    # then an RCCL all_gather and a fixed rank-order sum (bit-reproducible)
+    part = eng.get_stats(clear=False).double().sum(0)
+    if world > 1:
+        allp = [torch.zeros_like(part) for _ in range(world)]
+        dist.all_gather(allp, part)
+        total_stats = torch.stack(allp).sum(0)
+    else:
+        total_stats = part
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    el_t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    elapsed = float(el_t.item())
+
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    avg_ms = sum(kern_ms) / len(kern_ms)
+    bpe = bytes_per_env_step(extras=False, terms=True)
+    achieved = bpe * n / (avg_ms * 1e-3) / 1e9
+    iters = eng.solver_iters().float().mean().item()
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("envs") == n:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        value = world * n * args.steps / elapsed
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: actions = JOINT_BIASES + 0.05*N(0,1) on the Z-Bot-like descriptor",
+            "config": {
+                "workload": conf["name"],
+                "envs_per_gpu": n,
+                "global_envs": world * n,
+                "substeps_per_step": cfg.n_substeps,
+                "solver": f"newton, {cfg.iterations} iters / {cfg.ls_iterations} ls iters",
+                "parallelism": f"env-shard x{world} (one process per GPU)",
+                "avg_solver_iters_per_env_step": iters,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "zb::step_kernel<false>",
+                "kernel_avg_ms": avg_ms,
+                "algorithmic_bytes_per_env_step": bpe,
+                "note": "the path is FP32-VALU/latency bound (DESIGN.md §Roofline); HBM fraction reported as required",
+            },
+            "episode_stats": {
+                "episodes_done": float(total_stats[2].item()),
+                "mean_return": float((total_stats[0] / total_stats[2].clamp(min=1)).item()),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

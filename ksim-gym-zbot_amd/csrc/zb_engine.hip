@@ -44,7 +44,7 @@ constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0)
 enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3 };
 
 /* per-environment LDS working set (8.6 KB) */
-struct EnvL {
+struct __align__(16) EnvL {
   float cdof[32][6];
   float cdofdot[32][6];
   float M[32][CAP];
@@ -55,7 +55,6 @@ struct EnvL {
   float rowDA[32];
   float rowF[32];
   float Dk[32];
-  int rowlist[32];
 };
 
 /* ----------------------------- team primitives ----------------------------- */
@@ -216,6 +215,9 @@ struct Ctx {
   int ddep, dbody, qadr, act;
   uint32_t anc0, anc1, anc2;
   uint32_t desc; /* strict descendants of dof l */
+  uint32_t rowmask; /* contact rows whose Jacobian chain contains dof l */
+  int dk0;          /* index of dof l within its body's joint (free joint: 0..5) */
+  int dfree;        /* dof l belongs to a free joint */
 };
 
 __device__ __forceinline__ int ancof(const Ctx& c, int e) {
@@ -273,6 +275,7 @@ struct Rows {
   float alo, Dlo, jlo, flo; int actlo;
   float ahi, Dhi, jhi, fhi; int acthi;
   int nrow;
+  uint32_t exmask; /* team-uniform: existing contact rows */
 };
 
 /* ------------------------------- kinematics -------------------------------- */
@@ -477,44 +480,60 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 }
 
 /* ---------------------- sparse L'DL factor + solves ------------------------ */
-/* factor rows X (lane j, depth-indexed) in place; writes L rows to LDS L[][]
- * and the diagonal to LDS Dk[]; returns 1/D_j */
-__device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP]) {
+/* 16-byte LDS row access (rows are 12 floats = 48 B, 16-B aligned) */
+__device__ __forceinline__ void ld_row(const float* p, float v[CAP]) {
+  const float4* q = reinterpret_cast<const float4*>(p);
+  float4 a = q[0], b = q[1], c4 = q[2];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  v[8] = c4.x; v[9] = c4.y; v[10] = c4.z; v[11] = c4.w;
+}
+__device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
+  float4* q = reinterpret_cast<float4*>(p);
+  q[0] = make_float4(v[0], v[1], v[2], v[3]);
+  q[1] = make_float4(v[4], v[5], v[6], v[7]);
+  q[2] = make_float4(v[8], v[9], v[10], v[11]);
+}
+
+/* Sparse L'DL (mj_factorM order: leaves first) of depth-indexed rows.
+ * Lane j holds the off-diagonal entries X[e] = A(j, anc_e(j)), e < depth(j),
+ * and the diagonal Xd. On return the L rows are in LDS L[][] (L(k, anc_e(k))),
+ * the pivots in Dk[], and 1/D_j is returned. */
+__device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd) {
   EnvL* L = c.L;
   const int j = c.l;
   for (int k = c.nv - 1; k >= 0; k--) {
-    const int dk = c.m->dof_depth[k];
     if (j == k) {
-      float Dkv = 0.f;
-#pragma unroll
-      for (int e = 0; e < CAP; e++)
-        if (e == dk) Dkv = X[e];
-      Dkv = fmaxf(Dkv, MINVAL);
+      float Dkv = fmaxf(Xd, MINVAL);
       float inv = 1.0f / Dkv;
 #pragma unroll
-      for (int e = 0; e < CAP; e++) {
-        if (e < dk) X[e] = X[e] * inv;
-        L->L[k][e] = X[e];
-      }
+      for (int e = 0; e < CAP; e++) X[e] = X[e] * inv;
+      st_row(&L->L[k][0], X);
       L->Dk[k] = Dkv;
     }
     tsync();
     if ((c.desc >> k) & 1u) {
       float Dkv = L->Dk[k];
-      float lk = L->L[k][c.ddep];  /* L(k, j) */
-      float t = lk * Dkv;           /* = M(k, j) after Schur updates */
+      float lk = L->L[k][c.ddep]; /* L(k, j) */
+      float t = lk * Dkv;         /* A(k, j) after the Schur updates of k's subtree */
+      float row[CAP];
+      ld_row(&L->L[k][0], row);
+      Xd -= t * lk;
 #pragma unroll
-      for (int e = 0; e < CAP; e++)
-        if (e <= c.ddep) X[e] -= t * L->L[k][e];
+      for (int e = 0; e < CAP; e++) X[e] -= (e < c.ddep ? t : 0.f) * row[e];
     }
   }
-  float D = 1.f;
-#pragma unroll
-  for (int e = 0; e < CAP; e++)
-    if (e == c.ddep) D = X[e];
-  D = fmaxf(D, MINVAL);
   tsync();
-  return 1.0f / D;
+  return 1.0f / fmaxf(Xd, MINVAL);
+}
+
+/* load a depth-indexed M row into off-diagonal X[] (masked) and diagonal */
+__device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
+  const int j = c.l & 31;
+  ld_row(&c.L->M[j][0], X);
+#pragma unroll
+  for (int e = 0; e < CAP; e++) X[e] = (e < c.ddep && c.l < c.nv) ? X[e] : 0.f;
+  return (c.l < c.nv) ? c.L->M[j][c.ddep] : 1.f;
 }
 
 /* x <- (L'DL)^-1 x, x held by dof lanes */
@@ -571,11 +590,10 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
   EnvL* L = c.L;
   const int j = c.l;
   if (j < c.nv) {
-    int bj = c.dbody;
-    int jt = m->body_jnttype[bj];
-    int k0 = j - m->body_dofadr[bj];
-    int cap = c.ddep;                       /* hinge: before own contribution */
-    if (jt == ZB_JNT_FREE) cap = c.ddep - k0 + 3; /* free rot: after the translations */
+    const int k0 = c.dk0;
+    const bool isfree = c.dfree;
+    int cap = c.ddep;                     /* hinge: before own contribution */
+    if (isfree) cap = c.ddep - k0 + 3;    /* free rot: after the translations */
     float acc[6] = {0, 0, 0, 0, 0, 0}, before[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < CAP; e++) {
@@ -591,7 +609,7 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
       }
     }
     float cdd[6] = {0, 0, 0, 0, 0, 0};
-    if (!(jt == ZB_JNT_FREE && k0 < 3)) {
+    if (!(isfree && k0 < 3)) {
       float cd[6];
 #pragma unroll
       for (int k = 0; k < 6; k++) cd[k] = L->cdof[j][k];
@@ -780,9 +798,8 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   uint32_t tb = (uint32_t)(bal >> ((threadIdx.x & 63) & ~(TEAM - 1)));
   if (TEAM < 64) tb &= 0xffffffffu;
   r.nrow = __popc(tb);
+  r.exmask = tb;
   if (r.ex) {
-    int idx = __popc(tb & ((1u << l) - 1u));
-    L->rowlist[idx] = l;
 #pragma unroll
     for (int e = 0; e < CAP; e++) L->J[l][e] = Jc[e];
   }
@@ -857,15 +874,11 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
   tsync();
   float qc = 0.f;
   if (c.l < c.nv) {
-    for (int i = 0; i < r.nrow; i++) {
-      int row = L->rowlist[i];
-      float fr = L->rowF[row];
-      /* is this dof on the row's chain? rows of one geom share a chain */
-      if (fr != 0.f) {
-        int g = row >> 4;
-        int kdr = c.m->body_lastdof[c.m->geom_body[g]];
-        if (kdr == c.l || ((c.desc >> kdr) & 1u)) qc += L->J[row][c.ddep] * fr;
-      }
+    uint32_t tb = r.exmask;
+    while (tb) {
+      int row = __ffs(tb) - 1;
+      tb &= tb - 1u;
+      if ((c.rowmask >> row) & 1u) qc += L->J[row][c.ddep] * L->rowF[row];
     }
     if (r.hf) qc += r.ff;
     if (r.hlo) qc += r.flo;
@@ -879,33 +892,29 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
 __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
   EnvL* L = c.L;
   float H[CAP];
-#pragma unroll
-  for (int e = 0; e < CAP; e++) H[e] = (c.l < c.nv) ? L->M[c.l][e] : 0.f;
+  float Hd = load_mrow(c, H);
   if (c.l < c.nv) {
-    for (int i = 0; i < r.nrow; i++) {
-      int row = L->rowlist[i];
+    uint32_t tb = r.exmask & c.rowmask;
+    while (tb) {
+      int row = __ffs(tb) - 1;
+      tb &= tb - 1u;
       float da = L->rowDA[row];
-      if (da != 0.f) {
-        int g = row >> 4;
-        int kdr = c.m->body_lastdof[c.m->geom_body[g]];
-        if (kdr == c.l || ((c.desc >> kdr) & 1u)) {
-          float jj = da * L->J[row][c.ddep];
+      float jd = L->J[row][c.ddep];
+      float jr[CAP];
+      ld_row(&L->J[row][0], jr);
+      float jj = da * jd;
+      Hd += jj * jd;
 #pragma unroll
-          for (int e = 0; e < CAP; e++)
-            if (e <= c.ddep) H[e] += jj * L->J[row][e];
-        }
-      }
+      for (int e = 0; e < CAP; e++) H[e] += (e < c.ddep ? jj : 0.f) * jr[e];
     }
     float dd = 0.f;
     if (r.hf && r.actf) dd += r.Df;
     if (r.hlo && r.actlo) dd += r.Dlo;
     if (r.hhi && r.acthi) dd += r.Dhi;
-#pragma unroll
-    for (int e = 0; e < CAP; e++)
-      if (e == c.ddep) H[e] += dd;
+    Hd += dd;
   }
   tsync();
-  return factor_ldl(c, H);
+  return factor_ldl(c, H, Hd);
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
@@ -1003,8 +1012,12 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     r.jlo += alpha * search;
     r.jhi -= alpha * search;
     float oldcost = cost;
+    const int pa = r.act, pf = r.actf, plo = r.actlo, phi = r.acthi;
     cost = update_constraint(c, r, x, qs, fs, Ma, grad);
-    Dinv = hessian_factor(c, r);
+    /* H depends only on the active set (M, D fixed within a substep):
+       refactor only when it changed (MuJoCo's Newton does the same) */
+    const bool changed = tmaxi((r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1 : 0) != 0;
+    if (changed) Dinv = hessian_factor(c, r);
     float mg = solve_ldl(c, grad, Dinv);
     it++;
     float improvement = scale * (oldcost - cost);
@@ -1061,9 +1074,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   com_crb_m(c, s, ls, B, cm);
   /* factor M (copy of rows) */
   float X[CAP];
-#pragma unroll
-  for (int e = 0; e < CAP; e++) X[e] = (c.l < c.nv) ? L->M[c.l][e] : 0.f;
-  float DinvM = factor_ldl(c, X);
+  float Xd = load_mrow(c, X);
+  float DinvM = factor_ldl(c, X, Xd);
   /* velocities */
   if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < c.nv ? ls.v : 0.f;
   tsync();
@@ -1667,6 +1679,14 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
     if (isd && k != l && dk > c.ddep && m->dof_anc[k][c.ddep] == l) desc |= 1u << k;
   }
   c.desc = desc;
+  uint32_t rm = 0;
+  for (int g = 0; g < c.ngeom; g++) {
+    int kd = m->body_lastdof[m->geom_body[g]];
+    if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm |= 0xFFFFu << (16 * g);
+  }
+  c.rowmask = rm;
+  c.dk0 = isd ? l - m->body_dofadr[c.dbody] : 0;
+  c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
 }
 
 /* ---------------------------------- kernels --------------------------------- */
@@ -1830,8 +1850,8 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   /* smooth dynamics: qfrc_bias and qacc_smooth recomputed on the same state */
   {
     float X[CAP];
-    for (int ee = 0; ee < CAP; ee++) X[ee] = (l < c.nv) ? L->M[l][ee] : 0.f;
-    float Dinv = factor_ldl(c, X);
+    float Xd = load_mrow(c, X);
+    float Dinv = factor_ldl(c, X, Xd);
     if (l < 32) L->vec[V_QVEL][l] = l < c.nv ? ls.v : 0.f;
     tsync();
     com_vel(c, B);
