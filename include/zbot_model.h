@@ -28,7 +28,7 @@ extern "C" {
 #endif
 
 #define ZB_MODEL_MAGIC   0x5A424F54u /* 'ZBOT' */
-#define ZB_MODEL_VERSION 3
+#define ZB_MODEL_VERSION 4
 
 #define ZB_MAX_BODY  32
 #define ZB_MAX_DOF   32
@@ -142,6 +142,21 @@ typedef struct ZbModel {
   int32_t  body_right_foot; /* "Right_Foot" */
   int32_t  geom_left_foot;  /* touch sensor zone of left_foot site */
   int32_t  geom_right_foot;
+
+  /* derived topology tables (filled by the descriptor compiler, read by the
+     HIP engine so no per-launch scans are needed) */
+  int32_t  max_body_depth;
+  int32_t  mrow_size;                  /* packed depth-indexed row storage (floats) */
+  int32_t  pad_tab[2];
+  int32_t  body_nchild[ZB_MAX_BODY];
+  int32_t  body_child[ZB_MAX_BODY][8]; /* -1 padded */
+  int32_t  depth_maxchild[16];         /* max #children over bodies at a depth */
+  uint32_t dof_desc[ZB_MAX_DOF];       /* bitmask of strict descendant dofs */
+  uint32_t dof_ancpk[ZB_MAX_DOF][4];   /* dof_anc as bytes: byte (e&3) of word e>>2 */
+  uint32_t dof_rowmask[ZB_MAX_DOF];    /* contact rows (16 per geom) whose chain holds the dof */
+  int32_t  dof_act[ZB_MAX_DOF];        /* actuator driving the dof or -1 */
+  int32_t  dof_rowoff[ZB_MAX_DOF];     /* offset of the dof's row in packed storage */
+  int32_t  geom_lastdof[ZB_MAX_GEOM];
 
   /* task constants: JOINT_BIASES (train.py:61-82), ctrl order */
   float    joint_bias[ZB_MAX_ACT];

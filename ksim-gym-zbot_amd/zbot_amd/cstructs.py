@@ -16,7 +16,7 @@ MAX_ACT = 32
 CON_PER_GEOM = 4
 
 MODEL_MAGIC = 0x5A424F54
-MODEL_VERSION = 3
+MODEL_VERSION = 4
 
 JNT_NONE = -1
 JNT_FREE = 0
@@ -190,6 +190,18 @@ class ZbModel(C.Structure):
         ("body_right_foot", C.c_int32),
         ("geom_left_foot", C.c_int32),
         ("geom_right_foot", C.c_int32),
+        ("max_body_depth", C.c_int32),
+        ("mrow_size", C.c_int32),
+        ("pad_tab", _i(2)),
+        ("body_nchild", _i(MAX_BODY)),
+        ("body_child", _i(MAX_BODY, 8)),
+        ("depth_maxchild", _i(16)),
+        ("dof_desc", C.c_uint32 * MAX_DOF),
+        ("dof_ancpk", (C.c_uint32 * 4) * MAX_DOF),
+        ("dof_rowmask", C.c_uint32 * MAX_DOF),
+        ("dof_act", _i(MAX_DOF)),
+        ("dof_rowoff", _i(MAX_DOF)),
+        ("geom_lastdof", _i(MAX_GEOM)),
         ("joint_bias", _f(MAX_ACT)),
         ("joint_weight", _f(MAX_ACT)),
         ("pad_end", _f(4)),

@@ -27,8 +27,9 @@ def build_library(force: bool = False) -> str:
     """Compile libzbot_hip.so in-tree for gfx950 (hipcc; no GPU needed)."""
     import subprocess  # noqa: PLC0415
 
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-C", CSRC_DIR, "-s"], check=True)
+    if force and os.path.exists(LIB_PATH):
+        os.remove(LIB_PATH)
+    subprocess.run(["make", "-C", CSRC_DIR, "-s"], check=True)  # no-op when up to date
     return LIB_PATH
 
 

@@ -482,6 +482,8 @@ def compile_model(desc: dict | str | None = None) -> CompiledModel:
     m.geom_left_foot = geom_names.index(sites[m.site_left_foot]["touch_geom"])
     m.geom_right_foot = geom_names.index(sites[m.site_right_foot]["touch_geom"])
 
+    _fill_tables(m, bodies, nbody, nv, dof_depth, dof_anc, dof_parent, [m.geom_body[g] for g in range(len(geoms))])
+
     if nu != cs.NJ or nbody != cs.NBODY_TASK:
         raise ValueError(f"the Z-Bot task layout needs nu=20, nbody=26 (got nu={nu}, nbody={nbody})")
 
@@ -499,6 +501,60 @@ def compile_model(desc: dict | str | None = None) -> CompiledModel:
         site_names=site_names,
         cmodel=m,
     )
+
+
+def _fill_tables(m, bodies, nbody, nv, dof_depth, dof_anc, dof_parent, geom_body) -> None:
+    """Derived topology tables consumed by the HIP engine (zbot_model.h)."""
+    depth = [b.depth for b in bodies]
+    m.max_body_depth = max(depth)
+    if m.max_body_depth >= 16:
+        raise ValueError("body depth must be < 16")
+    for b in range(cs.MAX_BODY):
+        for k in range(8):
+            m.body_child[b][k] = -1
+    maxch = [0] * 16
+    for b in range(nbody):
+        ch = [c for c in range(1, nbody) if bodies[c].parent == b]
+        if len(ch) > 8:
+            raise ValueError(f"body {bodies[b].name} has more than 8 children")
+        m.body_nchild[b] = len(ch)
+        for k, c in enumerate(ch):
+            m.body_child[b][k] = c
+        maxch[depth[b]] = max(maxch[depth[b]], len(ch))
+    for d in range(16):
+        m.depth_maxchild[d] = maxch[d]
+    lastdof = [b.lastdof for b in bodies]
+    glast = [lastdof[g] for g in geom_body]
+    off = 0
+    for d in range(nv):
+        desc = 0
+        for k in range(nv):
+            if k != d and dof_depth[k] > dof_depth[d] and dof_anc[k, dof_depth[d]] == d:
+                desc |= 1 << k
+        m.dof_desc[d] = desc
+        for w in range(4):
+            v = 0
+            for bb in range(4):
+                e = 4 * w + bb
+                a = int(dof_anc[d, e]) if e < cs.MAX_DEPTH else -1
+                v |= (a if a >= 0 else 0) << (8 * bb)
+            m.dof_ancpk[d][w] = v
+        rm = 0
+        for g, kd in enumerate(glast):
+            if kd >= 0 and (kd == d or (desc >> kd) & 1):
+                rm |= 0xFFFF << (16 * g)
+        m.dof_rowmask[d] = rm
+        m.dof_act[d] = -1
+        m.dof_rowoff[d] = off
+        off += 4 * ((int(dof_depth[d]) + 1 + 3) // 4)
+    for d in range(nv, cs.MAX_DOF):
+        m.dof_act[d] = -1
+        m.dof_rowoff[d] = off
+    for a in range(m.nu):
+        m.dof_act[m.act_dof[a]] = a
+    m.mrow_size = off
+    for g, kd in enumerate(glast):
+        m.geom_lastdof[g] = kd
 
 
 def C_sizeof(t: type) -> int:  # noqa: N802

@@ -43,6 +43,7 @@ def lib(precision: str = "f32") -> C.CDLL:
     L.zbo_simulate.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, C.c_int]
     L.zbo_trapezoidal_step.argtypes = [fp, fp, fp, C.c_float, fp, fp, C.c_int, fp, fp]
     L.zbo_rotate_quat_by_quat.argtypes = [fp, fp, C.c_int, fp]
+    L.zbo_feetech.argtypes = [C.c_void_p, C.c_float, fp, fp, fp, fp, fp, fp, fp, fp]
     L.zbo_synthetic_actions.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_uint32, C.c_float, fp]
     L.zbo_field_offset.argtypes = [C.c_int, C.c_char_p]
     L.zbo_field_offset.restype = C.c_long
@@ -63,6 +64,31 @@ def threefry2x32(k0: int, k1: int, c0: int, c1: int) -> tuple[int, int]:
     out = (C.c_uint32 * 2)()
     lib().zbo_threefry2x32(k0 & 0xFFFFFFFF, k1 & 0xFFFFFFFF, c0 & 0xFFFFFFFF, c1 & 0xFFFFFFFF, out)
     return out[0], out[1]
+
+
+def trapezoidal_step(pos, vel, target, dt, vmax, amax):
+    pos, vel, target, vmax, amax = (np.ascontiguousarray(x, dtype=np.float32) for x in (pos, vel, target, vmax, amax))
+    n = pos.shape[0]
+    npos = np.zeros(n, np.float32)
+    nvel = np.zeros(n, np.float32)
+    lib().zbo_trapezoidal_step(_p(pos), _p(vel), _p(target), dt, _p(vmax), _p(amax), n, _p(npos), _p(nvel))
+    return npos, nvel
+
+
+def feetech(cmodel, dt, plan_pos, plan_vel, action, q, qd):
+    arrs = [np.ascontiguousarray(x, dtype=np.float32) for x in (plan_pos, plan_vel, action, q, qd)]
+    n = cmodel.nu
+    npos, nvel, tau = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    lib().zbo_feetech(C.byref(cmodel), dt, *[_p(a) for a in arrs], _p(npos), _p(nvel), _p(tau))
+    return npos, nvel, tau
+
+
+def rotate_quat_by_quat(q, r, inverse=False):
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    r = np.ascontiguousarray(r, dtype=np.float32)
+    out = np.zeros(4, np.float32)
+    lib().zbo_rotate_quat_by_quat(_p(q), _p(r), int(inverse), _p(out))
+    return out
 
 
 def synthetic_actions(cmodel, seed: int, n: int, env_offset: int, t: int, std: float = 0.05) -> np.ndarray:

@@ -1004,6 +1004,18 @@ static void feetech_ctrl(const ZbModel* m, ZbData* d, float* plan_pos, float* pl
   }
 }
 
+/* FeetechActuators.get_stateful_ctrl on raw arrays (KAT entry point) */
+void zbo_feetech(const ZbModel* m, float dt, const float* plan_pos, const float* plan_vel, const float* action,
+                 const float* q, const float* qd, float* npos, float* nvel, float* tau) {
+  zbo_trapezoidal_step(plan_pos, plan_vel, action, dt, m->fe_vmax, m->fe_amax, m->nu, npos, nvel);
+  for (int a = 0; a < m->nu; a++) {
+    real duty = (real)m->fe_kp[a] * m->fe_error_gain[a] * ((real)npos[a] - q[a]) + (real)m->fe_kd[a] * ((real)nvel[a] - qd[a]);
+    if (duty < -m->fe_max_pwm[a]) duty = -m->fe_max_pwm[a];
+    if (duty > m->fe_max_pwm[a]) duty = m->fe_max_pwm[a];
+    tau[a] = (float)(duty * m->fe_vin[a] * m->fe_kt[a] / m->fe_R[a]);
+  }
+}
+
 /* ------------------------------- quaternions (train.py) ---------------------- */
 /* rotate_quat_by_quat, train.py:751-787 */
 static void rotate_quat_by_quat(const real qr_[4], const real rq_[4], int inverse, real out[4]) {
@@ -1538,6 +1550,9 @@ static const FieldOff model_fields[] = {
     OFF(ZbModel, site_body), OFF(ZbModel, site_pos), OFF(ZbModel, site_quat), OFF(ZbModel, site_imu),
     OFF(ZbModel, site_left_foot), OFF(ZbModel, site_right_foot), OFF(ZbModel, body_base), OFF(ZbModel, body_left_foot),
     OFF(ZbModel, body_right_foot), OFF(ZbModel, geom_left_foot), OFF(ZbModel, geom_right_foot),
+    OFF(ZbModel, max_body_depth), OFF(ZbModel, mrow_size), OFF(ZbModel, pad_tab), OFF(ZbModel, body_nchild),
+    OFF(ZbModel, body_child), OFF(ZbModel, depth_maxchild), OFF(ZbModel, dof_desc), OFF(ZbModel, dof_ancpk),
+    OFF(ZbModel, dof_rowmask), OFF(ZbModel, dof_act), OFF(ZbModel, dof_rowoff), OFF(ZbModel, geom_lastdof),
     OFF(ZbModel, joint_bias), OFF(ZbModel, joint_weight), OFF(ZbModel, pad_end),
 };
 static const FieldOff config_fields[] = {

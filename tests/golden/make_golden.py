@@ -1,0 +1,59 @@
+"""Generate the committed golden vectors from the CPU oracle (fp32 build).
+
+    python tests/golden/make_golden.py
+
+The reference (JAX/MJX/ksim) cannot run in this container, so
+the fixtures pin the build's own oracle: a C1-shaped rollout (32 envs x 16
+env-steps, seed 0, default train.py configuration incl. observation noise) and
+a domain-randomized + push variant (configs 3/5 features). Tests re-run the
+oracle against them (regression pin) and compare the HIP engine to them.
+"""
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle as O  # noqa: E402
+from zbot_amd import compile_model, default_config  # noqa: E402
+
+CASES = {
+    "c1_seed0": dict(n=32, steps=16, seed=0, push=False, randomize=False, std=0.05),
+    "c5_push_seed1": dict(n=16, steps=16, seed=1, push=True, randomize=True, std=0.1),
+}
+
+
+def run_case(name, n, steps, seed, push, randomize, std):
+    cm = compile_model()
+    cfg = default_config(push=push, randomize=randomize)
+    env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
+    oa0, oc0, _ = env.reset()
+    rewards, dones, actions = [], [], []
+    for t in range(steps):
+        a = O.synthetic_actions(cm.cmodel, seed, n, 0, t, std=std)
+        out = env.step(a)
+        actions.append(a)
+        rewards.append(out["reward"])
+        dones.append(out["done"])
+    return dict(
+        reset_obs_actor=oa0, reset_obs_critic=oc0, actions=np.stack(actions), reward=np.stack(rewards),
+        done=np.stack(dones), final_state=env.state.copy(), final_rand=env.rand.copy(),
+        final_obs_actor=out["obs_actor"], final_obs_critic=out["obs_critic"], final_terms=out["reward_terms"],
+        stats=env.stats.copy(),
+    )
+
+
+def main():
+    for name, kw in CASES.items():
+        data = run_case(name, **kw)
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **data, **{f"cfg_{k}": v for k, v in kw.items()})
+        print(name, {k: v.shape for k, v in data.items()})
+
+
+if __name__ == "__main__":
+    main()

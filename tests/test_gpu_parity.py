@@ -1,0 +1,245 @@
+"""HIP engine (libzbot_hip.so, called through the C ABI) vs the CPU oracle.
+
+Tolerances (fp32 engine vs fp32/fp64 oracle; the reference computes in fp32):
+  * per-stage forward quantities: |gpu - oracle_f64| <= 1e-4 * max(|ref|, scale)
+  * one env-step from identical state: qpos 1e-4 abs, qvel 1e-2 abs,
+    observations/reward 1e-3 abs, done exact
+  * multi-step rollouts (contact dynamics are chaotic): rewards 1e-2 abs over
+    the first 8 steps, done flags equal
+  * integer/bookkeeping outputs (done, counters, RNG-driven resets): exact
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from zbot_amd import cstructs as cs
+from zbot_amd import default_config
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def engine(cm, cfg, n, **kw):
+    from zbot_amd.engine import HipEngine
+
+    return HipEngine(cm, cfg, n, **kw)
+
+
+def warm_states(O, cm, cfg, n, steps=20, seed=7, std=0.05):
+    env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
+    env.reset()
+    for t in range(steps):
+        env.step(O.synthetic_actions(cm.cmodel, seed, n, 0, t, std=std))
+    return env
+
+
+def close(a, b, scale):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.abs(a - b) <= 1e-4 * np.maximum(np.abs(b), scale)
+
+
+def test_engine_loads_native_library(torch_gpu, cmodel):
+    from zbot_amd import engine as E
+
+    eng = engine(cmodel, default_config(), 4)
+    assert E._lib is not None and os.path.basename(E.LIB_PATH) == "libzbot_hip.so"
+    del eng
+
+
+def test_forward_stages_match_oracle(torch_gpu, cmodel, oracle_mod):
+    torch = torch_gpu
+    from zbot_amd.engine import DBG
+
+    cfg = default_config()
+    n = 48
+    env = warm_states(oracle_mod, cmodel, cfg, n)
+    st = env.state.copy()
+    rng = np.random.default_rng(0)
+    # perturb a third of the envs: deeper penetration, violated joint limits, fast joints
+    st[16:32, 2] -= 0.004
+    st[32:48, 7 + 3] = -2.3  # right knee beyond its lower limit (-2.2)
+    st[32:48, 32 + 6:32 + 26] += rng.normal(scale=2.0, size=(16, 20)).astype(np.float32)
+    st[:, cs.S_QACCW:cs.S_QACCW + 32] = 0.0
+    ctrl = (rng.normal(size=(n, 20)) * 1.5).astype(np.float32)
+    eng = engine(cmodel, cfg, n)
+    dbg = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()
+    nv, nb = 26, 26
+    for e in range(n):
+        ref = oracle_mod.forward_debug(cmodel.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
+        g = dbg[e]
+        qM = g[DBG["qM"]:DBG["qM"] + nv * nv].reshape(nv, nv)
+        assert close(qM, ref["qM"], 1e-3).all(), e
+        assert close(g[DBG["bias"]:DBG["bias"] + nv], ref["qfrc_bias"], 1e-2).all(), e
+        assert close(g[DBG["qacc_smooth"]:DBG["qacc_smooth"] + nv], ref["qacc_smooth"], 10.0).all(), e
+        assert close(g[DBG["xpos"]:DBG["xpos"] + 3 * nb].reshape(nb, 3), ref["xpos"], 1e-2).all(), e
+        assert close(g[DBG["cinert"]:DBG["cinert"] + 10 * nb].reshape(nb, 10), ref["cinert"], 1e-3).all(), e
+        assert close(g[DBG["cvel"]:DBG["cvel"] + 6 * nb].reshape(nb, 6), ref["cvel"], 1e-1).all(), e
+        assert int(g[DBG["misc"]]) == ref["nefc"], e
+        assert int(g[DBG["misc"] + 1]) == ref["ncon"], e
+        # constrained acceleration: solver in fp32 vs fp64, 8 Newton iterations
+        qa = g[DBG["qacc"]:DBG["qacc"] + nv]
+        assert np.abs(qa - ref["qacc"]).max() <= 1e-3 * max(1.0, np.abs(ref["qacc"]).max()), e
+        np.testing.assert_allclose(g[DBG["misc"] + 2:DBG["misc"] + 4], ref["touch"], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("push,randomize", [(False, False), (True, False), (False, True), (True, True)])
+def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize):
+    torch = torch_gpu
+    cfg = default_config(push=push, randomize=randomize)
+    n = 64
+    env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
+    eng = engine(cmodel, cfg, n, seed=7)
+    for t in range(3):
+        eng.set_state(torch.from_numpy(env.state.copy()))
+        eng.set_rand(torch.from_numpy(env.rand.copy()))
+        a = oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100 + t)
+        ref = env.step(a)
+        out = eng.step(torch.from_numpy(a).cuda())
+        torch.cuda.synchronize()
+        gs = eng.get_state().cpu().numpy()
+        np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
+        np.testing.assert_allclose(gs[:, :27], env.state[:, :27], atol=1e-4)
+        np.testing.assert_allclose(gs[:, 32:58], env.state[:, 32:58], atol=1e-2)
+        np.testing.assert_allclose(gs[:, cs.S_PLAN_POS:cs.S_PLAN_TAU + 20], env.state[:, cs.S_PLAN_POS:cs.S_PLAN_TAU + 20],
+                                   atol=1e-2)
+        np.testing.assert_allclose(out["obs_actor"].cpu().numpy(), ref["obs_actor"], atol=1e-3)
+        np.testing.assert_allclose(out["obs_critic"].cpu().numpy(), ref["obs_critic"], atol=2e-2, rtol=1e-3)
+        np.testing.assert_allclose(out["obs_extra"].cpu().numpy()[:, :67], ref["obs_extra"][:, :67], atol=5e-2,
+                                   rtol=1e-2)
+        np.testing.assert_allclose(out["reward"].cpu().numpy(), ref["reward"], atol=1e-3)
+        np.testing.assert_allclose(out["reward_terms"].cpu().numpy(), ref["reward_terms"], atol=1e-3)
+        # integer bookkeeping is exact
+        for w in (cs.S_EP_STEPS, cs.S_RNG_STEP, cs.S_EPISODE):
+            assert np.array_equal(gs[:, w].view(np.uint32), env.state[:, w].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["c1_seed0", "c5_push_seed1"])
+def test_golden_rollout(torch_gpu, cmodel, name):
+    torch = torch_gpu
+    g = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
+    n, steps, seed = int(g["cfg_n"]), int(g["cfg_steps"]), int(g["cfg_seed"])
+    cfg = default_config(push=bool(g["cfg_push"]), randomize=bool(g["cfg_randomize"]))
+    eng = engine(cmodel, cfg, n, seed=seed)
+    out = eng.reset()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out["obs_actor"].cpu().numpy(), g["reset_obs_actor"], atol=1e-4)
+    np.testing.assert_allclose(out["obs_critic"].cpu().numpy(), g["reset_obs_critic"], atol=1e-3, rtol=1e-4)
+    rew, done = [], []
+    for t in range(steps):
+        o = eng.step(torch.from_numpy(g["actions"][t]).cuda())
+        rew.append(o["reward"].cpu().numpy().copy())
+        done.append(o["done"].cpu().numpy().copy())
+    rew, done = np.stack(rew), np.stack(done)
+    np.testing.assert_array_equal(done, g["done"])
+    np.testing.assert_allclose(rew[:8], g["reward"][:8], atol=1e-2)
+    gs = eng.get_state().cpu().numpy()
+    np.testing.assert_allclose(gs[:, :3], g["final_state"][:, :3], atol=1e-2)
+    np.testing.assert_allclose(eng.get_rand().cpu().numpy(), g["final_rand"], atol=1e-6)
+
+
+def test_deterministic_and_shard_invariant(torch_gpu, cmodel, oracle_mod):
+    torch = torch_gpu
+    cfg = default_config()
+    n = 64
+    acts = [torch.from_numpy(oracle_mod.synthetic_actions(cmodel.cmodel, 5, n, 0, t, std=0.1)).cuda() for t in range(6)]
+    states = []
+    for _ in range(2):
+        eng = engine(cmodel, cfg, n, seed=5)
+        eng.reset()
+        for a in acts:
+            eng.step(a)
+        states.append(eng.get_state().cpu().numpy())
+    assert np.array_equal(states[0], states[1])
+    half = engine(cmodel, cfg, n // 2, env_offset=n // 2, seed=5)
+    half.reset()
+    for a in acts:
+        half.step(a[n // 2:].contiguous())
+    assert np.array_equal(half.get_state().cpu().numpy(), states[0][n // 2:])
+
+
+def test_rollout_launch_equals_steps(torch_gpu, cmodel, oracle_mod):
+    torch = torch_gpu
+    cfg = default_config()
+    n, T = 32, 5
+    A = torch.from_numpy(np.stack([oracle_mod.synthetic_actions(cmodel.cmodel, 9, n, 0, t) for t in range(T)])).cuda()
+    a = engine(cmodel, cfg, n, seed=9)
+    b = engine(cmodel, cfg, n, seed=9)
+    a.reset()
+    b.reset()
+    for t in range(T):
+        a.step(A[t])
+    rsum = torch.zeros(n, device="cuda")
+    b.rollout(A, reward_sum=rsum)
+    torch.cuda.synchronize()
+    assert np.array_equal(a.get_state().cpu().numpy(), b.get_state().cpu().numpy())
+    np.testing.assert_allclose(b.obs_actor.cpu().numpy(), a.obs_actor.cpu().numpy(), atol=0)
+
+
+def test_reset_mask_and_autoreset(torch_gpu, cmodel, oracle_mod):
+    torch = torch_gpu
+    cfg = default_config(obs_noise=False)
+    n = 16
+    eng = engine(cmodel, cfg, n, seed=2)
+    eng.reset()
+    a = torch.from_numpy(oracle_mod.synthetic_actions(cmodel.cmodel, 2, n, 0, 0)).cuda()
+    eng.step(a)
+    before = eng.get_state().cpu().numpy()
+    mask = torch.zeros(n, dtype=torch.uint8)
+    mask[::2] = 1
+    eng.reset(mask=mask)
+    after = eng.get_state().cpu().numpy()
+    assert np.array_equal(after[1::2], before[1::2])
+    reset_q = cmodel.reset_qpos().astype(np.float32)
+    np.testing.assert_allclose(after[::2, :27], np.tile(reset_q, (n // 2, 1)), atol=1e-6)
+    # force a BadZ termination (train.py:1590) on env 3 -> done + auto-reset
+    st = eng.get_state()
+    st[3, 2] = 0.02
+    eng.set_state(st)
+    out = eng.step(a)
+    torch.cuda.synchronize()
+    d = out["done"].cpu().numpy()
+    assert d[3] == 1 and d.sum() == 1
+    s2 = eng.get_state().cpu().numpy()
+    np.testing.assert_allclose(s2[3, 7:27], reset_q[7:], atol=1e-6)
+    assert s2[3, cs.S_EP_STEPS].view(np.uint32) == 0
+    stats = eng.get_stats().cpu().numpy()
+    assert stats[3, cs.ST_DONE] == 1.0 and stats[:, cs.ST_DONE].sum() == 1.0
+
+
+def test_full_size_properties(torch_gpu, cmodel):
+    torch = torch_gpu
+    cfg = default_config()
+    n = 8192
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    bias = torch.tensor([cmodel.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    acts = [bias + 0.05 * torch.randn(n, 20, device="cuda", generator=g) for _ in range(8)]
+    sums = []
+    for _ in range(2):
+        eng = engine(cmodel, cfg, n, seed=1)
+        eng.reset()
+        for a in acts:
+            out = eng.step(a)
+        st = eng.get_state()
+        assert torch.isfinite(st[:, :58]).all()
+        assert torch.isfinite(out["obs_critic"]).all()
+        q = st[:, 3:7]
+        assert torch.allclose(q.norm(dim=1), torch.ones(n, device="cuda"), atol=2e-6)
+        sums.append(float(st[:, :58].double().sum().item()))
+        assert (st[:, cs.S_NAN].view(torch.int32) == 0).all()
+    assert sums[0] == sums[1]  # bit-reproducible at fixed seed
+    # standing task: almost all envs still alive and near the reset height
+    z = st[:, 2]
+    assert (z > 0.2).float().mean().item() > 0.95

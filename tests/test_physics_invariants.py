@@ -1,0 +1,143 @@
+"""Physics invariants of the CPU oracle.
+
+The oracle restates MuJoCo's pipeline (un-vendored, parity unpinned); these
+tests pin it against independent float64 computations in zbot_amd.model
+(Jacobian-based mass matrix / gravity) and against closed-form dynamics.
+"""
+
+import numpy as np
+import pytest
+
+from zbot_amd import cstructs as cs
+from zbot_amd import default_config
+from zbot_amd.model import _kinematics, _point_jacobian, mass_matrix
+
+
+def _model_copy(m):
+    return type(m).from_buffer_copy(m)
+
+
+def _random_qpos(cm, rng, scale=0.3):
+    q = cm.reset_qpos().copy()
+    q[7:] += rng.uniform(-scale, scale, size=20)
+    quat = rng.normal(size=4)
+    quat /= np.linalg.norm(quat)
+    q[3:7] = quat
+    q[2] = 1.0
+    return q
+
+
+def test_free_fall_exact(oracle_mod, cmodel):
+    cfg = default_config()
+    q = cmodel.reset_qpos().astype(np.float32)
+    q[2] = 2.0
+    n = 100
+    qp, qv, _ = oracle_mod.simulate(cmodel.cmodel, cfg, q, np.zeros(26), n, precision="f64")
+    dt = 0.001
+    assert qp[2] == pytest.approx(2.0 - 9.81 * dt * dt * n * (n + 1) / 2, abs=1e-6)
+    assert qv[2] == pytest.approx(-9.81 * dt * n, rel=1e-5)
+    np.testing.assert_allclose(qv[6:], 0.0, atol=1e-5)
+    np.testing.assert_allclose(qp[7:], q[7:], atol=1e-6)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_mass_matrix_matches_jacobian_form(oracle_mod, cmodel, seed):
+    rng = np.random.default_rng(seed)
+    q = _random_qpos(cmodel, rng)
+    cfg = default_config()
+    d = oracle_mod.forward_debug(cmodel.cmodel, cfg, q, np.zeros(26), precision="f64")
+    arm = np.array([cmodel.cmodel.dof_armature[i] for i in range(26)])
+    M_ref = mass_matrix(cmodel.bodies, q, 26, cmodel.dof_body, arm)
+    M = d["qM"].astype(np.float64)
+    np.testing.assert_allclose(M, M_ref, rtol=1e-5, atol=1e-7)
+    assert np.abs(M - M.T).max() == 0.0
+    assert np.linalg.eigvalsh(M).min() > 0.0
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_gravity_bias_matches_jacobian_form(oracle_mod, cmodel, seed):
+    rng = np.random.default_rng(seed)
+    q = _random_qpos(cmodel, rng)
+    cfg = default_config()
+    d = oracle_mod.forward_debug(cmodel.cmodel, cfg, q, np.zeros(26), precision="f64")
+    xpos, xmat = _kinematics(cmodel.bodies, q)
+    g = np.array([0.0, 0.0, -9.81])
+    bias = np.zeros(26)
+    for i, b in enumerate(cmodel.bodies):
+        if i == 0:
+            continue
+        com = xpos[i] + xmat[i] @ b.ipos
+        jp, _ = _point_jacobian(cmodel.bodies, xpos, xmat, 26, cmodel.dof_body, i, com)
+        bias -= b.mass * jp.T @ g
+    np.testing.assert_allclose(d["qfrc_bias"], bias, rtol=1e-5, atol=1e-6)
+
+
+def _conservative_model(cmodel):
+    m = _model_copy(cmodel.cmodel)
+    for i in range(26):
+        m.dof_damping[i] = 0.0
+        m.dof_frictionloss[i] = 0.0
+        m.dof_limited[i] = 0
+    m.gravity[2] = 0.0
+    return m
+
+
+def test_energy_and_momentum_conservation(oracle_mod, cmodel):
+    m = _conservative_model(cmodel)
+    cfg = default_config()
+    rng = np.random.default_rng(5)
+    q = cmodel.reset_qpos().astype(np.float64)
+    q[2] = 3.0
+    v = rng.normal(scale=0.3, size=26)
+    d0 = oracle_mod.forward_debug(m, cfg, q, v, precision="f64")
+    M0 = d0["qM"].astype(np.float64)
+    ke0 = 0.5 * v @ M0 @ v
+    p0 = (M0 @ v)[:3]
+    qp, qv, _ = oracle_mod.simulate(m, cfg, q, v, 400, precision="f64")
+    d1 = oracle_mod.forward_debug(m, cfg, qp, qv, precision="f64")
+    M1 = d1["qM"].astype(np.float64)
+    qv = qv.astype(np.float64)
+    ke1 = 0.5 * qv @ M1 @ qv
+    p1 = (M1 @ qv)[:3]
+    assert ke1 == pytest.approx(ke0, rel=2e-2)
+    np.testing.assert_allclose(p1, p0, rtol=1e-3, atol=1e-5)
+
+
+def test_static_stand_supports_weight(oracle_mod, cmodel):
+    cfg = default_config(obs_noise=False)
+    env = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 4, seed=0)
+    env.reset()
+    bias = np.array([cmodel.cmodel.joint_bias[a] for a in range(20)], np.float32)
+    for _ in range(30):
+        out = env.step(np.tile(bias, (4, 1)))
+    assert not out["done"].any()
+    total_mass = cmodel.cmodel.body_mass[1][1]
+    touch = env.state[:, cs.S_TOUCH] + env.state[:, cs.S_TOUCH + 1]
+    np.testing.assert_allclose(touch, total_mass * 9.81, rtol=0.15)
+    # standing height stays near the reset height
+    np.testing.assert_allclose(env.state[:, 2], cmodel.qpos0[2], atol=0.01)
+
+
+def test_quaternion_norm_preserved(oracle_mod, cmodel):
+    cfg = default_config()
+    env = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 8, seed=1)
+    env.reset()
+    for t in range(10):
+        env.step(oracle_mod.synthetic_actions(cmodel.cmodel, 1, 8, 0, t, std=0.2))
+    norms = np.linalg.norm(env.state[:, 3:7], axis=1)
+    np.testing.assert_allclose(norms, 1.0, atol=2e-6)
+
+
+def test_f32_oracle_tracks_f64(oracle_mod, cmodel):
+    """The fp32 oracle (CPU baseline) stays close to the fp64 build for one env-step."""
+    cfg = default_config(obs_noise=False)
+    a = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 8, seed=2)
+    b = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 8, seed=2, precision="f64")
+    a.reset()
+    b.reset()
+    for t in range(3):
+        act = oracle_mod.synthetic_actions(cmodel.cmodel, 2, 8, 0, t)
+        a.step(act)
+        b.step(act)
+    np.testing.assert_allclose(a.state[:, :27], b.state[:, :27], atol=2e-5)
+    np.testing.assert_allclose(a.state[:, 32:58], b.state[:, 32:58], atol=5e-3)
