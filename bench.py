@@ -181,7 +181,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "zb::step_kernel<false>",
+                "kernel": "zb::step_kernel",
                 "kernel_avg_ms": avg_ms,
                 "algorithmic_bytes_per_env_step": bpe,
                 "note": "the path is FP32-VALU/latency bound (DESIGN.md §Roofline); HBM fraction reported as required",

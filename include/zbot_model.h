@@ -28,7 +28,7 @@ extern "C" {
 #endif
 
 #define ZB_MODEL_MAGIC   0x5A424F54u /* 'ZBOT' */
-#define ZB_MODEL_VERSION 4
+#define ZB_MODEL_VERSION 5
 
 #define ZB_MAX_BODY  32
 #define ZB_MAX_DOF   32
@@ -157,6 +157,13 @@ typedef struct ZbModel {
   int32_t  dof_act[ZB_MAX_DOF];        /* actuator driving the dof or -1 */
   int32_t  dof_rowoff[ZB_MAX_DOF];     /* offset of the dof's row in packed storage */
   int32_t  geom_lastdof[ZB_MAX_GEOM];
+  /* elimination levels of the sparse L'DL (level = height of the dof in the
+     dof tree; dofs of one level are never ancestor/descendant of each other,
+     so they are eliminated together) */
+  int32_t  nlevel;
+  int32_t  pad_lvl[3];
+  int32_t  level_nmem[ZB_MAX_DEPTH];
+  int32_t  level_mem[ZB_MAX_DEPTH][8];
 
   /* task constants: JOINT_BIASES (train.py:61-82), ctrl order */
   float    joint_bias[ZB_MAX_ACT];

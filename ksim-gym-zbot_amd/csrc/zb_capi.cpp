@@ -30,6 +30,7 @@ struct ZbHandle {
   float* rnd;
   float* stats;
   int32_t* iters;
+  float* stamps; /* ZB_STAMPS diagnostic build only */
 };
 
 static thread_local std::string g_err;
@@ -175,6 +176,9 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMemset(h->rnd, 0, n * ZB_RAND_STRIDE * sizeof(float));
   if (e == hipSuccess) e = hipMemset(h->stats, 0, n * ZB_NUM_STATS * sizeof(float));
   if (e == hipSuccess) e = hipMemset(h->iters, 0, n * sizeof(int32_t));
+#ifdef ZB_STAMPS
+  if (e == hipSuccess) e = hipMalloc(&h->stamps, n * 16 * sizeof(unsigned long long));
+#endif
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     zb_destroy(h);
@@ -192,6 +196,7 @@ int zb_destroy(ZbHandle* h) {
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->stats) (void)hipFree(h->stats);
   if (h->iters) (void)hipFree(h->iters);
+  if (h->stamps) (void)hipFree(h->stamps);
   delete h;
   return ZB_OK;
 }
@@ -208,6 +213,7 @@ static zb::StepArgs base_args(ZbHandle* h) {
   a.rnd = h->rnd;
   a.stats = h->stats;
   a.iters = h->iters;
+  a.dbg = h->stamps;
   a.nsteps = 1;
   a.curriculum = 1.f;
   return a;
@@ -314,5 +320,12 @@ int zb_debug_forward(ZbHandle* h, float* state_dev, const float* ctrl_dev, float
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_debug_forward launch: %s", hipGetErrorString(e));
   return ZB_OK;
 }
+
+#ifdef ZB_STAMPS
+int zb_get_stamps(ZbHandle* h, void* out_dev, void* stream) {
+  if (!h || !h->stamps) return fail(ZB_EARG, "no stamps");
+  return copy_rows(h, out_dev, h->stamps, (size_t)h->n * 16 * sizeof(unsigned long long), stream);
+}
+#endif
 
 }  // extern "C"

@@ -44,38 +44,94 @@ constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0)
 enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3 };
 
 /* per-environment LDS working set (8.6 KB) */
+constexpr int MROW = 248; /* packed depth-indexed rows (model.mrow_size <= 240) + read padding */
 struct __align__(16) EnvL {
   float cdof[32][6];
-  float cdofdot[32][6];
   float M[32][CAP];
   float L[32][CAP];
-  float J[32][CAP];
+  union {
+    float J[32][CAP];     /* contact-row Jacobians (constraint phase) */
+    float cdofdot[32][6]; /* velocity phase; recomputed for the sensors */
+  } u;
   float sub[32][10];
   float vec[4][32];
   float rowDA[32];
   float rowF[32];
   float Dk[32];
+#ifdef ZB_STAMPS
+  unsigned long long stamp[16];
+  unsigned long long stamp_last;
+#endif
+};
+
+/* per-block copy of the small topology tables used inside the serial loops
+   (LDS reads instead of dependent scalar/global model loads) */
+struct __align__(16) Sched {
+  int rowoff[32];     /* packed row offset of each dof */
+  int mem[ZB_MAX_DEPTH][8]; /* members of each elimination level (-1 padded) */
+  int memoff[ZB_MAX_DEPTH][8]; /* their packed row offsets */
+  int nmem[ZB_MAX_DEPTH];
+  int nlevel;
+  int pad[3];
 };
 
 /* ----------------------------- team primitives ----------------------------- */
 __device__ __forceinline__ float tsh(float v, int src) { return __shfl(v, src, TEAM); }
 __device__ __forceinline__ int tshi(int v, int src) { return __shfl(v, src, TEAM); }
+/* DPP butterfly within 16-lane rows (quad xor 1, xor 2, half-row mirror, row
+   mirror), then one cross-row exchange (xor 16). Every pairing is symmetric,
+   so all lanes of a team end with the bit-identical result. */
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
 __device__ __forceinline__ float tsum(float v) {
-#pragma unroll
-  for (int o = TEAM / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, TEAM);
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  v += __shfl_xor(v, 16, TEAM);
   return v;
 }
 __device__ __forceinline__ float tmaxf(float v) {
-#pragma unroll
-  for (int o = TEAM / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, TEAM));
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  v = fmaxf(v, __shfl_xor(v, 16, TEAM));
   return v;
 }
 __device__ __forceinline__ int tmaxi(int v) {
-#pragma unroll
-  for (int o = TEAM / 2; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, TEAM));
+  v = max(v, dppi<0xB1>(v));
+  v = max(v, dppi<0x4E>(v));
+  v = max(v, dppi<0x141>(v));
+  v = max(v, dppi<0x140>(v));
+  v = max(v, __shfl_xor(v, 16, TEAM));
   return v;
 }
 __device__ __forceinline__ void tsync() { __syncthreads(); }
+
+/* Diagnostic phase stamps (separate build, -DZB_STAMPS): cycles per phase of the
+   step, accumulated per env; never compiled into the product library. */
+#ifdef ZB_STAMPS
+__device__ __forceinline__ void zb_stamp(EnvL* L, int i) {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if ((threadIdx.x & (TEAM - 1)) == 0) {
+    L->stamp[i] += t - L->stamp_last;
+    L->stamp_last = t;
+  }
+}
+#define STAMP(i) zb_stamp(c.L, i)
+#else
+#define STAMP(i) ((void)0)
+#endif
 
 /* ------------------------------- small math -------------------------------- */
 __device__ __forceinline__ void cross3(float r[3], const float a[3], const float b[3]) {
@@ -203,6 +259,7 @@ struct Ctx {
   const ZbModel* m;
   const ZbEnvConfig* cfg;
   EnvL* L;
+  const Sched* S;
   uint64_t seed;
   uint32_t env;
   int l;
@@ -217,6 +274,8 @@ struct Ctx {
   uint32_t desc; /* strict descendants of dof l */
   uint32_t rowmask; /* contact rows whose Jacobian chain contains dof l */
   int dk0;          /* index of dof l within its body's joint (free joint: 0..5) */
+  int moff;         /* offset of row l in packed M / L storage */
+  int mylevel;      /* elimination level of dof l */
   int dfree;        /* dof l belongs to a free joint */
 };
 
@@ -277,6 +336,21 @@ struct Rows {
   int nrow;
   uint32_t exmask; /* team-uniform: existing contact rows */
 };
+
+/* 16-byte LDS row access (rows are 12 floats = 48 B, 16-B aligned) */
+__device__ __forceinline__ void ld_row(const float* p, float v[CAP]) {
+  const float4* q = reinterpret_cast<const float4*>(p);
+  float4 a = q[0], b = q[1], c4 = q[2];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  v[8] = c4.x; v[9] = c4.y; v[10] = c4.z; v[11] = c4.w;
+}
+__device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
+  float4* q = reinterpret_cast<float4*>(p);
+  q[0] = make_float4(v[0], v[1], v[2], v[3]);
+  q[1] = make_float4(v[4], v[5], v[6], v[7]);
+  q[2] = make_float4(v[8], v[9], v[10], v[11]);
+}
 
 /* ------------------------------- kinematics -------------------------------- */
 __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B) {
@@ -451,11 +525,11 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   for (int k = 0; k < 10; k++) crb[k] = B.ci[k];
   tsync();
   subtree_sum<10>(c, crb);
-  /* M rows: M(j, anc_e(j)) = cdof_anc . (crb_body(j) * cdof_j) */
+  /* M rows: M(j, anc_e(j)) = cdof_anc . (crb_body(j) * cdof_j), packed storage */
   {
     const int j = c.l;
     if (j < c.nv) {
-      float cr[10], cd[6], F[6];
+      float cr[10], cd[6], F[6], mr[CAP];
 #pragma unroll
       for (int k = 0; k < 10; k++) cr[k] = L->sub[c.dbody][k];
 #pragma unroll
@@ -472,29 +546,15 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
           v = dot6(ca, F);
           if (e == c.ddep) v += ls.arm;
         }
-        L->M[j][e] = v;
+        mr[e] = v;
       }
+      st_row(&L->M[j][0], mr);
     }
   }
   tsync();
 }
 
 /* ---------------------- sparse L'DL factor + solves ------------------------ */
-/* 16-byte LDS row access (rows are 12 floats = 48 B, 16-B aligned) */
-__device__ __forceinline__ void ld_row(const float* p, float v[CAP]) {
-  const float4* q = reinterpret_cast<const float4*>(p);
-  float4 a = q[0], b = q[1], c4 = q[2];
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  v[8] = c4.x; v[9] = c4.y; v[10] = c4.z; v[11] = c4.w;
-}
-__device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
-  float4* q = reinterpret_cast<float4*>(p);
-  q[0] = make_float4(v[0], v[1], v[2], v[3]);
-  q[1] = make_float4(v[4], v[5], v[6], v[7]);
-  q[2] = make_float4(v[8], v[9], v[10], v[11]);
-}
-
 /* Sparse L'DL (mj_factorM order: leaves first) of depth-indexed rows.
  * Lane j holds the off-diagonal entries X[e] = A(j, anc_e(j)), e < depth(j),
  * and the diagonal Xd. On return the L rows are in LDS L[][] (L(k, anc_e(k))),
@@ -579,7 +639,7 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < CAP; e++)
-    if (e <= r.kdep) v += c.L->J[c.l][e] * c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
+    if (e <= r.kdep) v += c.L->u.J[c.l][e] * c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
   return v;
 }
 
@@ -617,7 +677,7 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
     }
 #pragma unroll
     for (int k = 0; k < 6; k++) {
-      L->cdofdot[j][k] = cdd[k];
+      L->u.cdofdot[j][k] = cdd[k];
       L->sub[j][k] = acc[k];
     }
   }
@@ -644,7 +704,7 @@ __device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc
         int a = ancof(c, e);
         float qv = L->vec[V_QVEL][a];
 #pragma unroll
-        for (int k = 0; k < 6; k++) acc[k] += L->cdofdot[a][k] * qv;
+        for (int k = 0; k < 6; k++) acc[k] += L->u.cdofdot[a][k] * qv;
         if (with_acc) {
           float qa = L->vec[V_QACC][a];
 #pragma unroll
@@ -801,7 +861,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   r.exmask = tb;
   if (r.ex) {
 #pragma unroll
-    for (int e = 0; e < CAP; e++) L->J[l][e] = Jc[e];
+    for (int e = 0; e < CAP; e++) L->u.J[l][e] = Jc[e];
   }
   /* ---- dof rows (lane j) ---- */
   r.hf = r.hlo = r.hhi = false;
@@ -878,7 +938,7 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
     while (tb) {
       int row = __ffs(tb) - 1;
       tb &= tb - 1u;
-      if ((c.rowmask >> row) & 1u) qc += L->J[row][c.ddep] * L->rowF[row];
+      if ((c.rowmask >> row) & 1u) qc += L->u.J[row][c.ddep] * L->rowF[row];
     }
     if (r.hf) qc += r.ff;
     if (r.hlo) qc += r.flo;
@@ -899,9 +959,9 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
       int row = __ffs(tb) - 1;
       tb &= tb - 1u;
       float da = L->rowDA[row];
-      float jd = L->J[row][c.ddep];
+      float jd = L->u.J[row][c.ddep];
       float jr[CAP];
-      ld_row(&L->J[row][0], jr);
+      ld_row(&L->u.J[row][0], jr);
       float jj = da * jd;
       Hd += jj * jd;
 #pragma unroll
@@ -1003,7 +1063,9 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   int it = 0;
   while (it < cfg->iterations) {
     float Mv;
+    STAMP(7);
     float alpha = line_search(c, r, search, Ma, fs, Mv);
+    STAMP(8);
     if (alpha == 0.f) break;
     x += alpha * search;
     Ma += alpha * Mv;
@@ -1017,8 +1079,11 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = tmaxi((r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1 : 0) != 0;
+    STAMP(9);
     if (changed) Dinv = hessian_factor(c, r);
+    STAMP(10);
     float mg = solve_ldl(c, grad, Dinv);
+    STAMP(11);
     it++;
     float improvement = scale * (oldcost - cost);
     float gradient = scale * sqrtf(tsum(c.l < c.nv ? grad * grad : 0.f));
@@ -1069,13 +1134,17 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
                                         Sensors& sen, int& iters) {
   const ZbModel* m = c.m;
   EnvL* L = c.L;
+  STAMP(15);
   kinematics(c, s, ls, B);
+  STAMP(1);
   float cm[3];
   com_crb_m(c, s, ls, B, cm);
+  STAMP(2);
   /* factor M (copy of rows) */
   float X[CAP];
   float Xd = load_mrow(c, X);
   float DinvM = factor_ldl(c, X, Xd);
+  STAMP(3);
   /* velocities */
   if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < c.nv ? ls.v : 0.f;
   tsync();
@@ -1093,9 +1162,12 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     ls.actforce = 0.f;
   }
   float fs = (c.l < c.nv) ? (-ls.damp * ls.v - bias + act) : 0.f;
+  STAMP(4);
   float qs = solve_ldl(c, fs, DinvM);
+  STAMP(5);
   /* constraints */
   make_constraints(c, s, ls, B, cm, r);
+  STAMP(6);
   int nrows = tmaxi(r.nrow + (r.hf || r.hlo || r.hhi ? 1 : 0));
   float qacc;
   if (nrows == 0) {
@@ -1104,6 +1176,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     qacc = solve_newton(c, r, qs, fs, ls.w, iters);
   }
   ls.qacc = (c.l < c.nv) ? qacc : 0.f;
+  STAMP(7);
   if (!with_sensors) return;
   /* ------------------- sensors (mj_rnePostConstraint etc.) ------------------ */
   if (c.l < 32) L->vec[V_QACC][c.l] = ls.qacc;
@@ -1131,6 +1204,10 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     if (g == m->geom_right_foot) sen.touch[1] = fnt;
   }
   float cacc[6];
+  {
+    BodyK B2 = B; /* com_vel rewrites cvel identically; recompute cdofdot (aliased with J) */
+    com_vel(c, B2);
+  }
   com_acc(c, cacc, true);
   /* cfrc_int subtree sums (in sub[]) */
   (void)rne_project(c, B, cacc, fext);
@@ -1181,6 +1258,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     }
   }
   tsync();
+  STAMP(12);
 }
 
 /* ------------------------------ Euler integrate ----------------------------- */
@@ -1615,8 +1693,10 @@ __device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, flo
 }
 
 /* ---------------------------- per-team context ------------------------------ */
-__device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvConfig* cfg, EnvL* L, uint64_t seed, uint32_t env) {
+__device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvConfig* cfg, EnvL* L, const Sched* S,
+                                         uint64_t seed, uint32_t env) {
   c.m = m;
+  c.S = S;
   c.cfg = cfg;
   c.L = L;
   c.seed = seed;
@@ -1686,22 +1766,52 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   }
   c.rowmask = rm;
   c.dk0 = isd ? l - m->body_dofadr[c.dbody] : 0;
+  c.moff = isd ? m->dof_rowoff[l] : m->mrow_size;
+  c.mylevel = -1;
+  for (int lv = 0; lv < m->nlevel; lv++)
+    for (int mi = 0; mi < m->level_nmem[lv]; mi++)
+      if (isd && m->level_mem[lv][mi] == l) c.mylevel = lv;
   c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
 }
 
 /* ---------------------------------- kernels --------------------------------- */
-template <bool ROLLOUT>
-__global__ __launch_bounds__(64) void step_kernel(StepArgs a) {
+__device__ __forceinline__ void fill_sched(const ZbModel* m, Sched* S) {
+  const int t = threadIdx.x;
+  if (t < 32) S->rowoff[t] = t < m->nv ? m->dof_rowoff[t] : m->mrow_size;
+  for (int i = t; i < ZB_MAX_DEPTH * 8; i += 64) {
+    int k = m->level_mem[i / 8][i % 8];
+    S->mem[i / 8][i % 8] = k;
+    S->memoff[i / 8][i % 8] = k >= 0 ? m->dof_rowoff[k] : m->mrow_size;
+  }
+  if (t < ZB_MAX_DEPTH) S->nmem[t] = m->level_nmem[t];
+  if (t == 0) S->nlevel = m->nlevel;
+  __syncthreads();
+}
+
+/* 2 waves per SIMD: the register allocator spills ~1 KB/lane of cold state to
+   scratch (L1/L2-resident) instead of holding ~440 registers at 1 wave/SIMD;
+   measured 1.6x faster (tests/diag_variants.py). */
+#ifndef ZB_WAVES_PER_EU
+#define ZB_WAVES_PER_EU 2
+#endif
+__global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   __shared__ EnvL lds[NTEAM];
+  __shared__ Sched sched;
+  fill_sched(a.model, &sched);
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = &a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &lds[team], &sched, a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
+#ifdef ZB_STAMPS
+  if (c.l < 16) c.L->stamp[c.l] = 0;
+  if (c.l == 0) c.L->stamp_last = __builtin_amdgcn_s_memtime();
+  tsync();
+#endif
   EnvS s;
   LaneS ls;
   load_state(c, s, ls, st);
@@ -1712,7 +1822,8 @@ __global__ __launch_bounds__(64) void step_kernel(StepArgs a) {
   int iters = 0;
   float rsum = 0.f;
   bool done = false;
-  const int nsteps = ROLLOUT ? a.nsteps : 1;
+  const int nsteps = a.nsteps;
+  const bool rollout = nsteps > 1;
   for (int t = 0; t < nsteps; t++) {
     const bool last_t = t == nsteps - 1;
     if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + e) * ZB_NJ + c.act];
@@ -1723,17 +1834,20 @@ __global__ __launch_bounds__(64) void step_kernel(StepArgs a) {
     /* 20 substeps; when the env terminates, one more pass of the same code path
        runs the reset forward (mjx.forward after MjxEngine.reset) */
     while (true) {
+      STAMP(14);
       if (!resetting) feetech(c, ls);
+      STAMP(0);
       forward(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, iters);
       if (resetting) break;
       integrate(c, s, ls);
+      STAMP(13);
       if (++ss < cfg->n_substeps) continue;
       {
         bool bad = (c.l < c.nv) && !(isfinite(ls.q) && isfinite(ls.v));
         if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
       }
       bool fail;
-      float* terms = (a.reward_terms && !ROLLOUT) ? a.reward_terms + (size_t)e * ZB_NUM_TERMS : nullptr;
+      float* terms = (a.reward_terms && !rollout) ? a.reward_terms + (size_t)e * ZB_NUM_TERMS : nullptr;
       done = rewards(c, s, ls, B, a.curriculum, terms, total, fail);
       rsum += total;
       if (a.stats && c.l == 0) {
@@ -1758,16 +1872,23 @@ __global__ __launch_bounds__(64) void step_kernel(StepArgs a) {
     }
     s.rng_step += 1u;
     if (c.l == 0 && last_t) {
-      if (a.reward) a.reward[e] = ROLLOUT ? rsum : total;
+      if (a.reward) a.reward[e] = rollout ? rsum : total;
       if (a.done) a.done[e] = done ? 1 : 0;
     }
   }
   if (a.iters && c.l == 0) a.iters[e] = iters;
   store_state(c, s, ls, st);
+#ifdef ZB_STAMPS
+  STAMP(14);
+  if (a.dbg && c.l == 0)
+    for (int i = 0; i < 16; i++) reinterpret_cast<unsigned long long*>(a.dbg)[(size_t)e * 16 + i] = c.L->stamp[i];
+#endif
 }
 
 __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   __shared__ EnvL lds[NTEAM];
+  __shared__ Sched sched;
+  fill_sched(a.model, &sched);
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
@@ -1775,7 +1896,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = &a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &lds[team], &sched, a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
   EnvS s;
@@ -1796,13 +1917,15 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
 /* single forward on the stored (qpos, qvel), ctrl = action row; dumps internals */
 __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   __shared__ EnvL lds[NTEAM];
+  __shared__ Sched sched;
+  fill_sched(a.model, &sched);
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = &a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &lds[team], &sched, a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   EnvS s;
   LaneS ls;
@@ -1871,10 +1994,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
 hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  if (a.nsteps > 1)
-    hipLaunchKernelGGL(step_kernel<true>, grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL(step_kernel<false>, grid, block, 0, s, a);
+  hipLaunchKernelGGL(step_kernel, grid, block, 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_reset(const StepArgs& a, hipStream_t s) {

@@ -16,7 +16,7 @@ MAX_ACT = 32
 CON_PER_GEOM = 4
 
 MODEL_MAGIC = 0x5A424F54
-MODEL_VERSION = 4
+MODEL_VERSION = 5
 
 JNT_NONE = -1
 JNT_FREE = 0
@@ -202,6 +202,10 @@ class ZbModel(C.Structure):
         ("dof_act", _i(MAX_DOF)),
         ("dof_rowoff", _i(MAX_DOF)),
         ("geom_lastdof", _i(MAX_GEOM)),
+        ("nlevel", C.c_int32),
+        ("pad_lvl", _i(3)),
+        ("level_nmem", _i(MAX_DEPTH)),
+        ("level_mem", _i(MAX_DEPTH, 8)),
         ("joint_bias", _f(MAX_ACT)),
         ("joint_weight", _f(MAX_ACT)),
         ("pad_end", _f(4)),

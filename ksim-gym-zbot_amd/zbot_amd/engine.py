@@ -33,14 +33,18 @@ def build_library(force: bool = False) -> str:
     return LIB_PATH
 
 
-def load_library() -> C.CDLL:
-    """Load the engine library; raises if it has not been built."""
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load the engine library; raises if it has not been built.
+
+    `path` selects another build of the same sources (the -DZB_STAMPS
+    diagnostic library used by tests/diag_stamps.py)."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ZbError(f"{LIB_PATH} not found: build it with `make -C {CSRC_DIR}` (or __graft_entry__.build())")
-    L = C.CDLL(LIB_PATH)
+    lp = path or LIB_PATH
+    if not os.path.exists(lp):
+        raise ZbError(f"{lp} not found: build it with `make -C {CSRC_DIR}` (or __graft_entry__.build())")
+    L = C.CDLL(lp)
     vp = C.c_void_p
     L.zb_abi_version.restype = C.c_int
     L.zb_model_struct_bytes.restype = C.c_size_t
@@ -66,7 +70,8 @@ def load_library() -> C.CDLL:
         raise ZbError("ZbModel layout mismatch between cstructs.py and the library")
     if L.zb_config_struct_bytes() != C.sizeof(cs.ZbEnvConfig):
         raise ZbError("ZbEnvConfig layout mismatch between cstructs.py and the library")
-    _lib = L
+    if path is None:
+        _lib = L
     return L
 
 
@@ -87,13 +92,13 @@ class HipEngine:
     """N Z-Bot environments on one GPU (one handle)."""
 
     def __init__(self, model, cfg: cs.ZbEnvConfig, n_envs: int, env_offset: int = 0, device: int = 0,
-                 seed: int = 0):
+                 seed: int = 0, lib_path: str | None = None):
         import torch  # noqa: PLC0415
 
         if not torch.cuda.is_available():
             raise ZbError("HipEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.torch = torch
-        self.L = load_library()
+        self.L = load_library(lib_path)
         self.cmodel = model.cmodel if hasattr(model, "cmodel") else model
         self.cfg = cfg
         self.n = n_envs

@@ -555,6 +555,22 @@ def _fill_tables(m, bodies, nbody, nv, dof_depth, dof_anc, dof_parent, geom_body
     m.mrow_size = off
     for g, kd in enumerate(glast):
         m.geom_lastdof[g] = kd
+    # elimination levels: height of each dof in the dof tree (leaves = 0)
+    height = [0] * nv
+    for d in range(nv - 1, -1, -1):  # children have larger indices than parents
+        p = dof_parent[d]
+        if p >= 0:
+            height[p] = max(height[p], height[d] + 1)
+    m.nlevel = max(height) + 1 if nv else 0
+    if m.nlevel > cs.MAX_DEPTH:
+        raise ValueError("too many elimination levels")
+    for lv in range(cs.MAX_DEPTH):
+        mem = [d for d in range(nv) if height[d] == lv]
+        if len(mem) > 8:
+            raise ValueError(f"elimination level {lv} has {len(mem)} dofs (max 8)")
+        m.level_nmem[lv] = len(mem)
+        for k in range(8):
+            m.level_mem[lv][k] = mem[k] if k < len(mem) else -1
 
 
 def C_sizeof(t: type) -> int:  # noqa: N802

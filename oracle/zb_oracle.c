@@ -1553,6 +1553,7 @@ static const FieldOff model_fields[] = {
     OFF(ZbModel, max_body_depth), OFF(ZbModel, mrow_size), OFF(ZbModel, pad_tab), OFF(ZbModel, body_nchild),
     OFF(ZbModel, body_child), OFF(ZbModel, depth_maxchild), OFF(ZbModel, dof_desc), OFF(ZbModel, dof_ancpk),
     OFF(ZbModel, dof_rowmask), OFF(ZbModel, dof_act), OFF(ZbModel, dof_rowoff), OFF(ZbModel, geom_lastdof),
+    OFF(ZbModel, nlevel), OFF(ZbModel, pad_lvl), OFF(ZbModel, level_nmem), OFF(ZbModel, level_mem),
     OFF(ZbModel, joint_bias), OFF(ZbModel, joint_weight), OFF(ZbModel, pad_end),
 };
 static const FieldOff config_fields[] = {

@@ -1,0 +1,56 @@
+"""Per-phase cycle shares of the step kernel from the -DZB_STAMPS diagnostic build.
+
+    make -C ksim-gym-zbot_amd/csrc stamps && python tests/diag_stamps.py [--n 8192]
+
+Stamps fence the pipeline (s_waitcnt around s_memtime), so read the SHARES,
+not the absolute time (cdna_hip_programming.md §7, In-kernel stamps).
+"""
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
+
+import torch  # noqa: E402
+from zbot_amd import compile_model, default_config  # noqa: E402
+from zbot_amd.engine import HipEngine  # noqa: E402
+
+PHASES = ["feetech", "kinematics", "com_crb_M", "factor_M", "rne_bias", "solve_smooth", "constraints",
+          "newton_init", "line_search", "update_constraint", "hessian_factor", "newton_solve", "sensors",
+          "integrate", "step_end(obs/reward/reset)", "forward_entry"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    lib = os.path.join(ROOT, "ksim-gym-zbot_amd", "zbot_amd", "libzbot_hip_stamps.so")
+    cm = compile_model()
+    eng = HipEngine(cm, default_config(), args.n, lib_path=lib)
+    eng.L.zb_get_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    eng.reset()
+    bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    tot = torch.zeros(16, dtype=torch.float64)
+    for t in range(args.steps):
+        eng.step(bias + 0.05 * torch.randn(args.n, 20, device="cuda"))
+        buf = torch.zeros(args.n, 16, dtype=torch.int64, device="cuda")
+        eng.L.zb_get_stamps(eng.h, buf.data_ptr(), eng._stream())
+        torch.cuda.synchronize()
+        tot += buf.double().sum(0).cpu()
+    share = tot / tot.sum()
+    res = {PHASES[i]: round(float(share[i]) * 100, 2) for i in range(16)}
+    res["cycles_per_env_step"] = float(tot.sum() / (args.n * args.steps))
+    print(json.dumps(res, indent=1))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,48 @@
+"""A/B timing of library variants (same sources, different build flags) in ONE process.
+
+    python tests/diag_variants.py lib1.so lib2.so ... [--n 8192 --steps 16 --rounds 3]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
+import torch  # noqa: E402
+from zbot_amd import compile_model, default_config  # noqa: E402
+from zbot_amd.engine import HipEngine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    cm = compile_model()
+    bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    acts = [bias + 0.05 * torch.randn(a.n, 20, device="cuda") for _ in range(8)]
+    engs = [HipEngine(cm, default_config(), a.n, lib_path=os.path.abspath(p), seed=0) for p in a.libs]
+    for e in engs:
+        e.reset()
+        for t in range(3):
+            e.step(acts[t])
+    torch.cuda.synchronize()
+    res = {p: [] for p in a.libs}
+    for r in range(a.rounds):
+        for p, e in zip(a.libs, engs):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for t in range(a.steps):
+                e.step(acts[t % 8], extras=False)
+            torch.cuda.synchronize()
+            res[p].append(a.n * a.steps / (time.perf_counter() - t0))
+    for p in a.libs:
+        v = sorted(res[p])
+        print(f"{os.path.basename(p):32s} median {v[len(v)//2]:.0f} env-steps/s  all {[round(x) for x in v]}")
+
+
+if __name__ == "__main__":
+    main()
