@@ -1,0 +1,145 @@
+"""ksim-shaped environment API over the HIP engine.
+
+Mirrors the names the reference task uses so a train.py-style caller can swap
+ksim's MjxEngine rollout for this engine:
+
+  * observations: the dict keys ksim builds from train.py:1478-1537
+    (``joint_position_observation``, ``imu_orientation_observation``, ...);
+  * rewards: the registered terms of train.py:1546-1586 with their scales;
+  * ``actor_inputs`` / ``critic_inputs``: the concatenations of
+    ZbotWalkingTask.run_actor (train.py:1629-1639) and run_critic
+    (train.py:1664-1679), produced directly by the kernel (50 / 484 floats);
+  * episode statistics reduced across ranks for the curriculum / logging.
+
+All tensors are torch device tensors (views into the engine's output buffers;
+clone them if they must survive the next step).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from . import cstructs as cs
+from .config import default_config
+from .constants import JOINT_BIASES, REWARDS
+from .engine import HipEngine
+from .model import compile_model
+
+# obs_critic layout (train.py:1664-1679)
+_CRITIC = dict(
+    joint_positions=(0, 20),
+    joint_velocity_div10=(20, 40),
+    com_inertia=(40, 290),
+    com_velocity=(290, 440),
+    imu_acc=(440, 443),
+    imu_gyro=(443, 446),
+    imu_quat=(446, 450),
+    cmd_all=(450, 457),
+    act_force_div100=(457, 477),
+    base_pos=(477, 480),
+    base_quat=(480, 484),
+)
+
+
+def observation_dict(out: dict) -> dict:
+    """ksim observation names -> tensors, from the engine outputs."""
+    oa, oc, ox = out["obs_actor"], out["obs_critic"], out["obs_extra"]
+
+    def c(k):
+        a, b = _CRITIC[k]
+        return oc[:, a:b]
+
+    obs = {
+        "joint_position_observation": oa[:, 0:20],
+        "joint_velocity_observation": oa[:, 20:40],
+        "imu_orientation_observation": oa[:, 40:44],
+        "actuator_force_observation": c("act_force_div100") * 100.0,
+        "center_of_mass_inertia_observation": c("com_inertia"),
+        "center_of_mass_velocity_observation": c("com_velocity"),
+        "base_position_observation": c("base_pos"),
+        "base_orientation_observation": c("base_quat"),
+        "sensor_observation_imu_acc": c("imu_acc"),
+        "sensor_observation_imu_gyro": c("imu_gyro"),
+    }
+    if ox is not None:
+        obs.update({
+            "base_linear_velocity_observation": ox[:, cs.X_BASE_LINVEL:cs.X_BASE_LINVEL + 3],
+            "base_angular_velocity_observation": ox[:, cs.X_BASE_ANGVEL:cs.X_BASE_ANGVEL + 3],
+            "base_linear_acceleration_observation": ox[:, cs.X_BASE_LINACC:cs.X_BASE_LINACC + 3],
+            "base_angular_acceleration_observation": ox[:, cs.X_BASE_ANGACC:cs.X_BASE_ANGACC + 3],
+            "base_height_observation": ox[:, cs.X_BASE_HEIGHT:cs.X_BASE_HEIGHT + 1],
+            "sensor_observation_left_foot_touch": ox[:, cs.X_TOUCH:cs.X_TOUCH + 1],
+            "sensor_observation_right_foot_touch": ox[:, cs.X_TOUCH + 1:cs.X_TOUCH + 2],
+            "sensor_observation_left_foot_force": ox[:, cs.X_FORCE:cs.X_FORCE + 3],
+            "sensor_observation_right_foot_force": ox[:, cs.X_FORCE + 3:cs.X_FORCE + 6],
+            "feet_position_observation": ox[:, cs.X_FEET_POS:cs.X_FEET_POS + 6],
+            "feetech_torque_observation": ox[:, cs.X_FEETECH_TAU:cs.X_FEETECH_TAU + 20],
+            "actuator_acceleration_observation": ox[:, cs.X_ACT_ACC:cs.X_ACT_ACC + 20],
+        })
+        for i, (name, _, _) in enumerate(JOINT_BIASES):  # ActPosObservation per joint [U: = joint position]
+            obs[f"act_pos_observation_{name}"] = oa[:, i:i + 1]
+    return obs
+
+
+@dataclass
+class StepResult:
+    obs: dict
+    actor_inputs: object
+    critic_inputs: object
+    reward: object
+    reward_terms: dict
+    done: object
+
+
+class ZbotWalkingEnv:
+    """Batched ZbotWalkingTask environment (train.py:1311-1763) on one GPU.
+
+    `num_envs`, `dt`, `ctrl_dt`, `iterations`, `ls_iterations` default to
+    train.py:1768-1781 (512 envs, 0.001, 0.02, 8, 8).
+    """
+
+    def __init__(self, num_envs: int = 512, *, seed: int = 0, device: int = 0, env_offset: int = 0,
+                 push: bool = False, randomize: bool = False, obs_noise: bool = True, model=None, **cfg_kw):
+        self.model = model or compile_model()
+        self.cfg = default_config(push=push, randomize=randomize, obs_noise=obs_noise, **cfg_kw)
+        self.engine = HipEngine(self.model, self.cfg, num_envs, env_offset=env_offset, device=device, seed=seed)
+        self.num_envs = num_envs
+        self.curriculum_level = 1.0
+
+    def _result(self, out: dict, with_reward: bool) -> StepResult:
+        terms = {}
+        if with_reward:
+            rt = out["reward_terms"]
+            terms = {name: rt[:, i] for i, (name, _, _) in enumerate(REWARDS)}
+        return StepResult(
+            obs=observation_dict(out),
+            actor_inputs=out["obs_actor"],
+            critic_inputs=out["obs_critic"],
+            reward=out["reward"] if with_reward else None,
+            reward_terms=terms,
+            done=out["done"] if with_reward else None,
+        )
+
+    def reset(self, mask=None) -> StepResult:
+        return self._result(self.engine.reset(mask=mask), with_reward=False)
+
+    def step(self, action) -> StepResult:
+        """One control step (20 physics substeps) for every env; done envs auto-reset."""
+        return self._result(self.engine.step(action, curriculum=self.curriculum_level), with_reward=True)
+
+    def default_action(self):
+        """FeetechActuators.get_default_action: current joint positions (train.py:1282-1283)."""
+        return self.engine.get_state()[:, 7:27].clone()
+
+    def episode_stats(self, clear: bool = True) -> dict:
+        """Globally reduced episode statistics (RCCL all_gather when distributed)."""
+        from .dist import reduce_episode_stats  # noqa: PLC0415
+
+        tot = reduce_episode_stats(self.engine.get_stats(clear=clear))
+        n = max(float(tot[cs.ST_DONE]), 1.0)
+        return {
+            "episodes": float(tot[cs.ST_DONE]),
+            "mean_return": float(tot[cs.ST_RETURN]) / n,
+            "mean_length_steps": float(tot[cs.ST_LENGTH]) / n,
+            "reward_sum": float(tot[cs.ST_REWARD]),
+        }

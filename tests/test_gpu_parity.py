@@ -243,3 +243,29 @@ def test_full_size_properties(torch_gpu, cmodel):
     # standing task: almost all envs still alive and near the reset height
     z = st[:, 2]
     assert (z > 0.2).float().mean().item() > 0.95
+
+
+def test_ksim_shaped_env(torch_gpu, cmodel):
+    torch = torch_gpu
+    from zbot_amd.task import ZbotWalkingEnv
+
+    env = ZbotWalkingEnv(num_envs=32, seed=4, model=cmodel)
+    r0 = env.reset()
+    assert r0.actor_inputs.shape == (32, 50) and r0.critic_inputs.shape == (32, 484)
+    a = env.default_action()
+    r = env.step(a)
+    torch.cuda.synchronize()
+    obs = r.obs
+    # run_actor concatenation (train.py:1629-1639): joint pos, joint vel, imu quat, 6 command zeros
+    assert torch.equal(r.actor_inputs[:, 0:20], obs["joint_position_observation"])
+    assert torch.equal(r.actor_inputs[:, 40:44], obs["imu_orientation_observation"])
+    assert torch.count_nonzero(r.actor_inputs[:, 44:50]) == 0
+    st = env.engine.get_state()
+    assert torch.equal(obs["joint_position_observation"], st[:, 7:27])
+    assert torch.equal(obs["base_position_observation"], st[:, 0:3])
+    assert set(r.reward_terms) >= {"stay_alive", "feet_airtime", "arm_pose_penalty"}
+    total = sum(s * (1.0 if not c else env.curriculum_level) * r.reward_terms[n] for n, s, c in __import__(
+        "zbot_amd").constants.REWARDS)
+    assert torch.allclose(total, r.reward, atol=1e-5)
+    stats = env.episode_stats()
+    assert stats["episodes"] >= 0
