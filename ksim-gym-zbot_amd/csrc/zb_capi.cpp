@@ -26,6 +26,7 @@ struct ZbHandle {
   ZbModel hmodel;
   ZbEnvConfig cfg;
   ZbModel* dmodel;
+  ZbEnvConfig* dcfg;
   float* state;
   float* rnd;
   float* stats;
@@ -167,6 +168,8 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   h->cfg = *cfg;
   size_t n = (size_t)(n_envs > 0 ? n_envs : 1);
   hipError_t e = hipMalloc(&h->dmodel, sizeof(ZbModel));
+  if (e == hipSuccess) e = hipMalloc(&h->dcfg, sizeof(ZbEnvConfig));
+  if (e == hipSuccess) e = hipMemcpy(h->dcfg, cfg, sizeof(ZbEnvConfig), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&h->state, n * ZB_STATE_STRIDE * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&h->rnd, n * ZB_RAND_STRIDE * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&h->stats, n * ZB_NUM_STATS * sizeof(float));
@@ -192,6 +195,7 @@ int zb_destroy(ZbHandle* h) {
   if (!h) return ZB_OK;
   (void)hipSetDevice(h->device);
   if (h->dmodel) (void)hipFree(h->dmodel);
+  if (h->dcfg) (void)hipFree(h->dcfg);
   if (h->state) (void)hipFree(h->state);
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->stats) (void)hipFree(h->stats);
@@ -205,7 +209,7 @@ static zb::StepArgs base_args(ZbHandle* h) {
   zb::StepArgs a;
   memset(&a, 0, sizeof a);
   a.model = h->dmodel;
-  a.cfg = h->cfg;
+  a.cfg = h->dcfg;
   a.n_envs = h->n;
   a.env_offset = h->env_offset;
   a.seed = h->seed;

@@ -42,9 +42,20 @@ constexpr float MAXIMP = 0.9999f;
 constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0); /* train.py:1113-1116 */
 
 enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3 };
+enum { P_Q0 = 0, P_ARM = 1, P_DAMP = 2, P_FLOSS = 3, P_MSCALE = 4 };
 
-/* per-environment LDS working set (8.6 KB) */
-constexpr int MROW = 248; /* packed depth-indexed rows (model.mrow_size <= 240) + read padding */
+/* per-env scalars: one copy per team in LDS, read by every lane (broadcast) and
+   written by every lane with the bit-identical value it computed */
+struct EnvS {
+  float bp[3], bq[4];
+  float ema[4], lag, air[2], push_timer, touch[2], feet_dist, ep_ret, prev_cont[2];
+  uint32_t ep_steps, rng_step, episode, nanflag;
+  float floor_mu, imu_q[4], imu_p[3];
+};
+struct Sensors {
+  float fq[4], gyro[3], acc[3], touch[2], force[6];
+};
+/* per-environment LDS working set */
 struct __align__(16) EnvL {
   float cdof[32][6];
   float M[32][CAP];
@@ -58,22 +69,16 @@ struct __align__(16) EnvL {
   float rowDA[32];
   float rowF[32];
   float Dk[32];
+  float ci[32][10];  /* body cinert (lane b), kept for RNE / sensors / observations */
+  float par[5][32];  /* effective dof / body parameters (lane), see P_* */
+  EnvS s;
+  Sensors sen;
 #ifdef ZB_STAMPS
   unsigned long long stamp[16];
   unsigned long long stamp_last;
 #endif
 };
 
-/* per-block copy of the small topology tables used inside the serial loops
-   (LDS reads instead of dependent scalar/global model loads) */
-struct __align__(16) Sched {
-  int rowoff[32];     /* packed row offset of each dof */
-  int mem[ZB_MAX_DEPTH][8]; /* members of each elimination level (-1 padded) */
-  int memoff[ZB_MAX_DEPTH][8]; /* their packed row offsets */
-  int nmem[ZB_MAX_DEPTH];
-  int nlevel;
-  int pad[3];
-};
 
 /* ----------------------------- team primitives ----------------------------- */
 __device__ __forceinline__ float tsh(float v, int src) { return __shfl(v, src, TEAM); }
@@ -255,11 +260,27 @@ __device__ __forceinline__ void normal2(uint64_t seed, uint32_t p, uint32_t k, u
 }
 
 /* --------------------------------- contexts -------------------------------- */
+/* The model and config are device buffers never written by a kernel, so they
+   are read through the constant address space (scalar loads for uniform
+   fields). `opaque` re-derives the pointers at the top of every substep: the
+   compiler cannot hoist the uniform loads out of the substep loop, so they
+   are re-issued from the scalar cache instead of pinning ~300 SGPRs (which
+   spilled into VGPR lanes) across the whole launch. */
+typedef const __attribute__((address_space(4))) ZbModel* MP;
+typedef const __attribute__((address_space(4))) ZbEnvConfig* CP;
+template <typename P>
+__device__ __forceinline__ P opaque(P p) {
+  uint64_t v = (uint64_t)p;
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  asm volatile("" : "+v"(lo), "+v"(hi));
+  lo = __builtin_amdgcn_readfirstlane(lo);
+  hi = __builtin_amdgcn_readfirstlane(hi);
+  return (P)(((uint64_t)hi << 32) | lo);
+}
 struct Ctx {
-  const ZbModel* m;
-  const ZbEnvConfig* cfg;
+  MP m;
+  CP cfg;
   EnvL* L;
-  const Sched* S;
   uint64_t seed;
   uint32_t env;
   int l;
@@ -292,42 +313,27 @@ __device__ __forceinline__ int childof(const Ctx& c, int k) {
   return (int)((w >> ((k & 3) * 8)) & 0xffu);
 }
 
-/* per-env replicated scalars */
-struct EnvS {
-  float bp[3], bq[4];
-  float ema[4], lag, air[2], push_timer, touch[2], feet_dist, ep_ret, prev_cont[2];
-  uint32_t ep_steps, rng_step, episode, nanflag;
-  float floor_mu, imu_q[4], imu_p[3];
-};
 /* per-lane persistent registers */
 struct LaneS {
   float q, v, w;        /* dof lane: hinge angle, qvel, qacc_warmstart */
-  float q0;             /* joint zero (hinge) */
   float pp, pv, ptau;   /* planner (actuated dof lane) */
   float tgt;            /* action target */
-  float arm, damp, floss; /* effective dof params */
-  float mscale;         /* body lane mass scale */
   float ctrl;           /* actuator ctrl of this dof lane */
   float qacc;           /* last constrained qacc */
   float actforce;       /* actuator force (gear*clamped ctrl) */
 };
 /* per-substep body outputs */
 struct BodyK {
-  float xp[3], xq[4], R[9];
-  float ci[10], cv[6];
-};
-struct Sensors {
-  float fq[4], gyro[3], acc[3], touch[2], force[6];
+  float xp[3], xq[4]; /* rotation matrices are recomputed from xq where needed */
+  float cv[6];
 };
 /* constraint rows held by the lane */
 struct Rows {
   /* contact row (lane = row) */
   bool ex;
-  uint32_t ka0, ka1, ka2; int kdep; int kd;
+  uint32_t ka0, ka1, ka2; int kdep;
   float aref, D, jar, Jv, f;
   int act;
-  float dir[3], pos[3];
-  int geom;
   /* dof rows: frictionloss, lower, upper limit */
   bool hf, hlo, hhi;
   float af, Df, Rf, fl, jf, ff; int actf;
@@ -354,9 +360,9 @@ __device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
 
 /* ------------------------------- kinematics -------------------------------- */
 __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B) {
-  const ZbModel* m = c.m;
+  MP m = c.m;
   /* relative hinge angle of this body's joint, from its dof lane */
-  float qrel_dof = ls.q - ls.q0;
+  float qrel_dof = ls.q - c.L->par[P_Q0][c.l];
   float ang = tsh(qrel_dof, c.bdofadr < 0 ? 0 : c.bdofadr);
   B.xp[0] = B.xp[1] = B.xp[2] = 0.f;
   B.xq[0] = 1.f; B.xq[1] = B.xq[2] = B.xq[3] = 0.f;
@@ -407,7 +413,6 @@ __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const La
       }
     }
   }
-  quat2mat(B.R, B.xq);
 }
 
 /* subtree sum of K-vectors over the body tree: out (lane b) = sum over subtree(b).
@@ -435,32 +440,35 @@ __device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
 /* ------------------------------ mass matrix -------------------------------- */
 /* com, cinert (lane b), cdof (lane j -> LDS), crb, M rows (LDS + return) */
 __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B, float cm[3]) {
-  const ZbModel* m = c.m;
+  MP m = c.m;
   EnvL* L = c.L;
   const int b = c.l;
   const bool isbody = b >= 1 && b < c.nb;
-  float mass = isbody ? m->body_mass[b][0] * ls.mscale : 0.f;
+  float mass = isbody ? m->body_mass[b][0] * c.L->par[P_MSCALE][c.l] : 0.f;
   float xipos[3], Ri[9];
   {
     float ip[3] = {m->body_ipos[isbody ? b : 0][0], m->body_ipos[isbody ? b : 0][1], m->body_ipos[isbody ? b : 0][2]}, t[3];
-    mulmv3(t, B.R, ip);
+    float BR[9];
+    quat2mat(BR, B.xq);
+    mulmv3(t, BR, ip);
 #pragma unroll
     for (int k = 0; k < 3; k++) xipos[k] = B.xp[k] + t[k];
     float iq[4] = {m->body_iquat[isbody ? b : 0][0], m->body_iquat[isbody ? b : 0][1],
                    m->body_iquat[isbody ? b : 0][2], m->body_iquat[isbody ? b : 0][3]}, iR[9];
     quat2mat(iR, iq);
-    mulmm3(Ri, B.R, iR);
+    mulmm3(Ri, BR, iR);
   }
   float mt = tsum(mass);
 #pragma unroll
   for (int k = 0; k < 3; k++) cm[k] = tsum(mass * xipos[k]) / mt;
   /* cinert: inertia about cm in world orientation (mju_inertCom) */
+  float ci[10];
   {
     float in[3] = {0.f, 0.f, 0.f};
     if (isbody) {
-      in[0] = m->body_inertia[b][0] * ls.mscale;
-      in[1] = m->body_inertia[b][1] * ls.mscale;
-      in[2] = m->body_inertia[b][2] * ls.mscale;
+      in[0] = m->body_inertia[b][0] * c.L->par[P_MSCALE][c.l];
+      in[1] = m->body_inertia[b][1] * c.L->par[P_MSCALE][c.l];
+      in[2] = m->body_inertia[b][2] * c.L->par[P_MSCALE][c.l];
     }
     float dif[3] = {xipos[0] - cm[0], xipos[1] - cm[1], xipos[2] - cm[2]};
     float I[9];
@@ -471,24 +479,27 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
         I[3 * a + bb] = Ri[3 * a] * in[0] * Ri[3 * bb] + Ri[3 * a + 1] * in[1] * Ri[3 * bb + 1] +
                         Ri[3 * a + 2] * in[2] * Ri[3 * bb + 2];
     float dd = dot3(dif, dif);
-    B.ci[0] = I[0] + mass * (dd - dif[0] * dif[0]);
-    B.ci[1] = I[4] + mass * (dd - dif[1] * dif[1]);
-    B.ci[2] = I[8] + mass * (dd - dif[2] * dif[2]);
-    B.ci[3] = I[1] - mass * dif[0] * dif[1];
-    B.ci[4] = I[2] - mass * dif[0] * dif[2];
-    B.ci[5] = I[5] - mass * dif[1] * dif[2];
-    B.ci[6] = mass * dif[0];
-    B.ci[7] = mass * dif[1];
-    B.ci[8] = mass * dif[2];
-    B.ci[9] = mass;
+    ci[0] = I[0] + mass * (dd - dif[0] * dif[0]);
+    ci[1] = I[4] + mass * (dd - dif[1] * dif[1]);
+    ci[2] = I[8] + mass * (dd - dif[2] * dif[2]);
+    ci[3] = I[1] - mass * dif[0] * dif[1];
+    ci[4] = I[2] - mass * dif[0] * dif[2];
+    ci[5] = I[5] - mass * dif[1] * dif[2];
+    ci[6] = mass * dif[0];
+    ci[7] = mass * dif[1];
+    ci[8] = mass * dif[2];
+    ci[9] = mass;
+#pragma unroll
+    for (int k = 0; k < 10; k++) L->ci[b][k] = ci[k];
   }
   /* cdof (lane j): fetch body frame of dof's body */
   {
     const int j = c.l;
     int bj = c.dbody < 0 ? 0 : c.dbody;
-    float R[9], xp[3];
+    float R[9], xp[3], xqs[4];
 #pragma unroll
-    for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], bj);
+    for (int k = 0; k < 4; k++) xqs[k] = tsh(B.xq[k], bj);
+    quat2mat(R, xqs);
 #pragma unroll
     for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], bj);
     if (j < c.nv) {
@@ -522,7 +533,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   /* crb = subtree sums of cinert */
   float crb[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) crb[k] = B.ci[k];
+  for (int k = 0; k < 10; k++) crb[k] = ci[k];
   tsync();
   subtree_sum<10>(c, crb);
   /* M rows: M(j, anc_e(j)) = cdof_anc . (crb_body(j) * cdof_j), packed storage */
@@ -544,7 +555,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 #pragma unroll
           for (int k = 0; k < 6; k++) ca[k] = L->cdof[a][k];
           v = dot6(ca, F);
-          if (e == c.ddep) v += ls.arm;
+          if (e == c.ddep) v += c.L->par[P_ARM][c.l];
         }
         mr[e] = v;
       }
@@ -646,7 +657,7 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
 /* ----------------------------------- RNE ----------------------------------- */
 /* cvel (lane b), cdofdot (LDS). Requires vec[V_QVEL]. */
 __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
-  const ZbModel* m = c.m;
+  MP m = c.m;
   EnvL* L = c.L;
   const int j = c.l;
   if (j < c.nv) {
@@ -693,7 +704,7 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
 
 /* cacc per body (lane b) with or without qacc (vec[V_QACC]) */
 __device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc) {
-  const ZbModel* m = c.m;
+  MP m = c.m;
   EnvL* L = c.L;
   const int j = c.l;
   if (j < c.nv) {
@@ -730,9 +741,11 @@ __device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const
   EnvL* L = c.L;
   float f[6];
   if (c.l >= 1 && c.l < c.nb) {
-    float f1[6], t[6], f2[6];
-    mul_inert_vec(f1, B.ci, ca);
-    mul_inert_vec(t, B.ci, B.cv);
+    float f1[6], t[6], f2[6], ci[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) ci[k] = L->ci[c.l][k];
+    mul_inert_vec(f1, ci, ca);
+    mul_inert_vec(t, ci, B.cv);
     cross_force(f2, B.cv, t);
 #pragma unroll
     for (int k = 0; k < 6; k++) f[k] = f1[k] + f2[k] - fext[k];
@@ -756,7 +769,8 @@ __device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const
 }
 
 /* --------------------------- constraint model ------------------------------ */
-__device__ __forceinline__ float impedance(const float* si, float xabs) {
+template <typename PS>
+__device__ __forceinline__ float impedance(PS si, float xabs) {
   float dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
   float imp;
   if (width <= MINVAL || xabs >= width) {
@@ -770,7 +784,8 @@ __device__ __forceinline__ float impedance(const float* si, float xabs) {
   }
   return fminf(fmaxf(imp, MINIMP), MAXIMP);
 }
-__device__ __forceinline__ void row_params(const float* solref, const float* solimp, float pos, float dA, float vel,
+template <typename PR, typename PS>
+__device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, float dA, float vel,
                                            float dt, float& D, float& R, float& aref) {
   float tc = fmaxf(solref[0], 2.f * dt), dr = solref[1], dmax = solimp[1];
   float bb = 2.f / (dmax * tc);
@@ -781,31 +796,62 @@ __device__ __forceinline__ void row_params(const float* solref, const float* sol
   aref = -bb * vel - kk * imp * pos;
 }
 
+/* Plane-box contact of team lane l = 16*geom + 4*corner + edge: the sole corner
+ * (mid-penetration point, as mj_collidePlaneBox), the pyramid edge direction
+ * n +- mu t (frame of mju_makeFrame(+z): t1 = +y, t2 = -x) and the friction
+ * coefficient; returns the signed distance (> margin: no contact). Recomputed
+ * by the sensors instead of being held in registers through the solver. */
+__device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, const BodyK& B, float pos[3], float dir[3],
+                                               float& mu) {
+  MP m = c.m;
+  const int l = c.l;
+  const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
+  const bool gvalid = g < c.ngeom;
+  const int gg = gvalid ? g : 0;
+  const int gb = gvalid ? m->geom_body[g] : 0;
+  float R[9], xp[3], xqs[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) xqs[k] = tsh(B.xq[k], gb);
+  quat2mat(R, xqs);
+#pragma unroll
+  for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
+  float gp[3] = {m->geom_pos[gg][0], m->geom_pos[gg][1], m->geom_pos[gg][2]}, t[3];
+  float gq[4] = {m->geom_quat[gg][0], m->geom_quat[gg][1], m->geom_quat[gg][2], m->geom_quat[gg][3]}, gR0[9], gR[9];
+  mulmv3(t, R, gp);
+  float gpos[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
+  quat2mat(gR0, gq);
+  mulmm3(gR, R, gR0);
+  float loc[3] = {(corner & 1) ? m->geom_size[gg][0] : -m->geom_size[gg][0],
+                  (corner & 2) ? m->geom_size[gg][1] : -m->geom_size[gg][1], -m->geom_size[gg][2]};
+  mulmv3(t, gR, loc);
+  float p[3] = {gpos[0] + t[0], gpos[1] + t[1], gpos[2] + t[2]};
+  float dist = p[2];
+  pos[0] = p[0]; pos[1] = p[1]; pos[2] = p[2] - 0.5f * dist;
+  mu = m->floor_friction[0] * s.floor_mu;
+  float sg = (edge & 1) ? -mu : mu;
+  if (edge < 2) { dir[0] = 0.f; dir[1] = sg; dir[2] = 1.f; }
+  else { dir[0] = -sg; dir[1] = 0.f; dir[2] = 1.f; }
+  return dist;
+}
+
 /* collision + contact rows (lane r) + dof rows (lane j) */
 __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
                                  Rows& r) {
-  const ZbModel* m = c.m;
-  const ZbEnvConfig* cfg = c.cfg;
+  MP m = c.m;
+  CP cfg = c.cfg;
   EnvL* L = c.L;
   const int l = c.l;
   /* ---- contact rows: lane = 16*geom + 4*corner + edge ---- */
   const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
   const bool gvalid = g < c.ngeom;
   const int gb = gvalid ? m->geom_body[g] : 0;
-  float R[9], xp[3];
-#pragma unroll
-  for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], gb);
-#pragma unroll
-  for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
   int kd = gvalid ? m->body_lastdof[gb] : 0;
   if (kd < 0) kd = 0;
   r.ka0 = (uint32_t)tshi((int)c.anc0, kd);
   r.ka1 = (uint32_t)tshi((int)c.anc1, kd);
   r.ka2 = (uint32_t)tshi((int)c.anc2, kd);
   r.kdep = tshi(c.ddep, kd);
-  r.kd = kd;
   r.ex = false;
-  r.geom = g;
   r.act = 0;
   r.f = 0.f;
   r.jar = 0.f;
@@ -815,43 +861,26 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   float Jc[CAP];
 #pragma unroll
   for (int e = 0; e < CAP; e++) Jc[e] = 0.f;
-  if (gvalid) {
-    float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]}, t[3];
-    float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]}, gR0[9], gR[9];
-    mulmv3(t, R, gp);
-    float gpos[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
-    quat2mat(gR0, gq);
-    mulmm3(gR, R, gR0);
-    float loc[3] = {(corner & 1) ? m->geom_size[g][0] : -m->geom_size[g][0],
-                    (corner & 2) ? m->geom_size[g][1] : -m->geom_size[g][1], -m->geom_size[g][2]};
-    mulmv3(t, gR, loc);
-    float p[3] = {gpos[0] + t[0], gpos[1] + t[1], gpos[2] + t[2]};
-    float dist = p[2];
-    if (dist < m->floor_margin) {
-      r.ex = true;
-      r.pos[0] = p[0]; r.pos[1] = p[1]; r.pos[2] = p[2] - 0.5f * dist;
-      float mu = m->floor_friction[0] * s.floor_mu;
-      float sg = (edge & 1) ? -mu : mu;
-      /* frame of mju_makeFrame(+z): t1 = +y, t2 = -x */
-      if (edge < 2) { r.dir[0] = 0.f; r.dir[1] = sg; r.dir[2] = 1.f; }
-      else { r.dir[0] = -sg; r.dir[1] = 0.f; r.dir[2] = 1.f; }
-      float off[3] = {r.pos[0] - cm[0], r.pos[1] - cm[1], r.pos[2] - cm[2]}, sa[3];
-      cross3(sa, off, r.dir);
-      float vel = 0.f;
+  float pos[3], dir[3], mu;
+  const float dist = contact_point(c, s, B, pos, dir, mu);
+  if (gvalid && dist < m->floor_margin) {
+    r.ex = true;
+    float off[3] = {pos[0] - cm[0], pos[1] - cm[1], pos[2] - cm[2]}, sa[3];
+    cross3(sa, off, dir);
+    float vel = 0.f;
 #pragma unroll
-      for (int e = 0; e < CAP; e++) {
-        if (e <= r.kdep) {
-          int a = anc_packed(r.ka0, r.ka1, r.ka2, e);
-          float v = sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
-                    r.dir[0] * L->cdof[a][3] + r.dir[1] * L->cdof[a][4] + r.dir[2] * L->cdof[a][5];
-          Jc[e] = v;
-          vel += v * L->vec[V_QVEL][a];
-        }
+    for (int e = 0; e < CAP; e++) {
+      if (e <= r.kdep) {
+        int a = anc_packed(r.ka0, r.ka1, r.ka2, e);
+        float v = sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
+                  dir[0] * L->cdof[a][3] + dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
+        Jc[e] = v;
+        vel += v * L->vec[V_QVEL][a];
       }
-      float dA = m->body_invweight0[gb][0] * (1.f + mu * mu);
-      float Rr;
-      row_params(m->floor_solref, m->floor_solimp, dist, dA, vel, cfg->dt, r.D, Rr, r.aref);
     }
+    float dA = m->body_invweight0[gb][0] * (1.f + mu * mu);
+    float Rr;
+    row_params(m->floor_solref, m->floor_solimp, dist, dA, vel, cfg->dt, r.D, Rr, r.aref);
   }
   /* compaction list of existing contact rows */
   uint64_t bal = __ballot(r.ex);
@@ -875,9 +904,9 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   if (l < c.nv) {
     float v = ls.v;
     float dA = m->dof_invweight0[l];
-    if (ls.floss > 0.f) {
+    if (c.L->par[P_FLOSS][c.l] > 0.f) {
       r.hf = true;
-      r.fl = ls.floss;
+      r.fl = c.L->par[P_FLOSS][c.l];
       row_params(m->dof_solref, m->dof_solimp, 0.f, dA, v, cfg->dt, r.Df, r.Rf, r.af);
     }
     if (m->dof_limited[l]) {
@@ -979,7 +1008,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
 __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float& Mv) {
-  const ZbEnvConfig* cfg = c.cfg;
+  CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
   r.Jv = r.ex ? row_dot(c, r, V_TMP) : 0.f;
@@ -1031,8 +1060,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
 __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters) {
-  const ZbEnvConfig* cfg = c.cfg;
-  const ZbModel* m = c.m;
+  CP cfg = c.cfg;
+  MP m = c.m;
   EnvL* L = c.L;
   /* warmstart selection */
   float x = w;
@@ -1097,7 +1126,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
 /* ----------------------------- Feetech actuator ---------------------------- */
 /* trapezoidal_step (train.py:1137-1196) + duty/torque (train.py:1260-1269) */
 __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
-  const ZbModel* m = c.m;
+  MP m = c.m;
   if (c.act < 0) { ls.ctrl = 0.f; return; }
   const int a = c.act;
   const float dt = c.cfg->dt;
@@ -1132,7 +1161,7 @@ __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
 /* mj_forward (+ sensors if requested). Leaves qacc in ls.qacc, kinematics in B. */
 __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
                                         Sensors& sen, int& iters) {
-  const ZbModel* m = c.m;
+  MP m = c.m;
   EnvL* L = c.L;
   STAMP(15);
   kinematics(c, s, ls, B);
@@ -1161,7 +1190,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   } else {
     ls.actforce = 0.f;
   }
-  float fs = (c.l < c.nv) ? (-ls.damp * ls.v - bias + act) : 0.f;
+  float fs = (c.l < c.nv) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
   STAMP(4);
   float qs = solve_ldl(c, fs, DinvM);
   STAMP(5);
@@ -1183,14 +1212,17 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   tsync();
   /* contact forces per geom -> cfrc_ext on the geom body, touch */
   float fext[6] = {0, 0, 0, 0, 0, 0};
-  sen.touch[0] = sen.touch[1] = 0.f;
+  float cpos[3], cdir[3], cmu;
+  (void)contact_point(c, s, B, cpos, cdir, cmu);
+  const int rgeom = c.l >> 4;
+  float tch0 = 0.f, tch1 = 0.f;
   for (int g = 0; g < c.ngeom; g++) {
-    bool mine = r.ex && r.geom == g;
+    bool mine = r.ex && rgeom == g;
     float F[3] = {0, 0, 0}, tq[3] = {0, 0, 0};
     float fn = 0.f;
     if (mine) {
-      F[0] = r.f * r.dir[0]; F[1] = r.f * r.dir[1]; F[2] = r.f * r.dir[2];
-      float off[3] = {r.pos[0] - cm[0], r.pos[1] - cm[1], r.pos[2] - cm[2]};
+      F[0] = r.f * cdir[0]; F[1] = r.f * cdir[1]; F[2] = r.f * cdir[2];
+      float off[3] = {cpos[0] - cm[0], cpos[1] - cm[1], cpos[2] - cm[2]};
       cross3(tq, off, F);
       fn = r.f;
     }
@@ -1200,9 +1232,11 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
 #pragma unroll
       for (int k = 0; k < 6; k++) fext[k] += ext[k];
     }
-    if (g == m->geom_left_foot) sen.touch[0] = fnt;
-    if (g == m->geom_right_foot) sen.touch[1] = fnt;
+    if (g == m->geom_left_foot) tch0 = fnt;
+    if (g == m->geom_right_foot) tch1 = fnt;
   }
+  sen.touch[0] = tch0;
+  sen.touch[1] = tch1;
   float cacc[6];
   {
     BodyK B2 = B; /* com_vel rewrites cvel identically; recompute cdofdot (aliased with J) */
@@ -1219,8 +1253,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     for (int k = 0; k < 4; k++) xq[k] = tsh(B.xq[k], sb);
 #pragma unroll
     for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], sb);
-#pragma unroll
-    for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], sb);
+    quat2mat(R, xq);
 #pragma unroll
     for (int k = 0; k < 6; k++) { cv[k] = tsh(B.cv[k], sb); cc[k] = tsh(cacc[k], sb); }
     float sq[4];
@@ -1289,18 +1322,21 @@ __device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls) {
 
 /* --------------------------- env-level (ksim) logic ------------------------- */
 __device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, const float* rnd) {
-  const ZbModel* m = c.m;
+  MP m = c.m;
   const bool rz = (c.cfg->flags & ZB_F_RANDOMIZE) && rnd;
   const int l = c.l;
-  ls.mscale = (rz && l < c.nb) ? rnd[ZB_R_MASS + l] : 1.f;
-  ls.arm = ls.damp = ls.floss = 0.f;
-  ls.q0 = 0.f;
+  float arm = 0.f, damp = 0.f, floss = 0.f, q0 = 0.f;
   if (l < c.nv) {
-    ls.arm = m->dof_armature[l] * (rz ? rnd[ZB_R_ARMATURE + l] : 1.f);
-    ls.damp = m->dof_damping[l] * (rz ? rnd[ZB_R_DAMPING + l] : 1.f);
-    ls.floss = m->dof_frictionloss[l] * (rz ? rnd[ZB_R_FRICTION + l] : 1.f);
-    if (c.qadr >= 0) ls.q0 = m->qpos0[c.qadr] + ((rz && c.act >= 0) ? rnd[ZB_R_QPOS0 + c.act] : 0.f);
+    arm = m->dof_armature[l] * (rz ? rnd[ZB_R_ARMATURE + l] : 1.f);
+    damp = m->dof_damping[l] * (rz ? rnd[ZB_R_DAMPING + l] : 1.f);
+    floss = m->dof_frictionloss[l] * (rz ? rnd[ZB_R_FRICTION + l] : 1.f);
+    if (c.qadr >= 0) q0 = m->qpos0[c.qadr] + ((rz && c.act >= 0) ? rnd[ZB_R_QPOS0 + c.act] : 0.f);
   }
+  c.L->par[P_MSCALE][l] = (rz && l < c.nb) ? rnd[ZB_R_MASS + l] : 1.f;
+  c.L->par[P_ARM][l] = arm;
+  c.L->par[P_DAMP][l] = damp;
+  c.L->par[P_FLOSS][l] = floss;
+  c.L->par[P_Q0][l] = q0;
   s.floor_mu = rz ? rnd[ZB_R_FLOOR_MU] : 1.f;
   int si = m->site_imu;
   float sq[4] = {m->site_quat[si][0], m->site_quat[si][1], m->site_quat[si][2], m->site_quat[si][3]};
@@ -1318,7 +1354,7 @@ __device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, co
 
 /* randomizer sampling (must match oracle/zb_oracle.c sample_rand) */
 __device__ __forceinline__ void sample_rand(const Ctx& c, uint32_t episode, float* rnd) {
-  const ZbEnvConfig* cfg = c.cfg;
+  CP cfg = c.cfg;
   const int l = c.l;
   for (int k = l; k < 75; k += TEAM) {
     float u0, u1;
@@ -1370,8 +1406,8 @@ __device__ __forceinline__ void rotate_quat_by_quat(const float q_[4], const flo
 /* observation assembly + obs-derived carries (train.py:1478-1537, 1624-1679) */
 __device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, const Sensors& sen, float* oa,
                         float* oc, float* ox) {
-  const ZbModel* m = c.m;
-  const ZbEnvConfig* cfg = c.cfg;
+  MP m = c.m;
+  CP cfg = c.cfg;
   const int l = c.l;
   /* ImuOrientationObservation (heading command 0) */
   float hq[4] = {1.f, 0.f, 0.f, 0.f}, bq[4];
@@ -1402,9 +1438,10 @@ __device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, 
     int sides[2] = {m->site_left_foot, m->site_right_foot};
     for (int sd = 0; sd < 2; sd++) {
       int ss = sides[sd], sb = m->site_body[ss];
-      float xp[3], R[9], t[3];
+      float xp[3], R[9], t[3], xqs[4];
       for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], sb);
-      for (int k = 0; k < 9; k++) R[k] = tsh(B.R[k], sb);
+      for (int k = 0; k < 4; k++) xqs[k] = tsh(B.xq[k], sb);
+      quat2mat(R, xqs);
       float sp[3] = {m->site_pos[ss][0], m->site_pos[ss][1], m->site_pos[ss][2]};
       mulmv3(t, R, sp);
       float w[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
@@ -1435,7 +1472,7 @@ __device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, 
       oc[457 + l] = fa / 100.f;
     }
     if (l >= 1 && l < c.nb) {
-      for (int k = 0; k < 10; k++) oc[40 + (l - 1) * 10 + k] = B.ci[k];
+      for (int k = 0; k < 10; k++) oc[40 + (l - 1) * 10 + k] = c.L->ci[l][k];
       for (int k = 0; k < 6; k++) oc[290 + (l - 1) * 6 + k] = B.cv[k];
     }
     if (l < 3) oc[440 + l] = acc[l];
@@ -1483,8 +1520,8 @@ __device__ __forceinline__ void quat_roll_pitch(const float q_[4], float& roll, 
 /* terminations + reward terms (train.py:1546-1593) ; returns done */
 __device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, float cur, float* terms_out,
                         float& total, bool& fail) {
-  const ZbModel* m = c.m;
-  const ZbEnvConfig* cfg = c.cfg;
+  MP m = c.m;
+  CP cfg = c.cfg;
   const int l = c.l;
   float z = s.bp[2];
   float bq[4] = {s.bq[0], s.bq[1], s.bq[2], s.bq[3]};
@@ -1635,8 +1672,8 @@ __device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const L
 
 /* ksim reset (train.py:1471-1476); the caller then runs mjx.forward (forward()) */
 __device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, float* rnd) {
-  const ZbModel* m = c.m;
-  const ZbEnvConfig* cfg = c.cfg;
+  MP m = c.m;
+  CP cfg = c.cfg;
   const int l = c.l;
   uint32_t episode = s.episode;
   if ((cfg->flags & ZB_F_RANDOMIZE) && rnd) {
@@ -1651,7 +1688,7 @@ __device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, 
   ls.w = 0.f;
   if (c.act >= 0) {
     int qa = c.qadr;
-    ls.q = m->joint_bias[c.act] + (ls.q0 - m->qpos0[qa]);
+    ls.q = m->joint_bias[c.act] + (c.L->par[P_Q0][c.l] - m->qpos0[qa]);
     float u0, u1;
     uniform2(c.seed, P_RESET, (uint32_t)(c.act / 2), c.env, episode, u0, u1);
     float u = (c.act & 1) ? u1 : u0;
@@ -1677,7 +1714,7 @@ __device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, 
 
 /* push event (train.py:1459-1468) */
 __device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, float cur) {
-  const ZbEnvConfig* cfg = c.cfg;
+  CP cfg = c.cfg;
   float timer = s.push_timer - cfg->ctrl_dt;
   if (timer <= 0.f) {
     float u0, u1, w0, w1;
@@ -1693,11 +1730,10 @@ __device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, flo
 }
 
 /* ---------------------------- per-team context ------------------------------ */
-__device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvConfig* cfg, EnvL* L, const Sched* S,
+__device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvConfig* cfg, EnvL* L,
                                          uint64_t seed, uint32_t env) {
-  c.m = m;
-  c.S = S;
-  c.cfg = cfg;
+  c.m = (MP)m;
+  c.cfg = (CP)cfg;
   c.L = L;
   c.seed = seed;
   c.env = env;
@@ -1775,18 +1811,6 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 }
 
 /* ---------------------------------- kernels --------------------------------- */
-__device__ __forceinline__ void fill_sched(const ZbModel* m, Sched* S) {
-  const int t = threadIdx.x;
-  if (t < 32) S->rowoff[t] = t < m->nv ? m->dof_rowoff[t] : m->mrow_size;
-  for (int i = t; i < ZB_MAX_DEPTH * 8; i += 64) {
-    int k = m->level_mem[i / 8][i % 8];
-    S->mem[i / 8][i % 8] = k;
-    S->memoff[i / 8][i % 8] = k >= 0 ? m->dof_rowoff[k] : m->mrow_size;
-  }
-  if (t < ZB_MAX_DEPTH) S->nmem[t] = m->level_nmem[t];
-  if (t == 0) S->nlevel = m->nlevel;
-  __syncthreads();
-}
 
 /* 2 waves per SIMD: the register allocator spills ~1 KB/lane of cold state to
    scratch (L1/L2-resident) instead of holding ~440 registers at 1 wave/SIMD;
@@ -1796,15 +1820,13 @@ __device__ __forceinline__ void fill_sched(const ZbModel* m, Sched* S) {
 #endif
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   __shared__ EnvL lds[NTEAM];
-  __shared__ Sched sched;
-  fill_sched(a.model, &sched);
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
   const ZbModel* m = a.model;
-  const ZbEnvConfig* cfg = &a.cfg;
+  const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], &sched, a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
 #ifdef ZB_STAMPS
@@ -1812,13 +1834,13 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   if (c.l == 0) c.L->stamp_last = __builtin_amdgcn_s_memtime();
   tsync();
 #endif
-  EnvS s;
+  EnvS& s = c.L->s;
   LaneS ls;
   load_state(c, s, ls, st);
   load_params(c, s, ls, rnd);
   BodyK B;
   Rows r;
-  Sensors sen;
+  Sensors& sen = c.L->sen;
   int iters = 0;
   float rsum = 0.f;
   bool done = false;
@@ -1834,6 +1856,8 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
     /* 20 substeps; when the env terminates, one more pass of the same code path
        runs the reset forward (mjx.forward after MjxEngine.reset) */
     while (true) {
+      c.m = opaque((MP)m);
+      c.cfg = opaque((CP)cfg);
       STAMP(14);
       if (!resetting) feetech(c, ls);
       STAMP(0);
@@ -1863,6 +1887,8 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       reset_prepare(c, s, ls, rnd);
       resetting = true;
     }
+    c.m = opaque((MP)m);
+    c.cfg = opaque((CP)cfg);
     if (last_t) {
       observe(c, s, ls, B, sen, a.obs_actor ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
               a.obs_critic ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
@@ -1887,24 +1913,22 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
 
 __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   __shared__ EnvL lds[NTEAM];
-  __shared__ Sched sched;
-  fill_sched(a.model, &sched);
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
   if (a.reset_mask && !a.reset_mask[e]) return;
   const ZbModel* m = a.model;
-  const ZbEnvConfig* cfg = &a.cfg;
+  const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], &sched, a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
-  EnvS s;
+  EnvS& s = c.L->s;
   LaneS ls;
   load_state(c, s, ls, st);
   BodyK B;
   Rows r;
-  Sensors sen;
+  Sensors& sen = c.L->sen;
   int it = 0;
   reset_prepare(c, s, ls, rnd);
   forward(c, s, ls, B, r, true, sen, it);
@@ -1917,24 +1941,22 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
 /* single forward on the stored (qpos, qvel), ctrl = action row; dumps internals */
 __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   __shared__ EnvL lds[NTEAM];
-  __shared__ Sched sched;
-  fill_sched(a.model, &sched);
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
   const ZbModel* m = a.model;
-  const ZbEnvConfig* cfg = &a.cfg;
+  const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], &sched, a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
-  EnvS s;
+  EnvS& s = c.L->s;
   LaneS ls;
   load_state(c, s, ls, st);
   load_params(c, s, ls, nullptr);
   ls.ctrl = (c.act >= 0 && a.action) ? a.action[(size_t)e * ZB_NJ + c.act] : 0.f;
   BodyK B;
   Rows r;
-  Sensors sen;
+  Sensors& sen = c.L->sen;
   int it = 0;
   forward(c, s, ls, B, r, true, sen, it);
   float* d = a.dbg + (size_t)e * ZB_DBG_STRIDE;
@@ -1957,7 +1979,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
      bias/qacc_smooth slots are filled by a second, constraint-free pass below */
   if (l < c.nb) {
     for (int k = 0; k < 3; k++) d[ZB_DBG_XPOS + 3 * l + k] = B.xp[k];
-    for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = B.ci[k];
+    for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = c.L->ci[l][k];
     for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
   }
   int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (r.hf ? 1 : 0) + (r.hlo ? 1 : 0) + (r.hhi ? 1 : 0)));
@@ -1982,7 +2004,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     com_acc(c, ca, false);
     float bias = rne_project(c, B, ca, z6);
     float act = c.act >= 0 ? m->act_gear[c.act] * ls.actforce : 0.f;
-    float fs = (l < c.nv) ? (-ls.damp * ls.v - bias + act) : 0.f;
+    float fs = (l < c.nv) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
     float qs = solve_ldl(c, fs, Dinv);
     if (l < c.nv) {
       d[ZB_DBG_BIAS + l] = bias;

@@ -25,7 +25,7 @@ namespace zb {
 
 struct StepArgs {
   const ZbModel* model;     /* device copy */
-  ZbEnvConfig cfg;
+  const ZbEnvConfig* cfg;   /* device copy */
   int n_envs;
   int env_offset;
   uint64_t seed;
