@@ -119,7 +119,7 @@ static int check_model(const ZbModel* m) {
   if (m->version != ZB_MODEL_VERSION) return fail(ZB_EARG, "model version %d != %d", m->version, ZB_MODEL_VERSION);
   if (m->struct_bytes != (int32_t)sizeof(ZbModel))
     return fail(ZB_EARG, "model struct_bytes %d != %zu (layout mismatch)", m->struct_bytes, sizeof(ZbModel));
-  if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
+  if (m->nbody > 32 || m->nv > 31 || m->nq > ZB_MAX_QPOS) /* factor row 31 is the engine's zero row */
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
   if (m->ngeom * ZB_CON_PER_GEOM * 4 > 32)
     return fail(ZB_EMODEL, "ngeom=%d: contact rows exceed the 32-lane team", m->ngeom);
@@ -180,7 +180,7 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMemset(h->stats, 0, n * ZB_NUM_STATS * sizeof(float));
   if (e == hipSuccess) e = hipMemset(h->iters, 0, n * sizeof(int32_t));
 #ifdef ZB_STAMPS
-  if (e == hipSuccess) e = hipMalloc(&h->stamps, n * 16 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc(&h->stamps, n * ZB_NSTAMP * sizeof(unsigned long long));
 #endif
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
@@ -328,7 +328,7 @@ int zb_debug_forward(ZbHandle* h, float* state_dev, const float* ctrl_dev, float
 #ifdef ZB_STAMPS
 int zb_get_stamps(ZbHandle* h, void* out_dev, void* stream) {
   if (!h || !h->stamps) return fail(ZB_EARG, "no stamps");
-  return copy_rows(h, out_dev, h->stamps, (size_t)h->n * 16 * sizeof(unsigned long long), stream);
+  return copy_rows(h, out_dev, h->stamps, (size_t)h->n * ZB_NSTAMP * sizeof(unsigned long long), stream);
 }
 #endif
 

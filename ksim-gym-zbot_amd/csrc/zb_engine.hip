@@ -41,8 +41,15 @@ constexpr float MINIMP = 0.0001f;
 constexpr float MAXIMP = 0.9999f;
 constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0); /* train.py:1113-1116 */
 
-enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3 };
+enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3, V_SOLVE = 4, NVEC = 5 };
+constexpr int ZROW = 31; /* all-zero factor row: target of the padded update slots */
 enum { P_Q0 = 0, P_ARM = 1, P_DAMP = 2, P_FLOSS = 3, P_MSCALE = 4 };
+/* stamp slots: STAMP(i) closes phase i (time since the previous stamp) */
+enum {
+  S_FEETECH, S_KIN, S_CRB, S_FACM, S_RNE, S_SOLVES, S_CON, S_WARM, S_UPD0, S_HESS0, S_SOLVE0, S_LS, S_UPD,
+  S_HESS, S_SOLVE, S_CHECK, S_SENS, S_INT, S_STEPEND, S_ENTRY, NSTAMP
+};
+static_assert(NSTAMP == ZB_NSTAMP, "stamp slots");
 
 /* per-env scalars: one copy per team in LDS, read by every lane (broadcast) and
    written by every lane with the bit-identical value it computed */
@@ -65,7 +72,7 @@ struct __align__(16) EnvL {
     float cdofdot[32][6]; /* velocity phase; recomputed for the sensors */
   } u;
   float sub[32][10];
-  float vec[4][32];
+  float vec[NVEC][32];
   float rowDA[32];
   float rowF[32];
   float Dk[32];
@@ -74,11 +81,14 @@ struct __align__(16) EnvL {
   EnvS s;
   Sensors sen;
 #ifdef ZB_STAMPS
-  unsigned long long stamp[16];
+  unsigned long long stamp[NSTAMP];
   unsigned long long stamp_last;
 #endif
 };
 
+
+/* the block's two team working sets (one wave = two teams) */
+__shared__ EnvL g_lds[NTEAM];
 
 /* ----------------------------- team primitives ----------------------------- */
 __device__ __forceinline__ float tsh(float v, int src) { return __shfl(v, src, TEAM); }
@@ -119,6 +129,17 @@ __device__ __forceinline__ int tmaxi(int v) {
   return v;
 }
 __device__ __forceinline__ void tsync() { __syncthreads(); }
+/* An opaque copy of a per-lane constant: stops the compiler from hoisting
+   compares against it (e.g. the 12 `e < depth` lane masks) out of the step
+   loops, where they would pin SGPR pairs for the whole launch. */
+__device__ __forceinline__ int vopq(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+/* bitmask over the team's lanes of predicate p */
+__device__ __forceinline__ uint32_t team_ballot(bool p) {
+  return (uint32_t)(__ballot(p) >> (threadIdx.x & 32));
+}
 
 /* Diagnostic phase stamps (separate build, -DZB_STAMPS): cycles per phase of the
    step, accumulated per env; never compiled into the product library. */
@@ -237,7 +258,13 @@ __device__ __forceinline__ void threefry2x32(uint32_t k0, uint32_t k1, uint32_t 
 #define P_RAND 4u
 __device__ __forceinline__ void rng_bits(uint64_t seed, uint32_t purpose, uint32_t k, uint32_t env, uint32_t ctr,
                                          uint32_t& a, uint32_t& b) {
-  threefry2x32((uint32_t)seed ^ (purpose * 0x9E3779B9u), (uint32_t)(seed >> 32) ^ (k * 0x85EBCA6Bu), env, ctr, a, b);
+  /* the key is re-derived at every draw site (opaque seed) so its round-key
+     schedule is not hoisted into SGPRs for the whole launch */
+  uint32_t slo = (uint32_t)seed, shi = (uint32_t)(seed >> 32);
+  asm volatile("" : "+v"(slo), "+v"(shi));
+  slo = __builtin_amdgcn_readfirstlane(slo);
+  shi = __builtin_amdgcn_readfirstlane(shi);
+  threefry2x32(slo ^ (purpose * 0x9E3779B9u), shi ^ (k * 0x85EBCA6Bu), env, ctr, a, b);
 }
 __device__ __forceinline__ float u01(uint32_t b) { return (float)(b >> 8) * (1.0f / 16777216.0f); }
 __device__ __forceinline__ void uniform2(uint64_t seed, uint32_t p, uint32_t k, uint32_t env, uint32_t ctr, float& u0,
@@ -295,10 +322,25 @@ struct Ctx {
   uint32_t desc; /* strict descendants of dof l */
   uint32_t rowmask; /* contact rows whose Jacobian chain contains dof l */
   int dk0;          /* index of dof l within its body's joint (free joint: 0..5) */
-  int moff;         /* offset of row l in packed M / L storage */
   int mylevel;      /* elimination level of dof l */
   int dfree;        /* dof l belongs to a free joint */
 };
+
+/* Per-function copy of the context with every per-lane field made opaque and
+   the LDS base re-derived: values derived from the context (LDS addresses of
+   parents/children/ancestors, depth masks) are then computed inside each
+   phase instead of being hoisted to the kernel prologue and held in
+   registers for the whole launch. */
+__device__ __forceinline__ Ctx fresh_ctx(const Ctx& c0) {
+  Ctx c = c0;
+  int team = (int)(threadIdx.x >> 5);
+  asm volatile("" : "+v"(team), "+v"(c.l), "+v"(c.bpar), "+v"(c.bdep), "+v"(c.bjt), "+v"(c.bdofadr),
+               "+v"(c.blast), "+v"(c.nch), "+v"(c.ch0), "+v"(c.ch1), "+v"(c.ddep), "+v"(c.dbody));
+  asm volatile("" : "+v"(c.qadr), "+v"(c.act), "+v"(c.anc0), "+v"(c.anc1), "+v"(c.anc2), "+v"(c.desc),
+               "+v"(c.rowmask), "+v"(c.dk0), "+v"(c.mylevel), "+v"(c.dfree), "+v"(c.env));
+  c.L = &g_lds[team];
+  return c;
+}
 
 __device__ __forceinline__ int ancof(const Ctx& c, int e) {
   uint32_t w = e < 4 ? c.anc0 : (e < 8 ? c.anc1 : c.anc2);
@@ -359,7 +401,8 @@ __device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
 }
 
 /* ------------------------------- kinematics -------------------------------- */
-__device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B) {
+__device__ __forceinline__ void kinematics(const Ctx& c_, const EnvS& s, const LaneS& ls, BodyK& B) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   /* relative hinge angle of this body's joint, from its dof lane */
   float qrel_dof = ls.q - c.L->par[P_Q0][c.l];
@@ -418,7 +461,8 @@ __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const La
 /* subtree sum of K-vectors over the body tree: out (lane b) = sum over subtree(b).
  * Uses c.L->sub as the exchange buffer; result also left in sub[b]. */
 template <int K>
-__device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
+__device__ __forceinline__ void subtree_sum(const Ctx& c_, float v[K]) {
+  const Ctx c = fresh_ctx(c_);
   EnvL* L = c.L;
   for (int d = c.maxbd; d >= 1; d--) {
     int nmax = (int)((c.lvlch >> (4 * d)) & 0xfull);
@@ -439,7 +483,9 @@ __device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
 
 /* ------------------------------ mass matrix -------------------------------- */
 /* com, cinert (lane b), cdof (lane j -> LDS), crb, M rows (LDS + return) */
-__device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B, float cm[3]) {
+__device__ __forceinline__ void com_crb_m(const Ctx& c_, const EnvS& s, const LaneS& ls, BodyK& B, float cm[3]) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   MP m = c.m;
   EnvL* L = c.L;
   const int b = c.l;
@@ -549,13 +595,13 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 #pragma unroll
       for (int e = 0; e < CAP; e++) {
         float v = 0.f;
-        if (e <= c.ddep) {
+        if (e <= ddep) {
           int a = ancof(c, e);
           float ca[6];
 #pragma unroll
           for (int k = 0; k < 6; k++) ca[k] = L->cdof[a][k];
           v = dot6(ca, F);
-          if (e == c.ddep) v += c.L->par[P_ARM][c.l];
+          if (e == ddep) v += c.L->par[P_ARM][c.l];
         }
         mr[e] = v;
       }
@@ -566,32 +612,48 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 }
 
 /* ---------------------- sparse L'DL factor + solves ------------------------ */
-/* Sparse L'DL (mj_factorM order: leaves first) of depth-indexed rows.
- * Lane j holds the off-diagonal entries X[e] = A(j, anc_e(j)), e < depth(j),
- * and the diagonal Xd. On return the L rows are in LDS L[][] (L(k, anc_e(k))),
- * the pivots in Dk[], and 1/D_j is returned. */
-__device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd) {
+/* Sparse L'DL of depth-indexed rows (mj_factorM), eliminated by LEVEL: the
+ * level of a dof is its height in the dof tree (leaves 0), so the dofs of one
+ * level are never ancestor/descendant of each other and are divided out
+ * together. Lane j holds the off-diagonal entries X[e] = A(j, anc_e(j)),
+ * e < depth(j), and the diagonal Xd; after level lv it applies the Schur
+ * updates of its level-lv descendants, two rows per pass with every load
+ * issued up front (padded slots read the all-zero row ZROW). On return the L
+ * rows are in LDS L[][] (L(k, anc_e(k))), pivots in Dk[]; returns 1/D_j. */
+__device__ __forceinline__ float factor_ldl(const Ctx& c_, float X[CAP], float Xd) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
-  const int j = c.l;
-  for (int k = c.nv - 1; k >= 0; k--) {
-    if (j == k) {
+  const int nlevel = c.m->nlevel;
+  for (int lv = 0; lv < nlevel; lv++) {
+    if (c.mylevel == lv) {
       float Dkv = fmaxf(Xd, MINVAL);
       float inv = 1.0f / Dkv;
 #pragma unroll
       for (int e = 0; e < CAP; e++) X[e] = X[e] * inv;
-      st_row(&L->L[k][0], X);
-      L->Dk[k] = Dkv;
+      st_row(&L->L[c.l][0], X);
+      L->Dk[c.l] = Dkv;
     }
     tsync();
-    if ((c.desc >> k) & 1u) {
-      float Dkv = L->Dk[k];
-      float lk = L->L[k][c.ddep]; /* L(k, j) */
-      float t = lk * Dkv;         /* A(k, j) after the Schur updates of k's subtree */
-      float row[CAP];
-      ld_row(&L->L[k][0], row);
-      Xd -= t * lk;
+    uint32_t dm = c.desc & team_ballot(c.mylevel == lv);
+    while (dm) {
+      const int k0 = __ffs(dm) - 1;
+      dm &= dm - 1u;
+      const int k1 = dm ? __ffs(dm) - 1 : ZROW;
+      dm &= dm - 1u;
+      float r0[CAP], r1[CAP];
+      ld_row(&L->L[k0][0], r0);
+      ld_row(&L->L[k1][0], r1);
+      const float d0 = L->Dk[k0], d1 = L->Dk[k1];
+      const float l0 = L->L[k0][ddep], l1 = L->L[k1][ddep]; /* L(k, j) */
+      const float t0 = l0 * d0, t1 = l1 * d1;                     /* A(k, j) after k's subtree */
+      Xd -= t0 * l0;
+      Xd -= t1 * l1;
 #pragma unroll
-      for (int e = 0; e < CAP; e++) X[e] -= (e < c.ddep ? t : 0.f) * row[e];
+      for (int e = 0; e < CAP; e++) {
+        X[e] -= (e < ddep ? t0 : 0.f) * r0[e];
+        X[e] -= (e < ddep ? t1 : 0.f) * r1[e];
+      }
     }
   }
   tsync();
@@ -599,32 +661,54 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
 }
 
 /* load a depth-indexed M row into off-diagonal X[] (masked) and diagonal */
-__device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
+__device__ __forceinline__ float load_mrow(const Ctx& c_, float X[CAP]) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   const int j = c.l & 31;
   ld_row(&c.L->M[j][0], X);
 #pragma unroll
-  for (int e = 0; e < CAP; e++) X[e] = (e < c.ddep && c.l < c.nv) ? X[e] : 0.f;
-  return (c.l < c.nv) ? c.L->M[j][c.ddep] : 1.f;
+  for (int e = 0; e < CAP; e++) X[e] = (e < ddep && c.l < c.nv) ? X[e] : 0.f;
+  return (c.l < c.nv) ? c.L->M[j][ddep] : 1.f;
 }
 
-/* x <- (L'DL)^-1 x, x held by dof lanes */
-__device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
+/* x <- (L'DL)^-1 x, x held by dof lanes. Forward pass by level (a lane's
+ * value is final once its level is reached; descendants' contributions come
+ * through LDS two at a time), then the diagonal, then the root-to-leaf pass
+ * over ancestors by depth. */
+__device__ __forceinline__ float solve_ldl(const Ctx& c_, float x, float Dinv) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
-  for (int k = c.nv - 1; k >= 0; k--) {
-    float xk = tsh(x, k);
-    if ((c.desc >> k) & 1u) x -= L->L[k][c.ddep] * xk;
+  const int nlevel = c.m->nlevel;
+  for (int lv = 0; lv < nlevel; lv++) {
+    if (c.mylevel == lv) L->vec[V_SOLVE][c.l] = x;
+    tsync();
+    uint32_t dm = c.desc & team_ballot(c.mylevel == lv);
+    while (dm) {
+      const int k0 = __ffs(dm) - 1;
+      dm &= dm - 1u;
+      const bool h1 = dm != 0u;
+      const int k1 = h1 ? __ffs(dm) - 1 : k0;
+      dm &= dm - 1u;
+      const float a0 = L->L[k0][ddep] * L->vec[V_SOLVE][k0];
+      const float a1 = L->L[k1][ddep] * L->vec[V_SOLVE][k1];
+      x -= a0;
+      x -= h1 ? a1 : 0.f;
+    }
   }
   x *= Dinv;
   for (int e = 0; e < c.maxdd - 1; e++) {
-    int a = e <= c.ddep ? ancof(c, e) : 0;
+    int a = e <= ddep ? ancof(c, e) : 0;
     float xa = tsh(x, a);
-    if (e < c.ddep) x -= L->L[c.l][e] * xa;
+    if (e < ddep) x -= L->L[c.l][e] * xa;
   }
   return x;
 }
 
 /* y = M x (M rows in LDS), x in dof lanes; uses vec[slot] */
-__device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
+__device__ __forceinline__ float mul_m(const Ctx& c_, float x, int slot) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int j = c.l;
   if (j < 32) L->vec[slot][j] = x;
@@ -633,12 +717,12 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   if (j < c.nv) {
 #pragma unroll
     for (int e = 0; e < CAP; e++)
-      if (e <= c.ddep) y += L->M[j][e] * L->vec[slot][ancof(c, e)];
+      if (e <= ddep) y += L->M[j][e] * L->vec[slot][ancof(c, e)];
     uint32_t dm = c.desc;
     while (dm) {
       int k = __ffs(dm) - 1;
       dm &= dm - 1;
-      y += L->M[k][c.ddep] * L->vec[slot][k];
+      y += L->M[k][ddep] * L->vec[slot][k];
     }
   }
   tsync();
@@ -646,25 +730,29 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
 }
 
 /* chain gather: sum_e Jc[e] * vec[slot][anc_e] for a contact row */
-__device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) {
+__device__ __forceinline__ float row_dot(const Ctx& c_, const Rows& r, int slot) {
+  const Ctx c = fresh_ctx(c_);
+  const int kdep = vopq(r.kdep);
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < CAP; e++)
-    if (e <= r.kdep) v += c.L->u.J[c.l][e] * c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
+    if (e <= kdep) v += c.L->u.J[c.l][e] * c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
   return v;
 }
 
 /* ----------------------------------- RNE ----------------------------------- */
 /* cvel (lane b), cdofdot (LDS). Requires vec[V_QVEL]. */
-__device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
+__device__ __forceinline__ void com_vel(const Ctx& c_, BodyK& B) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   MP m = c.m;
   EnvL* L = c.L;
   const int j = c.l;
   if (j < c.nv) {
     const int k0 = c.dk0;
     const bool isfree = c.dfree;
-    int cap = c.ddep;                     /* hinge: before own contribution */
-    if (isfree) cap = c.ddep - k0 + 3;    /* free rot: after the translations */
+    int cap = ddep;                     /* hinge: before own contribution */
+    if (isfree) cap = ddep - k0 + 3;    /* free rot: after the translations */
     float acc[6] = {0, 0, 0, 0, 0, 0}, before[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < CAP; e++) {
@@ -672,7 +760,7 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
 #pragma unroll
         for (int k = 0; k < 6; k++) before[k] = acc[k];
       }
-      if (e <= c.ddep) {
+      if (e <= ddep) {
         int a = ancof(c, e);
         float qv = L->vec[V_QVEL][a];
 #pragma unroll
@@ -703,7 +791,9 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
 }
 
 /* cacc per body (lane b) with or without qacc (vec[V_QACC]) */
-__device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc) {
+__device__ __forceinline__ void com_acc(const Ctx& c_, float ca[6], bool with_acc) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   MP m = c.m;
   EnvL* L = c.L;
   const int j = c.l;
@@ -711,7 +801,7 @@ __device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc
     float acc[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
 #pragma unroll
     for (int e = 0; e < CAP; e++) {
-      if (e <= c.ddep) {
+      if (e <= ddep) {
         int a = ancof(c, e);
         float qv = L->vec[V_QVEL][a];
 #pragma unroll
@@ -737,7 +827,8 @@ __device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc
 }
 
 /* body force cfrc (lane b) -> subtree sums in sub[] ; returns dof projection cdof_j . sub[body(j)] */
-__device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const float ca[6], const float fext[6]) {
+__device__ __forceinline__ float rne_project(const Ctx& c_, const BodyK& B, const float ca[6], const float fext[6]) {
+  const Ctx c = fresh_ctx(c_);
   EnvL* L = c.L;
   float f[6];
   if (c.l >= 1 && c.l < c.nb) {
@@ -801,8 +892,9 @@ __device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, floa
  * n +- mu t (frame of mju_makeFrame(+z): t1 = +y, t2 = -x) and the friction
  * coefficient; returns the signed distance (> margin: no contact). Recomputed
  * by the sensors instead of being held in registers through the solver. */
-__device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, const BodyK& B, float pos[3], float dir[3],
+__device__ __forceinline__ float contact_point(const Ctx& c_, const EnvS& s, const BodyK& B, float pos[3], float dir[3],
                                                float& mu) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   const int l = c.l;
   const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
@@ -835,8 +927,9 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
 }
 
 /* collision + contact rows (lane r) + dof rows (lane j) */
-__device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
+__device__ __forceinline__ void make_constraints(const Ctx& c_, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
                                  Rows& r) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   CP cfg = c.cfg;
   EnvL* L = c.L;
@@ -937,7 +1030,8 @@ __device__ __forceinline__ float eval_one(float jar, float D, float& force, int&
 }
 
 /* row costs at given jar values (no state change) */
-__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jlo_, float jhi_) {
+__device__ __forceinline__ float rows_cost(const Ctx& c_, const Rows& r, float jc, float jf_, float jlo_, float jhi_) {
+  const Ctx c = fresh_ctx(c_);
   float cost = 0.f, f;
   int a;
   if (r.ex) cost += eval_one(jc, r.D, f, a);
@@ -948,7 +1042,9 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
 }
 
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
-__device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float qacc, float qs, float fs, float Ma, float& grad) {
+__device__ __forceinline__ float update_constraint(const Ctx& c_, Rows& r, float qacc, float qs, float fs, float Ma, float& grad) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float cost = 0.f;
   if (c.l < c.nv) cost += 0.5f * (Ma - fs) * (qacc - qs);
@@ -967,7 +1063,7 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
     while (tb) {
       int row = __ffs(tb) - 1;
       tb &= tb - 1u;
-      if ((c.rowmask >> row) & 1u) qc += L->u.J[row][c.ddep] * L->rowF[row];
+      if ((c.rowmask >> row) & 1u) qc += L->u.J[row][ddep] * L->rowF[row];
     }
     if (r.hf) qc += r.ff;
     if (r.hlo) qc += r.flo;
@@ -978,7 +1074,9 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
 }
 
 /* H = M + J' D_active J rows (depth-indexed), then factor -> Dinv */
-__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
+__device__ __forceinline__ float hessian_factor(const Ctx& c_, const Rows& r) {
+  const Ctx c = fresh_ctx(c_);
+  const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float H[CAP];
   float Hd = load_mrow(c, H);
@@ -988,13 +1086,13 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
       int row = __ffs(tb) - 1;
       tb &= tb - 1u;
       float da = L->rowDA[row];
-      float jd = L->u.J[row][c.ddep];
+      float jd = L->u.J[row][ddep];
       float jr[CAP];
       ld_row(&L->u.J[row][0], jr);
       float jj = da * jd;
       Hd += jj * jd;
 #pragma unroll
-      for (int e = 0; e < CAP; e++) H[e] += (e < c.ddep ? jj : 0.f) * jr[e];
+      for (int e = 0; e < CAP; e++) H[e] += (e < ddep ? jj : 0.f) * jr[e];
     }
     float dd = 0.f;
     if (r.hf && r.actf) dd += r.Df;
@@ -1007,7 +1105,8 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
-__device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float& Mv) {
+__device__ __forceinline__ float line_search(const Ctx& c_, Rows& r, float search, float Ma, float fs, float& Mv) {
+  const Ctx c = fresh_ctx(c_);
   CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
@@ -1059,7 +1158,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
 }
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
-__device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters) {
+__device__ __forceinline__ float solve_newton(const Ctx& c_, Rows& r, float qs, float fs, float w, int& iters) {
+  const Ctx c = fresh_ctx(c_);
   CP cfg = c.cfg;
   MP m = c.m;
   EnvL* L = c.L;
@@ -1081,20 +1181,24 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   } else {
     r.jar = jw;
   }
+  STAMP(S_WARM);
   r.jf = x - r.af;
   r.jlo = x - r.alo;
   r.jhi = -x - r.ahi;
   float scale = 1.0f / (m->meaninertia * (float)(c.nv > 1 ? c.nv : 1));
   float grad;
   float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
+  STAMP(S_UPD0);
   float Dinv = hessian_factor(c, r);
+  STAMP(S_HESS0);
   float search = -solve_ldl(c, grad, Dinv);
+  STAMP(S_SOLVE0);
   int it = 0;
   while (it < cfg->iterations) {
     float Mv;
-    STAMP(7);
+    STAMP(S_CHECK);
     float alpha = line_search(c, r, search, Ma, fs, Mv);
-    STAMP(8);
+    STAMP(S_LS);
     if (alpha == 0.f) break;
     x += alpha * search;
     Ma += alpha * Mv;
@@ -1108,11 +1212,11 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = tmaxi((r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1 : 0) != 0;
-    STAMP(9);
+    STAMP(S_UPD);
     if (changed) Dinv = hessian_factor(c, r);
-    STAMP(10);
+    STAMP(S_HESS);
     float mg = solve_ldl(c, grad, Dinv);
-    STAMP(11);
+    STAMP(S_SOLVE);
     it++;
     float improvement = scale * (oldcost - cost);
     float gradient = scale * sqrtf(tsum(c.l < c.nv ? grad * grad : 0.f));
@@ -1125,7 +1229,8 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
 
 /* ----------------------------- Feetech actuator ---------------------------- */
 /* trapezoidal_step (train.py:1137-1196) + duty/torque (train.py:1260-1269) */
-__device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
+__device__ __forceinline__ void feetech(const Ctx& c_, LaneS& ls) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   if (c.act < 0) { ls.ctrl = 0.f; return; }
   const int a = c.act;
@@ -1159,21 +1264,22 @@ __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
 
 /* ------------------------------- full forward ------------------------------ */
 /* mj_forward (+ sensors if requested). Leaves qacc in ls.qacc, kinematics in B. */
-__device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
+__device__ __forceinline__ void forward(const Ctx& c_, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
                                         Sensors& sen, int& iters) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   EnvL* L = c.L;
-  STAMP(15);
+  STAMP(S_ENTRY);
   kinematics(c, s, ls, B);
-  STAMP(1);
+  STAMP(S_KIN);
   float cm[3];
   com_crb_m(c, s, ls, B, cm);
-  STAMP(2);
+  STAMP(S_CRB);
   /* factor M (copy of rows) */
   float X[CAP];
   float Xd = load_mrow(c, X);
   float DinvM = factor_ldl(c, X, Xd);
-  STAMP(3);
+  STAMP(S_FACM);
   /* velocities */
   if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < c.nv ? ls.v : 0.f;
   tsync();
@@ -1191,12 +1297,12 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     ls.actforce = 0.f;
   }
   float fs = (c.l < c.nv) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
-  STAMP(4);
+  STAMP(S_RNE);
   float qs = solve_ldl(c, fs, DinvM);
-  STAMP(5);
+  STAMP(S_SOLVES);
   /* constraints */
   make_constraints(c, s, ls, B, cm, r);
-  STAMP(6);
+  STAMP(S_CON);
   int nrows = tmaxi(r.nrow + (r.hf || r.hlo || r.hhi ? 1 : 0));
   float qacc;
   if (nrows == 0) {
@@ -1205,7 +1311,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     qacc = solve_newton(c, r, qs, fs, ls.w, iters);
   }
   ls.qacc = (c.l < c.nv) ? qacc : 0.f;
-  STAMP(7);
+  STAMP(S_CHECK);
   if (!with_sensors) return;
   /* ------------------- sensors (mj_rnePostConstraint etc.) ------------------ */
   if (c.l < 32) L->vec[V_QACC][c.l] = ls.qacc;
@@ -1291,11 +1397,12 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     }
   }
   tsync();
-  STAMP(12);
+  STAMP(S_SENS);
 }
 
 /* ------------------------------ Euler integrate ----------------------------- */
-__device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls) {
+__device__ __forceinline__ void integrate(const Ctx& c_, EnvS& s, LaneS& ls) {
+  const Ctx c = fresh_ctx(c_);
   const float dt = c.cfg->dt;
   float vn = ls.v + dt * ls.qacc;
   float v0 = tsh(vn, 0), v1 = tsh(vn, 1), v2 = tsh(vn, 2), w0 = tsh(vn, 3), w1 = tsh(vn, 4), w2 = tsh(vn, 5);
@@ -1321,7 +1428,8 @@ __device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls) {
 }
 
 /* --------------------------- env-level (ksim) logic ------------------------- */
-__device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, const float* rnd) {
+__device__ __forceinline__ void load_params(const Ctx& c_, EnvS& s, LaneS& ls, const float* rnd) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   const bool rz = (c.cfg->flags & ZB_F_RANDOMIZE) && rnd;
   const int l = c.l;
@@ -1353,7 +1461,8 @@ __device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, co
 }
 
 /* randomizer sampling (must match oracle/zb_oracle.c sample_rand) */
-__device__ __forceinline__ void sample_rand(const Ctx& c, uint32_t episode, float* rnd) {
+__device__ __forceinline__ void sample_rand(const Ctx& c_, uint32_t episode, float* rnd) {
+  const Ctx c = fresh_ctx(c_);
   CP cfg = c.cfg;
   const int l = c.l;
   for (int k = l; k < 75; k += TEAM) {
@@ -1404,8 +1513,9 @@ __device__ __forceinline__ void rotate_quat_by_quat(const float q_[4], const flo
 }
 
 /* observation assembly + obs-derived carries (train.py:1478-1537, 1624-1679) */
-__device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, const Sensors& sen, float* oa,
+__device__ __forceinline__ void observe(const Ctx& c_, EnvS& s, const LaneS& ls, const BodyK& B, const Sensors& sen, float* oa,
                         float* oc, float* ox) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   CP cfg = c.cfg;
   const int l = c.l;
@@ -1518,8 +1628,9 @@ __device__ __forceinline__ void quat_roll_pitch(const float q_[4], float& roll, 
 }
 
 /* terminations + reward terms (train.py:1546-1593) ; returns done */
-__device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, float cur, float* terms_out,
+__device__ __forceinline__ bool rewards(const Ctx& c_, EnvS& s, const LaneS& ls, const BodyK& B, float cur, float* terms_out,
                         float& total, bool& fail) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   CP cfg = c.cfg;
   const int l = c.l;
@@ -1607,7 +1718,8 @@ __device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, 
 }
 
 /* ------------------------------ state I/O ---------------------------------- */
-__device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, const float* st) {
+__device__ __forceinline__ void load_state(const Ctx& c_, EnvS& s, LaneS& ls, const float* st) {
+  const Ctx c = fresh_ctx(c_);
   const int l = c.l;
   for (int k = 0; k < 3; k++) s.bp[k] = st[ZB_S_QPOS + k];
   for (int k = 0; k < 4; k++) s.bq[k] = st[ZB_S_QPOS + 3 + k];
@@ -1640,7 +1752,8 @@ __device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, con
   ls.actforce = 0.f;
 }
 
-__device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const LaneS& ls, float* st) {
+__device__ __forceinline__ void store_state(const Ctx& c_, const EnvS& s, const LaneS& ls, float* st) {
+  const Ctx c = fresh_ctx(c_);
   const int l = c.l;
   if (l < c.nv) {
     st[ZB_S_QVEL + l] = ls.v;
@@ -1671,7 +1784,8 @@ __device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const L
 }
 
 /* ksim reset (train.py:1471-1476); the caller then runs mjx.forward (forward()) */
-__device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, float* rnd) {
+__device__ __forceinline__ void reset_prepare(const Ctx& c_, EnvS& s, LaneS& ls, float* rnd) {
+  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   CP cfg = c.cfg;
   const int l = c.l;
@@ -1713,7 +1827,8 @@ __device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, 
 }
 
 /* push event (train.py:1459-1468) */
-__device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, float cur) {
+__device__ __forceinline__ void push_event(const Ctx& c_, EnvS& s, LaneS& ls, float cur) {
+  const Ctx c = fresh_ctx(c_);
   CP cfg = c.cfg;
   float timer = s.push_timer - cfg->ctrl_dt;
   if (timer <= 0.f) {
@@ -1802,12 +1917,18 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   }
   c.rowmask = rm;
   c.dk0 = isd ? l - m->body_dofadr[c.dbody] : 0;
-  c.moff = isd ? m->dof_rowoff[l] : m->mrow_size;
   c.mylevel = -1;
   for (int lv = 0; lv < m->nlevel; lv++)
     for (int mi = 0; mi < m->level_nmem[lv]; mi++)
       if (isd && m->level_mem[lv][mi] == l) c.mylevel = lv;
   c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
+  if (l == ZROW) {
+    float z[CAP];
+#pragma unroll
+    for (int e = 0; e < CAP; e++) z[e] = 0.f;
+    st_row(&L->L[ZROW][0], z);
+    L->Dk[ZROW] = 0.f;
+  }
 }
 
 /* ---------------------------------- kernels --------------------------------- */
@@ -1819,18 +1940,17 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 #define ZB_WAVES_PER_EU 2
 #endif
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
-  __shared__ EnvL lds[NTEAM];
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
 #ifdef ZB_STAMPS
-  if (c.l < 16) c.L->stamp[c.l] = 0;
+  if (c.l < NSTAMP) c.L->stamp[c.l] = 0;
   if (c.l == 0) c.L->stamp_last = __builtin_amdgcn_s_memtime();
   tsync();
 #endif
@@ -1858,13 +1978,13 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
     while (true) {
       c.m = opaque((MP)m);
       c.cfg = opaque((CP)cfg);
-      STAMP(14);
+      STAMP(S_STEPEND);
       if (!resetting) feetech(c, ls);
-      STAMP(0);
+      STAMP(S_FEETECH);
       forward(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, iters);
       if (resetting) break;
       integrate(c, s, ls);
-      STAMP(13);
+      STAMP(S_INT);
       if (++ss < cfg->n_substeps) continue;
       {
         bool bad = (c.l < c.nv) && !(isfinite(ls.q) && isfinite(ls.v));
@@ -1905,14 +2025,13 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   if (a.iters && c.l == 0) a.iters[e] = iters;
   store_state(c, s, ls, st);
 #ifdef ZB_STAMPS
-  STAMP(14);
+  STAMP(S_STEPEND);
   if (a.dbg && c.l == 0)
-    for (int i = 0; i < 16; i++) reinterpret_cast<unsigned long long*>(a.dbg)[(size_t)e * 16 + i] = c.L->stamp[i];
+    for (int i = 0; i < NSTAMP; i++) reinterpret_cast<unsigned long long*>(a.dbg)[(size_t)e * NSTAMP + i] = c.L->stamp[i];
 #endif
 }
 
 __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
-  __shared__ EnvL lds[NTEAM];
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
@@ -1920,7 +2039,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
   EnvS& s = c.L->s;
@@ -1940,14 +2059,13 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
 
 /* single forward on the stored (qpos, qvel), ctrl = action row; dumps internals */
 __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
-  __shared__ EnvL lds[NTEAM];
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
   if (e >= a.n_envs) return;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &lds[team], a.seed, (uint32_t)(a.env_offset + e));
+  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + e));
   float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
   EnvS& s = c.L->s;
   LaneS ls;

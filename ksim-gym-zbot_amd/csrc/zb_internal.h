@@ -20,6 +20,7 @@
 #define ZB_DBG_CVEL    1536  /* [nbody*6] */
 #define ZB_DBG_MISC    1728  /* nefc, ncon, touch_l, touch_r, imu quat(4), gyro(3), acc(3) */
 #define ZB_DBG_STRIDE  1760
+#define ZB_NSTAMP      20    /* phase-stamp slots of the -DZB_STAMPS build (zb_engine.hip S_*) */
 
 namespace zb {
 

@@ -20,8 +20,10 @@ from zbot_amd import compile_model, default_config  # noqa: E402
 from zbot_amd.engine import HipEngine  # noqa: E402
 
 PHASES = ["feetech", "kinematics", "com_crb_M", "factor_M", "rne_bias", "solve_smooth", "constraints",
-          "newton_init", "line_search", "update_constraint", "hessian_factor", "newton_solve", "sensors",
-          "integrate", "step_end(obs/reward/reset)", "forward_entry"]
+          "nw_warmstart", "nw_update0", "nw_hessian0", "nw_solve0", "line_search", "update_constraint",
+          "hessian_refactor", "newton_solve", "newton_check", "sensors", "integrate", "step_end(obs/reward/reset)",
+          "forward_entry"]
+NS = len(PHASES)
 
 
 def main():
@@ -36,15 +38,15 @@ def main():
     eng.L.zb_get_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     eng.reset()
     bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
-    tot = torch.zeros(16, dtype=torch.float64)
+    tot = torch.zeros(NS, dtype=torch.float64)
     for t in range(args.steps):
         eng.step(bias + 0.05 * torch.randn(args.n, 20, device="cuda"))
-        buf = torch.zeros(args.n, 16, dtype=torch.int64, device="cuda")
+        buf = torch.zeros(args.n, NS, dtype=torch.int64, device="cuda")
         eng.L.zb_get_stamps(eng.h, buf.data_ptr(), eng._stream())
         torch.cuda.synchronize()
         tot += buf.double().sum(0).cpu()
     share = tot / tot.sum()
-    res = {PHASES[i]: round(float(share[i]) * 100, 2) for i in range(16)}
+    res = {PHASES[i]: round(float(share[i]) * 100, 2) for i in range(NS)}
     res["cycles_per_env_step"] = float(tot.sum() / (args.n * args.steps))
     print(json.dumps(res, indent=1))
     if args.out:

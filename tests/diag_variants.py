@@ -30,6 +30,14 @@ def main():
         for t in range(3):
             e.step(acts[t])
     torch.cuda.synchronize()
+    # screening parity: every variant against the first library after the same 3 steps
+    ref = engs[0].get_state()
+    for p, e in zip(a.libs[1:], engs[1:]):
+        st = e.get_state()
+        dq = (st[:, :27] - ref[:, :27]).abs().max().item()
+        dv = (st[:, 32:58] - ref[:, 32:58]).abs().max().item()
+        bad = int((~torch.isfinite(st[:, :58])).sum().item())
+        print(f"{os.path.basename(p):32s} vs {os.path.basename(a.libs[0])}: max|dqpos| {dq:.2e} max|dqvel| {dv:.2e} nonfinite {bad}")
     res = {p: [] for p in a.libs}
     for r in range(a.rounds):
         for p, e in zip(a.libs, engs):
