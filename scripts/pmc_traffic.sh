@@ -1,7 +1,8 @@
 #!/bin/bash
 # Separate rocprofv3 PMC passes over a short C2 bench (run on the GPU box):
 #   FETCH_SIZE, WRITE_SIZE (cannot share a TCC pass) and fp32 VALU instruction
-#   counts; then summarise into profiles/pmc_traffic_c2.json.
+#   counts; summarised into gpurun_out/pmc_traffic_c2.json (copied into
+#   profiles/ so a following bench.py run in the same call reports it).
 set -e -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -13,4 +14,6 @@ for pass in fetch:FETCH_SIZE write:WRITE_SIZE "valu:SQ_INSTS_VALU_FMA_F32 SQ_INS
   rm -rf gpurun_out/pmc_$name
   timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d gpurun_out/pmc_$name -o run -- python3 $B > gpurun_out/pmc_$name.log 2>&1
 done
-python3 scripts/pmc_summary.py --config c2 --envs 8192 --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write --valu gpurun_out/pmc_valu
+python3 scripts/pmc_summary.py --config c2 --envs 8192 --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write \
+  --valu gpurun_out/pmc_valu --out gpurun_out/pmc_traffic_c2.json
+cp gpurun_out/pmc_traffic_c2.json profiles/pmc_traffic_c2.json
