@@ -43,6 +43,7 @@ constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0)
 
 enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3, V_SOLVE = 4, NVEC = 5 };
 constexpr int ZROW = 31; /* all-zero factor row: target of the padded update slots */
+constexpr int RMAX = 6;  /* longest root dof chain factored as one dense block (free joint) */
 enum { P_Q0 = 0, P_ARM = 1, P_DAMP = 2, P_FLOSS = 3, P_MSCALE = 4 };
 /* stamp slots: STAMP(i) closes phase i (time since the previous stamp) */
 enum {
@@ -76,6 +77,7 @@ struct __align__(16) EnvL {
   float rowDA[32];
   float rowF[32];
   float Dk[32];
+  float Di[32];      /* 1 / pivot of the root-chain block */
   float ci[32][10];  /* body cinert (lane b), kept for RNE / sensors / observations */
   float par[5][32];  /* effective dof / body parameters (lane), see P_* */
   EnvS s;
@@ -312,6 +314,7 @@ struct Ctx {
   uint32_t env;
   int l;
   int nb, nv, nu, ngeom, maxbd, maxdd;
+  int nroot; /* dofs 0..nroot-1: the unbranched chain at the top of the dof tree (one per top level) */
   /* lane as body */
   int bpar, bdep, bjt, bdofadr, blast, nch;
   uint32_t ch0, ch1;
@@ -326,21 +329,6 @@ struct Ctx {
   int dfree;        /* dof l belongs to a free joint */
 };
 
-/* Per-function copy of the context with every per-lane field made opaque and
-   the LDS base re-derived: values derived from the context (LDS addresses of
-   parents/children/ancestors, depth masks) are then computed inside each
-   phase instead of being hoisted to the kernel prologue and held in
-   registers for the whole launch. */
-__device__ __forceinline__ Ctx fresh_ctx(const Ctx& c0) {
-  Ctx c = c0;
-  int team = (int)(threadIdx.x >> 5);
-  asm volatile("" : "+v"(team), "+v"(c.l), "+v"(c.bpar), "+v"(c.bdep), "+v"(c.bjt), "+v"(c.bdofadr),
-               "+v"(c.blast), "+v"(c.nch), "+v"(c.ch0), "+v"(c.ch1), "+v"(c.ddep), "+v"(c.dbody));
-  asm volatile("" : "+v"(c.qadr), "+v"(c.act), "+v"(c.anc0), "+v"(c.anc1), "+v"(c.anc2), "+v"(c.desc),
-               "+v"(c.rowmask), "+v"(c.dk0), "+v"(c.mylevel), "+v"(c.dfree), "+v"(c.env));
-  c.L = &g_lds[team];
-  return c;
-}
 
 __device__ __forceinline__ int ancof(const Ctx& c, int e) {
   uint32_t w = e < 4 ? c.anc0 : (e < 8 ? c.anc1 : c.anc2);
@@ -401,8 +389,7 @@ __device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
 }
 
 /* ------------------------------- kinematics -------------------------------- */
-__device__ __forceinline__ void kinematics(const Ctx& c_, const EnvS& s, const LaneS& ls, BodyK& B) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B) {
   MP m = c.m;
   /* relative hinge angle of this body's joint, from its dof lane */
   float qrel_dof = ls.q - c.L->par[P_Q0][c.l];
@@ -461,8 +448,7 @@ __device__ __forceinline__ void kinematics(const Ctx& c_, const EnvS& s, const L
 /* subtree sum of K-vectors over the body tree: out (lane b) = sum over subtree(b).
  * Uses c.L->sub as the exchange buffer; result also left in sub[b]. */
 template <int K>
-__device__ __forceinline__ void subtree_sum(const Ctx& c_, float v[K]) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
   EnvL* L = c.L;
   for (int d = c.maxbd; d >= 1; d--) {
     int nmax = (int)((c.lvlch >> (4 * d)) & 0xfull);
@@ -483,8 +469,7 @@ __device__ __forceinline__ void subtree_sum(const Ctx& c_, float v[K]) {
 
 /* ------------------------------ mass matrix -------------------------------- */
 /* com, cinert (lane b), cdof (lane j -> LDS), crb, M rows (LDS + return) */
-__device__ __forceinline__ void com_crb_m(const Ctx& c_, const EnvS& s, const LaneS& ls, BodyK& B, float cm[3]) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B, float cm[3]) {
   const int ddep = vopq(c.ddep);
   MP m = c.m;
   EnvL* L = c.L;
@@ -620,11 +605,11 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c_, const EnvS& s, const La
  * updates of its level-lv descendants, two rows per pass with every load
  * issued up front (padded slots read the all-zero row ZROW). On return the L
  * rows are in LDS L[][] (L(k, anc_e(k))), pivots in Dk[]; returns 1/D_j. */
-__device__ __forceinline__ float factor_ldl(const Ctx& c_, float X[CAP], float Xd) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
-  const int nlevel = c.m->nlevel;
+  const int nroot = c.nroot;
+  const int nlevel = c.m->nlevel - nroot; /* branch levels; the root chain is one dense block */
   for (int lv = 0; lv < nlevel; lv++) {
     if (c.mylevel == lv) {
       float Dkv = fmaxf(Xd, MINVAL);
@@ -656,13 +641,55 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c_, float X[CAP], float X
       }
     }
   }
+  if (nroot > 0) {
+    /* root chain (dofs 0..nroot-1, dense after the branch updates): every lane
+       eliminates the same block in registers, k = nroot-1 .. 0, with the
+       per-entry arithmetic of the level path */
+    if (c.l < nroot) {
+      st_row(&L->L[c.l][0], X);
+      L->Dk[c.l] = Xd;
+    }
+    tsync();
+    float A[RMAX][RMAX], D[RMAX];
+#pragma unroll
+    for (int i = 0; i < RMAX; i++) {
+      D[i] = i < nroot ? L->Dk[i] : 1.f;
+#pragma unroll
+      for (int j = 0; j < RMAX; j++) A[i][j] = (j < i && i < nroot) ? L->L[i][j] : 0.f;
+    }
+    tsync();
+#pragma unroll
+    for (int k = RMAX - 1; k >= 0; k--) {
+      if (k < nroot) {
+        const float Dkv = fmaxf(D[k], MINVAL);
+        const float inv = 1.0f / Dkv;
+        D[k] = Dkv;
+#pragma unroll
+        for (int i = 0; i < k; i++) A[k][i] = A[k][i] * inv;
+#pragma unroll
+        for (int i = 0; i < k; i++) {
+          const float t = A[k][i] * Dkv;
+          D[i] -= t * A[k][i];
+#pragma unroll
+          for (int e = 0; e < i; e++) A[i][e] -= t * A[k][e];
+        }
+        if (c.l == 0) {
+#pragma unroll
+          for (int i = 0; i < k; i++) L->L[k][i] = A[k][i];
+          L->Dk[k] = Dkv;
+          L->Di[k] = inv;
+        }
+      }
+    }
+    tsync();
+    if (c.l < nroot) return L->Di[c.l];
+  }
   tsync();
   return 1.0f / fmaxf(Xd, MINVAL);
 }
 
 /* load a depth-indexed M row into off-diagonal X[] (masked) and diagonal */
-__device__ __forceinline__ float load_mrow(const Ctx& c_, float X[CAP]) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
   const int ddep = vopq(c.ddep);
   const int j = c.l & 31;
   ld_row(&c.L->M[j][0], X);
@@ -675,11 +702,11 @@ __device__ __forceinline__ float load_mrow(const Ctx& c_, float X[CAP]) {
  * value is final once its level is reached; descendants' contributions come
  * through LDS two at a time), then the diagonal, then the root-to-leaf pass
  * over ancestors by depth. */
-__device__ __forceinline__ float solve_ldl(const Ctx& c_, float x, float Dinv) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
-  const int nlevel = c.m->nlevel;
+  const int nroot = c.nroot;
+  const int nlevel = c.m->nlevel - nroot;
   for (int lv = 0; lv < nlevel; lv++) {
     if (c.mylevel == lv) L->vec[V_SOLVE][c.l] = x;
     tsync();
@@ -696,8 +723,44 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c_, float x, float Dinv) {
       x -= h1 ? a1 : 0.f;
     }
   }
+  /* root chain, dense and redundant in every lane: the rest of the forward
+     pass, the diagonal, and the root-to-leaf pass inside the chain */
+  float xr[RMAX];
+#pragma unroll
+  for (int k = 0; k < RMAX; k++) xr[k] = 0.f;
+  if (nroot > 0) {
+    if (c.l < nroot) L->vec[V_SOLVE][c.l] = x;
+    tsync();
+#pragma unroll
+    for (int k = 0; k < RMAX; k++) xr[k] = k < nroot ? L->vec[V_SOLVE][k] : 0.f;
+    tsync();
+#pragma unroll
+    for (int k = RMAX - 1; k >= 1; k--)
+      if (k < nroot)
+#pragma unroll
+        for (int i = 0; i < k; i++) xr[i] -= L->L[k][i] * xr[k];
+#pragma unroll
+    for (int k = 0; k < RMAX; k++)
+      if (k < nroot) xr[k] *= L->Di[k];
+#pragma unroll
+    for (int k = 1; k < RMAX; k++)
+      if (k < nroot)
+#pragma unroll
+        for (int a = 0; a < k; a++) xr[k] -= L->L[k][a] * xr[a];
+  }
   x *= Dinv;
-  for (int e = 0; e < c.maxdd - 1; e++) {
+  int e0 = 0;
+  if (nroot > 0) {
+    /* branch dofs: ancestors 0..nroot-1 are the chain */
+#pragma unroll
+    for (int e = 0; e < RMAX; e++)
+      if (e < nroot && e < ddep) x -= L->L[c.l][e] * xr[e];
+#pragma unroll
+    for (int k = 0; k < RMAX; k++)
+      if (c.l == k && k < nroot) x = xr[k];
+    e0 = nroot;
+  }
+  for (int e = e0; e < c.maxdd - 1; e++) {
     int a = e <= ddep ? ancof(c, e) : 0;
     float xa = tsh(x, a);
     if (e < ddep) x -= L->L[c.l][e] * xa;
@@ -706,8 +769,7 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c_, float x, float Dinv) {
 }
 
 /* y = M x (M rows in LDS), x in dof lanes; uses vec[slot] */
-__device__ __forceinline__ float mul_m(const Ctx& c_, float x, int slot) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int j = c.l;
@@ -718,11 +780,23 @@ __device__ __forceinline__ float mul_m(const Ctx& c_, float x, int slot) {
 #pragma unroll
     for (int e = 0; e < CAP; e++)
       if (e <= ddep) y += L->M[j][e] * L->vec[slot][ancof(c, e)];
+    /* transposed part M(k, j) x_k over descendants k, four per pass with
+       all loads issued up front (padded slots repeat k0 and add 0) */
     uint32_t dm = c.desc;
     while (dm) {
-      int k = __ffs(dm) - 1;
-      dm &= dm - 1;
-      y += L->M[k][ddep] * L->vec[slot][k];
+      int k[4];
+      bool h[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        h[i] = dm != 0u;
+        k[i] = h[i] ? __ffs(dm) - 1 : k[0];
+        dm &= dm - 1u;
+      }
+      float a[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) a[i] = L->M[k[i]][ddep] * L->vec[slot][k[i]];
+#pragma unroll
+      for (int i = 0; i < 4; i++) y += h[i] ? a[i] : 0.f;
     }
   }
   tsync();
@@ -730,8 +804,7 @@ __device__ __forceinline__ float mul_m(const Ctx& c_, float x, int slot) {
 }
 
 /* chain gather: sum_e Jc[e] * vec[slot][anc_e] for a contact row */
-__device__ __forceinline__ float row_dot(const Ctx& c_, const Rows& r, int slot) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) {
   const int kdep = vopq(r.kdep);
   float v = 0.f;
 #pragma unroll
@@ -742,8 +815,7 @@ __device__ __forceinline__ float row_dot(const Ctx& c_, const Rows& r, int slot)
 
 /* ----------------------------------- RNE ----------------------------------- */
 /* cvel (lane b), cdofdot (LDS). Requires vec[V_QVEL]. */
-__device__ __forceinline__ void com_vel(const Ctx& c_, BodyK& B) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
   const int ddep = vopq(c.ddep);
   MP m = c.m;
   EnvL* L = c.L;
@@ -791,8 +863,7 @@ __device__ __forceinline__ void com_vel(const Ctx& c_, BodyK& B) {
 }
 
 /* cacc per body (lane b) with or without qacc (vec[V_QACC]) */
-__device__ __forceinline__ void com_acc(const Ctx& c_, float ca[6], bool with_acc) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc) {
   const int ddep = vopq(c.ddep);
   MP m = c.m;
   EnvL* L = c.L;
@@ -827,8 +898,7 @@ __device__ __forceinline__ void com_acc(const Ctx& c_, float ca[6], bool with_ac
 }
 
 /* body force cfrc (lane b) -> subtree sums in sub[] ; returns dof projection cdof_j . sub[body(j)] */
-__device__ __forceinline__ float rne_project(const Ctx& c_, const BodyK& B, const float ca[6], const float fext[6]) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const float ca[6], const float fext[6]) {
   EnvL* L = c.L;
   float f[6];
   if (c.l >= 1 && c.l < c.nb) {
@@ -892,9 +962,8 @@ __device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, floa
  * n +- mu t (frame of mju_makeFrame(+z): t1 = +y, t2 = -x) and the friction
  * coefficient; returns the signed distance (> margin: no contact). Recomputed
  * by the sensors instead of being held in registers through the solver. */
-__device__ __forceinline__ float contact_point(const Ctx& c_, const EnvS& s, const BodyK& B, float pos[3], float dir[3],
+__device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, const BodyK& B, float pos[3], float dir[3],
                                                float& mu) {
-  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   const int l = c.l;
   const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
@@ -927,9 +996,8 @@ __device__ __forceinline__ float contact_point(const Ctx& c_, const EnvS& s, con
 }
 
 /* collision + contact rows (lane r) + dof rows (lane j) */
-__device__ __forceinline__ void make_constraints(const Ctx& c_, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
+__device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
                                  Rows& r) {
-  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   CP cfg = c.cfg;
   EnvL* L = c.L;
@@ -1030,8 +1098,7 @@ __device__ __forceinline__ float eval_one(float jar, float D, float& force, int&
 }
 
 /* row costs at given jar values (no state change) */
-__device__ __forceinline__ float rows_cost(const Ctx& c_, const Rows& r, float jc, float jf_, float jlo_, float jhi_) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jlo_, float jhi_) {
   float cost = 0.f, f;
   int a;
   if (r.ex) cost += eval_one(jc, r.D, f, a);
@@ -1042,8 +1109,7 @@ __device__ __forceinline__ float rows_cost(const Ctx& c_, const Rows& r, float j
 }
 
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
-__device__ __forceinline__ float update_constraint(const Ctx& c_, Rows& r, float qacc, float qs, float fs, float Ma, float& grad) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float qacc, float qs, float fs, float Ma, float& grad) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float cost = 0.f;
@@ -1059,11 +1125,21 @@ __device__ __forceinline__ float update_constraint(const Ctx& c_, Rows& r, float
   tsync();
   float qc = 0.f;
   if (c.l < c.nv) {
-    uint32_t tb = r.exmask;
+    uint32_t tb = r.exmask & c.rowmask;
     while (tb) {
-      int row = __ffs(tb) - 1;
-      tb &= tb - 1u;
-      if ((c.rowmask >> row) & 1u) qc += L->u.J[row][ddep] * L->rowF[row];
+      int k[4];
+      bool h[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        h[i] = tb != 0u;
+        k[i] = h[i] ? __ffs(tb) - 1 : k[0];
+        tb &= tb - 1u;
+      }
+      float a[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) a[i] = L->u.J[k[i]][ddep] * L->rowF[k[i]];
+#pragma unroll
+      for (int i = 0; i < 4; i++) qc += h[i] ? a[i] : 0.f;
     }
     if (r.hf) qc += r.ff;
     if (r.hlo) qc += r.flo;
@@ -1074,8 +1150,7 @@ __device__ __forceinline__ float update_constraint(const Ctx& c_, Rows& r, float
 }
 
 /* H = M + J' D_active J rows (depth-indexed), then factor -> Dinv */
-__device__ __forceinline__ float hessian_factor(const Ctx& c_, const Rows& r) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float H[CAP];
@@ -1083,16 +1158,24 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c_, const Rows& r) {
   if (c.l < c.nv) {
     uint32_t tb = r.exmask & c.rowmask;
     while (tb) {
-      int row = __ffs(tb) - 1;
+      const int k0 = __ffs(tb) - 1;
       tb &= tb - 1u;
-      float da = L->rowDA[row];
-      float jd = L->u.J[row][ddep];
-      float jr[CAP];
-      ld_row(&L->u.J[row][0], jr);
-      float jj = da * jd;
-      Hd += jj * jd;
+      const bool h1 = tb != 0u;
+      const int k1 = h1 ? __ffs(tb) - 1 : k0;
+      tb &= tb - 1u;
+      float j0[CAP], j1[CAP];
+      ld_row(&L->u.J[k0][0], j0);
+      ld_row(&L->u.J[k1][0], j1);
+      const float jd0 = L->u.J[k0][ddep], jd1 = L->u.J[k1][ddep];
+      const float jj0 = L->rowDA[k0] * jd0;
+      const float jj1 = h1 ? L->rowDA[k1] * jd1 : 0.f;
+      Hd += jj0 * jd0;
+      Hd += jj1 * jd1;
 #pragma unroll
-      for (int e = 0; e < CAP; e++) H[e] += (e < ddep ? jj : 0.f) * jr[e];
+      for (int e = 0; e < CAP; e++) {
+        H[e] += (e < ddep ? jj0 : 0.f) * j0[e];
+        H[e] += (e < ddep ? jj1 : 0.f) * j1[e];
+      }
     }
     float dd = 0.f;
     if (r.hf && r.actf) dd += r.Df;
@@ -1105,8 +1188,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c_, const Rows& r) {
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
-__device__ __forceinline__ float line_search(const Ctx& c_, Rows& r, float search, float Ma, float fs, float& Mv) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float& Mv) {
   CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
@@ -1158,8 +1240,7 @@ __device__ __forceinline__ float line_search(const Ctx& c_, Rows& r, float searc
 }
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
-__device__ __forceinline__ float solve_newton(const Ctx& c_, Rows& r, float qs, float fs, float w, int& iters) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters) {
   CP cfg = c.cfg;
   MP m = c.m;
   EnvL* L = c.L;
@@ -1229,8 +1310,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c_, Rows& r, float qs, 
 
 /* ----------------------------- Feetech actuator ---------------------------- */
 /* trapezoidal_step (train.py:1137-1196) + duty/torque (train.py:1260-1269) */
-__device__ __forceinline__ void feetech(const Ctx& c_, LaneS& ls) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
   MP m = c.m;
   if (c.act < 0) { ls.ctrl = 0.f; return; }
   const int a = c.act;
@@ -1264,9 +1344,8 @@ __device__ __forceinline__ void feetech(const Ctx& c_, LaneS& ls) {
 
 /* ------------------------------- full forward ------------------------------ */
 /* mj_forward (+ sensors if requested). Leaves qacc in ls.qacc, kinematics in B. */
-__device__ __forceinline__ void forward(const Ctx& c_, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
+__device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
                                         Sensors& sen, int& iters) {
-  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   EnvL* L = c.L;
   STAMP(S_ENTRY);
@@ -1401,8 +1480,7 @@ __device__ __forceinline__ void forward(const Ctx& c_, const EnvS& s, LaneS& ls,
 }
 
 /* ------------------------------ Euler integrate ----------------------------- */
-__device__ __forceinline__ void integrate(const Ctx& c_, EnvS& s, LaneS& ls) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls) {
   const float dt = c.cfg->dt;
   float vn = ls.v + dt * ls.qacc;
   float v0 = tsh(vn, 0), v1 = tsh(vn, 1), v2 = tsh(vn, 2), w0 = tsh(vn, 3), w1 = tsh(vn, 4), w2 = tsh(vn, 5);
@@ -1428,8 +1506,7 @@ __device__ __forceinline__ void integrate(const Ctx& c_, EnvS& s, LaneS& ls) {
 }
 
 /* --------------------------- env-level (ksim) logic ------------------------- */
-__device__ __forceinline__ void load_params(const Ctx& c_, EnvS& s, LaneS& ls, const float* rnd) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, const float* rnd) {
   MP m = c.m;
   const bool rz = (c.cfg->flags & ZB_F_RANDOMIZE) && rnd;
   const int l = c.l;
@@ -1461,8 +1538,7 @@ __device__ __forceinline__ void load_params(const Ctx& c_, EnvS& s, LaneS& ls, c
 }
 
 /* randomizer sampling (must match oracle/zb_oracle.c sample_rand) */
-__device__ __forceinline__ void sample_rand(const Ctx& c_, uint32_t episode, float* rnd) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void sample_rand(const Ctx& c, uint32_t episode, float* rnd) {
   CP cfg = c.cfg;
   const int l = c.l;
   for (int k = l; k < 75; k += TEAM) {
@@ -1513,9 +1589,8 @@ __device__ __forceinline__ void rotate_quat_by_quat(const float q_[4], const flo
 }
 
 /* observation assembly + obs-derived carries (train.py:1478-1537, 1624-1679) */
-__device__ __forceinline__ void observe(const Ctx& c_, EnvS& s, const LaneS& ls, const BodyK& B, const Sensors& sen, float* oa,
+__device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, const Sensors& sen, float* oa,
                         float* oc, float* ox) {
-  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   CP cfg = c.cfg;
   const int l = c.l;
@@ -1628,9 +1703,8 @@ __device__ __forceinline__ void quat_roll_pitch(const float q_[4], float& roll, 
 }
 
 /* terminations + reward terms (train.py:1546-1593) ; returns done */
-__device__ __forceinline__ bool rewards(const Ctx& c_, EnvS& s, const LaneS& ls, const BodyK& B, float cur, float* terms_out,
+__device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, float cur, float* terms_out,
                         float& total, bool& fail) {
-  const Ctx c = fresh_ctx(c_);
   MP m = c.m;
   CP cfg = c.cfg;
   const int l = c.l;
@@ -1718,8 +1792,7 @@ __device__ __forceinline__ bool rewards(const Ctx& c_, EnvS& s, const LaneS& ls,
 }
 
 /* ------------------------------ state I/O ---------------------------------- */
-__device__ __forceinline__ void load_state(const Ctx& c_, EnvS& s, LaneS& ls, const float* st) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, const float* st) {
   const int l = c.l;
   for (int k = 0; k < 3; k++) s.bp[k] = st[ZB_S_QPOS + k];
   for (int k = 0; k < 4; k++) s.bq[k] = st[ZB_S_QPOS + 3 + k];
@@ -1752,8 +1825,7 @@ __device__ __forceinline__ void load_state(const Ctx& c_, EnvS& s, LaneS& ls, co
   ls.actforce = 0.f;
 }
 
-__device__ __forceinline__ void store_state(const Ctx& c_, const EnvS& s, const LaneS& ls, float* st) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const LaneS& ls, float* st) {
   const int l = c.l;
   if (l < c.nv) {
     st[ZB_S_QVEL + l] = ls.v;
@@ -1784,8 +1856,7 @@ __device__ __forceinline__ void store_state(const Ctx& c_, const EnvS& s, const 
 }
 
 /* ksim reset (train.py:1471-1476); the caller then runs mjx.forward (forward()) */
-__device__ __forceinline__ void reset_prepare(const Ctx& c_, EnvS& s, LaneS& ls, float* rnd) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, float* rnd) {
   MP m = c.m;
   CP cfg = c.cfg;
   const int l = c.l;
@@ -1827,8 +1898,7 @@ __device__ __forceinline__ void reset_prepare(const Ctx& c_, EnvS& s, LaneS& ls,
 }
 
 /* push event (train.py:1459-1468) */
-__device__ __forceinline__ void push_event(const Ctx& c_, EnvS& s, LaneS& ls, float cur) {
-  const Ctx c = fresh_ctx(c_);
+__device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, float cur) {
   CP cfg = c.cfg;
   float timer = s.push_timer - cfg->ctrl_dt;
   if (timer <= 0.f) {
@@ -1922,6 +1992,15 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
     for (int mi = 0; mi < m->level_nmem[lv]; mi++)
       if (isd && m->level_mem[lv][mi] == l) c.mylevel = lv;
   c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
+  {
+    int nr = 0;
+    for (int k = 0; k < RMAX && k < m->nlevel; k++) {
+      const int lv = m->nlevel - 1 - k;
+      if (m->level_nmem[lv] == 1 && m->level_mem[lv][0] == k && m->dof_depth[k] == k) nr++;
+      else break;
+    }
+    c.nroot = nr;
+  }
   if (l == ZROW) {
     float z[CAP];
 #pragma unroll
