@@ -31,7 +31,7 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(cm, cfg, budget_s: float, n_envs: int = 256) -> dict:
+def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int = 256) -> dict:
     """Time the CPU oracle (fp32 C, OpenMP over envs) on a bounded sample."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     os.environ["OMP_NUM_THREADS"] = str(threads)
@@ -55,7 +55,7 @@ def cpu_baseline(cm, cfg, budget_s: float, n_envs: int = 256) -> dict:
         "unit": "env-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n_envs} envs x {steps} env-steps of the same C2 workload on the oracle "
+        "sample": f"{n_envs} envs x {steps} env-steps of the same workload ({workload}) on the oracle "
                   f"(fp32 C restatement, OpenMP {threads} threads), {el:.1f} s",
     }
 
@@ -78,7 +78,7 @@ def main() -> None:
     from zbot_amd import cstructs as cs  # noqa: PLC0415
     from zbot_amd.constants import JOINT_BIASES  # noqa: PLC0415
     from zbot_amd.engine import HipEngine  # noqa: PLC0415
-    from zbot_amd.metrics import HBM_PEAK_GBS, bytes_per_env_step  # noqa: PLC0415
+    from zbot_amd.metrics import FP32_PEAK_TFLOPS, HBM_PEAK_GBS, bytes_per_env_step  # noqa: PLC0415
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -142,13 +142,17 @@ def main() -> None:
     achieved = bpe * n / (avg_ms * 1e-3) / 1e9
     iters = eng.solver_iters().float().mean().item()
 
+    # HBM bytes per launch and issued fp32 FLOP per env-step from the separate
+    # rocprofv3 PMC passes of the same kernel (scripts/pmc_traffic.sh)
     traffic = None
+    flop_per_env_step = None
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.config}.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
         if tj.get("envs") == n:
             traffic = tj.get("hbm_bytes_per_launch")
+            flop_per_env_step = tj.get("issued_fp32_flop_per_env_step")
 
     if rank == 0:
         value = world * n * args.steps / elapsed
@@ -186,13 +190,22 @@ def main() -> None:
                 "algorithmic_bytes_per_env_step": bpe,
                 "note": "the path is FP32-VALU/latency bound (DESIGN.md §Roofline); HBM fraction reported as required",
             },
+            "roofline_fp32": None if flop_per_env_step is None else {
+                "bound": "fp32-valu",
+                "achieved": flop_per_env_step * n / (avg_ms * 1e-3) / 1e12,
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": flop_per_env_step * n / (avg_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                "note": "issued VALU lane-FLOP (PMC SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32, FMA=2) per env-step "
+                        "x envs / kernel time; the binding resource of this latency/VALU-bound kernel",
+            },
             "episode_stats": {
                 "episodes_done": float(total_stats[2].item()),
                 "mean_return": float((total_stats[0] / total_stats[2].clamp(min=1)).item()),
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec)
+            out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper())
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
