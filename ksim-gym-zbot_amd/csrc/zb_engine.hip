@@ -152,7 +152,7 @@ __device__ __forceinline__ void zb_stamp(EnvL* L, int i) {
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
   __builtin_amdgcn_sched_barrier(0);
   if ((threadIdx.x & (TEAM - 1)) == 0) {
-    L->stamp[i] += t - L->stamp_last;
+    L->stamp[i] += (t - L->stamp_last) + (1ull << 44); /* cycles (low 44 bits) + call count */
     L->stamp_last = t;
   }
 }
@@ -389,60 +389,76 @@ __device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
 }
 
 /* ------------------------------- kinematics -------------------------------- */
+/* mj_kinematics by pointer jumping: each body lane first builds its frame
+ * relative to its parent (for a hinge: rotate about the anchor, the local form
+ * of MuJoCo's anchor -> rotate -> un-anchor update), then composes with the
+ * frame of the ancestor its transform is currently relative to, doubling the
+ * covered depth each round: ceil(log2(depth)) rounds instead of one pass per
+ * tree level. The floating base is absolute from the start. */
 __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B) {
   MP m = c.m;
+  const int b = c.l;
+  const bool isb = b >= 1 && b < c.nb;
   /* relative hinge angle of this body's joint, from its dof lane */
   float qrel_dof = ls.q - c.L->par[P_Q0][c.l];
   float ang = tsh(qrel_dof, c.bdofadr < 0 ? 0 : c.bdofadr);
-  B.xp[0] = B.xp[1] = B.xp[2] = 0.f;
-  B.xq[0] = 1.f; B.xq[1] = B.xq[2] = B.xq[3] = 0.f;
-  int par = c.bpar < 0 ? 0 : c.bpar;
-  for (int d = 1; d <= c.maxbd; d++) {
-    float pxp[3], pxq[4];
+  float p[3] = {0.f, 0.f, 0.f}, q[4] = {1.f, 0.f, 0.f, 0.f};
+  int anc = 0; /* frame the transform is relative to (0: world) */
+  if (isb) {
+    if (c.bjt == ZB_JNT_FREE) {
 #pragma unroll
-    for (int k = 0; k < 3; k++) pxp[k] = tsh(B.xp[k], par);
+      for (int k = 0; k < 3; k++) p[k] = s.bp[k];
 #pragma unroll
-    for (int k = 0; k < 4; k++) pxq[k] = tsh(B.xq[k], par);
-    if (c.bdep == d) {
-      const int b = c.l;
-      if (c.bjt == ZB_JNT_FREE) {
+      for (int k = 0; k < 4; k++) q[k] = s.bq[k];
+      quat_normalize(q);
+    } else {
 #pragma unroll
-        for (int k = 0; k < 3; k++) B.xp[k] = s.bp[k];
+      for (int k = 0; k < 3; k++) p[k] = m->body_pos[b][k];
 #pragma unroll
-        for (int k = 0; k < 4; k++) B.xq[k] = s.bq[k];
-        quat_normalize(B.xq);
-      } else {
-        float pR[9], t[3];
-        quat2mat(pR, pxq);
-        float bpos[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]};
-        float bqt[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]};
-        mulmv3(t, pR, bpos);
-        float xp[3] = {pxp[0] + t[0], pxp[1] + t[1], pxp[2] + t[2]}, xq[4];
-        quat_mul(xq, pxq, bqt);
-        if (c.bjt == ZB_JNT_HINGE) {
-          float R[9], jp[3] = {m->jnt_pos[b][0], m->jnt_pos[b][1], m->jnt_pos[b][2]};
-          float ax[3] = {m->jnt_axis[b][0], m->jnt_axis[b][1], m->jnt_axis[b][2]};
-          quat2mat(R, xq);
-          mulmv3(t, R, jp);
-          float anchor[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
-          float ql[4], qn[4];
-          axis_angle_quat(ql, ax, ang);
-          quat_mul(qn, xq, ql);
-          quat_normalize(qn);
-          quat2mat(R, qn);
-          mulmv3(t, R, jp);
+      for (int k = 0; k < 4; k++) q[k] = m->body_quat[b][k];
+      if (c.bjt == ZB_JNT_HINGE) {
+        float jp[3] = {m->jnt_pos[b][0], m->jnt_pos[b][1], m->jnt_pos[b][2]};
+        float ax[3] = {m->jnt_axis[b][0], m->jnt_axis[b][1], m->jnt_axis[b][2]};
+        float R[9], t1[3], t2[3], ql[4], qn[4];
+        quat2mat(R, q);
+        mulmv3(t1, R, jp);
+        axis_angle_quat(ql, ax, ang);
+        quat_mul(qn, q, ql);
+        quat_normalize(qn);
+        quat2mat(R, qn);
+        mulmv3(t2, R, jp);
 #pragma unroll
-          for (int k = 0; k < 3; k++) xp[k] = anchor[k] - t[k];
+        for (int k = 0; k < 3; k++) p[k] += t1[k] - t2[k];
 #pragma unroll
-          for (int k = 0; k < 4; k++) xq[k] = qn[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 3; k++) B.xp[k] = xp[k];
-#pragma unroll
-        for (int k = 0; k < 4; k++) B.xq[k] = xq[k];
+        for (int k = 0; k < 4; k++) q[k] = qn[k];
       }
+      anc = c.bpar;
     }
   }
+  for (int span = 1; span < c.maxbd; span <<= 1) {
+    float ap[3], aq[4];
+#pragma unroll
+    for (int k = 0; k < 3; k++) ap[k] = tsh(p[k], anc);
+#pragma unroll
+    for (int k = 0; k < 4; k++) aq[k] = tsh(q[k], anc);
+    const int aa = tshi(anc, anc);
+    if (anc != 0) {
+      float R[9], t[3], qq[4];
+      quat2mat(R, aq);
+      mulmv3(t, R, p);
+#pragma unroll
+      for (int k = 0; k < 3; k++) p[k] = ap[k] + t[k];
+      quat_mul(qq, aq, q);
+#pragma unroll
+      for (int k = 0; k < 4; k++) q[k] = qq[k];
+      anc = aa;
+    }
+  }
+  if (isb && c.bjt != ZB_JNT_FREE) quat_normalize(q);
+#pragma unroll
+  for (int k = 0; k < 3; k++) B.xp[k] = p[k];
+#pragma unroll
+  for (int k = 0; k < 4; k++) B.xq[k] = q[k];
 }
 
 /* subtree sum of K-vectors over the body tree: out (lane b) = sum over subtree(b).

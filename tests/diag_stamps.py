@@ -39,15 +39,20 @@ def main():
     eng.reset()
     bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
     tot = torch.zeros(NS, dtype=torch.float64)
+    calls = torch.zeros(NS, dtype=torch.float64)
     for t in range(args.steps):
         eng.step(bias + 0.05 * torch.randn(args.n, 20, device="cuda"))
         buf = torch.zeros(args.n, NS, dtype=torch.int64, device="cuda")
         eng.L.zb_get_stamps(eng.h, buf.data_ptr(), eng._stream())
         torch.cuda.synchronize()
-        tot += buf.double().sum(0).cpu()
+        b = buf.cpu()
+        tot += (b & ((1 << 44) - 1)).double().sum(0)
+        calls += (b >> 44).double().sum(0)
     share = tot / tot.sum()
     res = {PHASES[i]: round(float(share[i]) * 100, 2) for i in range(NS)}
     res["cycles_per_env_step"] = float(tot.sum() / (args.n * args.steps))
+    res["calls_per_env_step"] = {PHASES[i]: round(float(calls[i]) / (args.n * args.steps), 2) for i in range(NS)}
+    res["cycles_per_call"] = {PHASES[i]: round(float(tot[i] / max(calls[i], 1)), 0) for i in range(NS)}
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:
