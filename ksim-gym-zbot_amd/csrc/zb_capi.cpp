@@ -134,6 +134,8 @@ static int check_model(const ZbModel* m) {
     for (int c = 1; c < m->nbody; c++)
       if (m->body_parent[c] == b) nch++;
     if (nch > 8) return fail(ZB_EMODEL, "body %d has %d children (max 8)", b, nch);
+    /* subtree sums are chain suffix sums below the base (zb_engine.hip subtree_sum) */
+    if (b != 1 && nch > 1) return fail(ZB_EMODEL, "body %d branches (%d children): only the base may", b, nch);
   }
   if (maxbd > 15) return fail(ZB_EMODEL, "body depth %d > 15", maxbd);
   return ZB_OK;

@@ -463,24 +463,43 @@ __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const La
 
 /* subtree sum of K-vectors over the body tree: out (lane b) = sum over subtree(b).
  * Uses c.L->sub as the exchange buffer; result also left in sub[b]. */
+/* subtree sums of K-vectors over the body tree: out (lane b) = sum over
+ * subtree(b), left in registers and in LDS sub[b]. The model has a single
+ * branching body (the floating base, body 1; checked by zb_create), so below
+ * it every subtree is a chain suffix: pointer jumping along the child links
+ * sums the chains in log2(length) rounds, then the base gathers its children. */
 template <int K>
 __device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
   EnvL* L = c.L;
-  for (int d = c.maxbd; d >= 1; d--) {
-    int nmax = (int)((c.lvlch >> (4 * d)) & 0xfull);
-    if (c.bdep == d) {
-      for (int k = 0; k < nmax; k++) {
-        if (k < c.nch) {
-          int ch = childof(c, k);
+  const bool chain = c.l >= 2 && c.l < c.nb && c.nch == 1;
+  int nxt = chain ? childof(c, 0) : c.l;
+  bool live = chain;
+  for (int span = 1; span < c.maxbd - 1; span <<= 1) {
+    float w[K];
 #pragma unroll
-          for (int i = 0; i < K; i++) v[i] += L->sub[ch][i];
-        }
-      }
+    for (int i = 0; i < K; i++) w[i] = tsh(v[i], nxt);
+    const int nn = tshi(nxt, nxt);
+    const bool nl = tshi(live ? 1 : 0, nxt) != 0;
+    if (live) {
 #pragma unroll
-      for (int i = 0; i < K; i++) L->sub[c.l][i] = v[i];
+      for (int i = 0; i < K; i++) v[i] += w[i];
+      nxt = nn;
+      live = nl;
     }
-    tsync();
   }
+#pragma unroll
+  for (int i = 0; i < K; i++) L->sub[c.l][i] = v[i];
+  tsync();
+  if (c.l == 1) {
+    for (int k = 0; k < c.nch; k++) {
+      const int ch = childof(c, k);
+#pragma unroll
+      for (int i = 0; i < K; i++) v[i] += L->sub[ch][i];
+    }
+#pragma unroll
+    for (int i = 0; i < K; i++) L->sub[1][i] = v[i];
+  }
+  tsync();
 }
 
 /* ------------------------------ mass matrix -------------------------------- */
