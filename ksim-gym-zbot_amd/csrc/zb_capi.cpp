@@ -119,7 +119,7 @@ static int check_model(const ZbModel* m) {
   if (m->version != ZB_MODEL_VERSION) return fail(ZB_EARG, "model version %d != %d", m->version, ZB_MODEL_VERSION);
   if (m->struct_bytes != (int32_t)sizeof(ZbModel))
     return fail(ZB_EARG, "model struct_bytes %d != %zu (layout mismatch)", m->struct_bytes, sizeof(ZbModel));
-  if (m->nbody > 32 || m->nv > 31 || m->nq > ZB_MAX_QPOS) /* factor row 31 is the engine's zero row */
+  if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
   if (m->ngeom * ZB_CON_PER_GEOM * 4 > 32)
     return fail(ZB_EMODEL, "ngeom=%d: contact rows exceed the 32-lane team", m->ngeom);
@@ -138,6 +138,25 @@ static int check_model(const ZbModel* m) {
     if (b != 1 && nch > 1) return fail(ZB_EMODEL, "body %d branches (%d children): only the base may", b, nch);
   }
   if (maxbd > 15) return fail(ZB_EMODEL, "body depth %d > 15", maxbd);
+  /* dof tree shape the factorization relies on (zb_engine.hip factor_ldl):
+     a root chain 0..R-1 (R <= 6, one dof per top elimination level) and
+     unbranched limb chains of consecutive dofs hanging off dof R-1 */
+  int nroot = 0;
+  for (int k = 0; k < 6 && k < m->nlevel; k++) {
+    const int lv = m->nlevel - 1 - k;
+    if (m->level_nmem[lv] == 1 && m->level_mem[lv][0] == k && m->dof_depth[k] == k) nroot++;
+    else break;
+  }
+  if (nroot < 1) return fail(ZB_EMODEL, "dof tree has no root chain");
+  for (int k = nroot; k < m->nv; k++) {
+    const int p = m->dof_parent[k];
+    int nchild_prev = 0;
+    for (int j = nroot; j < m->nv; j++) nchild_prev += (m->dof_parent[j] == k - 1);
+    const bool head = p == nroot - 1;
+    const bool cont = p == k - 1 && k - 1 >= nroot && nchild_prev == 1;
+    if (!head && !cont)
+      return fail(ZB_EMODEL, "dof %d: limbs must be unbranched chains of consecutive dofs off dof %d", k, nroot - 1);
+  }
   return ZB_OK;
 }
 

@@ -42,7 +42,6 @@ constexpr float MAXIMP = 0.9999f;
 constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0); /* train.py:1113-1116 */
 
 enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3, V_SOLVE = 4, NVEC = 5 };
-constexpr int ZROW = 31; /* all-zero factor row: target of the padded update slots */
 constexpr int RMAX = 6;  /* longest root dof chain factored as one dense block (free joint) */
 enum { P_Q0 = 0, P_ARM = 1, P_DAMP = 2, P_FLOSS = 3, P_MSCALE = 4 };
 /* stamp slots: STAMP(i) closes phase i (time since the previous stamp) */
@@ -95,6 +94,13 @@ __shared__ EnvL g_lds[NTEAM];
 /* ----------------------------- team primitives ----------------------------- */
 __device__ __forceinline__ float tsh(float v, int src) { return __shfl(v, src, TEAM); }
 __device__ __forceinline__ int tshi(int v, int src) { return __shfl(v, src, TEAM); }
+/* value of v in lane k (team-relative, uniform k) of this lane's team: two
+   readlanes and a select, no LDS */
+__device__ __forceinline__ float team_lane(float v, int k) {
+  const int a = __builtin_amdgcn_readlane(__float_as_int(v), k);
+  const int b = __builtin_amdgcn_readlane(__float_as_int(v), k + TEAM);
+  return __int_as_float((threadIdx.x & TEAM) ? b : a);
+}
 /* DPP butterfly within 16-lane rows (quad xor 1, xor 2, half-row mirror, row
    mirror), then one cross-row exchange (xor 16). Every pairing is symmetric,
    so all lanes of a team end with the bit-identical result. */
@@ -137,10 +143,6 @@ __device__ __forceinline__ void tsync() { __syncthreads(); }
 __device__ __forceinline__ int vopq(int x) {
   asm volatile("" : "+v"(x));
   return x;
-}
-/* bitmask over the team's lanes of predicate p */
-__device__ __forceinline__ uint32_t team_ballot(bool p) {
-  return (uint32_t)(__ballot(p) >> (threadIdx.x & 32));
 }
 
 /* Diagnostic phase stamps (separate build, -DZB_STAMPS): cycles per phase of the
@@ -315,6 +317,9 @@ struct Ctx {
   int l;
   int nb, nv, nu, ngeom, maxbd, maxdd;
   int nroot; /* dofs 0..nroot-1: the unbranched chain at the top of the dof tree (one per top level) */
+  /* lane as a limb-chain dof (dofs >= nroot; each limb is an unbranched chain of
+     consecutive dofs hanging off dof nroot-1, checked by zb_create) */
+  int chd, cps, cln; /* chain head dof, position in the chain, chain length (chd = -1: not a chain dof) */
   /* lane as body */
   int bpar, bdep, bjt, bdofadr, blast, nch;
   uint32_t ch0, ch1;
@@ -325,7 +330,6 @@ struct Ctx {
   uint32_t desc; /* strict descendants of dof l */
   uint32_t rowmask; /* contact rows whose Jacobian chain contains dof l */
   int dk0;          /* index of dof l within its body's joint (free joint: 0..5) */
-  int mylevel;      /* elimination level of dof l */
   int dfree;        /* dof l belongs to a free joint */
 };
 
@@ -632,65 +636,71 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 }
 
 /* ---------------------- sparse L'DL factor + solves ------------------------ */
-/* Sparse L'DL of depth-indexed rows (mj_factorM), eliminated by LEVEL: the
- * level of a dof is its height in the dof tree (leaves 0), so the dofs of one
- * level are never ancestor/descendant of each other and are divided out
- * together. Lane j holds the off-diagonal entries X[e] = A(j, anc_e(j)),
- * e < depth(j), and the diagonal Xd; after level lv it applies the Schur
- * updates of its level-lv descendants, two rows per pass with every load
- * issued up front (padded slots read the all-zero row ZROW). On return the L
- * rows are in LDS L[][] (L(k, anc_e(k))), pivots in Dk[]; returns 1/D_j. */
+/* Sparse L'DL of depth-indexed rows (mj_factorM order: leaves first) for the
+ * dof tree the engine accepts (zb_create): a root chain 0..nroot-1 and
+ * unbranched limb chains hanging off dof nroot-1. Lane j holds the
+ * off-diagonal entries X[e] = A(j, anc_e(j)), e < depth(j), and the diagonal
+ * Xd. Limbs are eliminated level by level (height inside the chain) with the
+ * pivot rows pulled through ds_bpermute; their Schur complement on the root
+ * block is a set of team reductions; the root block is eliminated densely in
+ * registers. On return the L rows are in LDS L[][] (L(k, anc_e(k))), pivots in
+ * Dk[] (root: also 1/D in Di[]); returns 1/D_j. */
 __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int nroot = c.nroot;
-  const int nlevel = c.m->nlevel - nroot; /* branch levels; the root chain is one dense block */
-  for (int lv = 0; lv < nlevel; lv++) {
-    if (c.mylevel == lv) {
-      float Dkv = fmaxf(Xd, MINVAL);
-      float inv = 1.0f / Dkv;
+  const bool isroot = c.l < nroot;
+  const bool ischain = c.chd >= 0;
+  /* root rows are only touched by the dense block at the end: park them */
+  if (isroot) {
+    st_row(&L->L[c.l][0], X);
+    L->Dk[c.l] = Xd;
+  }
+  /* limb levels (height inside the chain, leaves first): the pivot of each
+     chain divides its row; every shallower lane of the chain pulls that row
+     with ds_bpermute (no LDS round trip) and applies its Schur update */
+  const int nlv = c.m->nlevel - nroot;
+  for (int lv = 0; lv < nlv; lv++) {
+    const int q = c.cln - 1 - lv; /* chain position of this level's pivot */
+    if (ischain && q == c.cps) {
+      const float Dkv = fmaxf(Xd, MINVAL);
+      const float inv = 1.0f / Dkv;
 #pragma unroll
       for (int e = 0; e < CAP; e++) X[e] = X[e] * inv;
-      st_row(&L->L[c.l][0], X);
-      L->Dk[c.l] = Dkv;
+      Xd = Dkv;
     }
-    tsync();
-    uint32_t dm = c.desc & team_ballot(c.mylevel == lv);
-    while (dm) {
-      const int k0 = __ffs(dm) - 1;
-      dm &= dm - 1u;
-      const int k1 = dm ? __ffs(dm) - 1 : ZROW;
-      dm &= dm - 1u;
-      float r0[CAP], r1[CAP];
-      ld_row(&L->L[k0][0], r0);
-      ld_row(&L->L[k1][0], r1);
-      const float d0 = L->Dk[k0], d1 = L->Dk[k1];
-      const float l0 = L->L[k0][ddep], l1 = L->L[k1][ddep]; /* L(k, j) */
-      const float t0 = l0 * d0, t1 = l1 * d1;                     /* A(k, j) after k's subtree */
-      Xd -= t0 * l0;
-      Xd -= t1 * l1;
+    const bool has = ischain && q > c.cps;
+    const int src = has ? c.chd + q : c.l;
+    float r[CAP];
 #pragma unroll
-      for (int e = 0; e < CAP; e++) {
-        X[e] -= (e < ddep ? t0 : 0.f) * r0[e];
-        X[e] -= (e < ddep ? t1 : 0.f) * r1[e];
-      }
+    for (int e = 0; e < CAP; e++) r[e] = tsh(X[e], src);
+    const float dk = tsh(Xd, src);
+    if (has) {
+      float lk = 0.f; /* L(k, j) = r[depth(j)] */
+#pragma unroll
+      for (int e = 0; e < CAP; e++) lk = e == ddep ? r[e] : lk;
+      const float t = lk * dk; /* A(k, j) after k's subtree */
+      Xd -= t * lk;
+#pragma unroll
+      for (int e = 0; e < CAP; e++) X[e] -= (e < ddep ? t : 0.f) * r[e];
     }
   }
+  if (ischain) {
+    st_row(&L->L[c.l][0], X);
+    L->Dk[c.l] = Xd;
+  }
   if (nroot > 0) {
-    /* root chain (dofs 0..nroot-1, dense after the branch updates): every lane
-       eliminates the same block in registers, k = nroot-1 .. 0, with the
-       per-entry arithmetic of the level path */
-    if (c.l < nroot) {
-      st_row(&L->L[c.l][0], X);
-      L->Dk[c.l] = Xd;
-    }
+    /* root block: parked rows minus the limbs' Schur complement
+       G[i][e] = sum_k D_k L(k,i) L(k,e) (team reductions), then the dense
+       elimination k = nroot-1 .. 0, redundantly in every lane */
     tsync();
     float A[RMAX][RMAX], D[RMAX];
 #pragma unroll
     for (int i = 0; i < RMAX; i++) {
-      D[i] = i < nroot ? L->Dk[i] : 1.f;
+      const float wi = ischain ? Xd * X[i] : 0.f;
+      D[i] = i < nroot ? L->Dk[i] - tsum(wi * X[i]) : 1.f;
 #pragma unroll
-      for (int j = 0; j < RMAX; j++) A[i][j] = (j < i && i < nroot) ? L->L[i][j] : 0.f;
+      for (int j = 0; j < RMAX; j++) A[i][j] = (j < i && i < nroot) ? L->L[i][j] - tsum(wi * X[j]) : 0.f;
     }
     tsync();
 #pragma unroll
@@ -717,7 +727,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
       }
     }
     tsync();
-    if (c.l < nroot) return L->Di[c.l];
+    if (isroot) return L->Di[c.l];
   }
   tsync();
   return 1.0f / fmaxf(Xd, MINVAL);
@@ -741,34 +751,28 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int nroot = c.nroot;
-  const int nlevel = c.m->nlevel - nroot;
-  for (int lv = 0; lv < nlevel; lv++) {
-    if (c.mylevel == lv) L->vec[V_SOLVE][c.l] = x;
-    tsync();
-    uint32_t dm = c.desc & team_ballot(c.mylevel == lv);
-    while (dm) {
-      const int k0 = __ffs(dm) - 1;
-      dm &= dm - 1u;
-      const bool h1 = dm != 0u;
-      const int k1 = h1 ? __ffs(dm) - 1 : k0;
-      dm &= dm - 1u;
-      const float a0 = L->L[k0][ddep] * L->vec[V_SOLVE][k0];
-      const float a1 = L->L[k1][ddep] * L->vec[V_SOLVE][k1];
-      x -= a0;
-      x -= h1 ? a1 : 0.f;
-    }
+  const bool ischain = c.chd >= 0;
+  /* forward pass along the limbs (leaves first): pull the pivot's final x */
+  const int nlv = c.m->nlevel - nroot;
+  for (int lv = 0; lv < nlv; lv++) {
+    const int q = c.cln - 1 - lv;
+    const bool has = ischain && q > c.cps;
+    const int src = has ? c.chd + q : c.l;
+    const float lk = L->L[has ? src : c.l][ddep];
+    const float xk = tsh(x, src);
+    if (has) x -= lk * xk;
   }
-  /* root chain, dense and redundant in every lane: the rest of the forward
-     pass, the diagonal, and the root-to-leaf pass inside the chain */
+  /* root chain, dense and redundant in every lane */
   float xr[RMAX];
 #pragma unroll
   for (int k = 0; k < RMAX; k++) xr[k] = 0.f;
   if (nroot > 0) {
-    if (c.l < nroot) L->vec[V_SOLVE][c.l] = x;
-    tsync();
+    float own[RMAX];
 #pragma unroll
-    for (int k = 0; k < RMAX; k++) xr[k] = k < nroot ? L->vec[V_SOLVE][k] : 0.f;
-    tsync();
+    for (int i = 0; i < RMAX; i++) own[i] = (ischain && i < nroot) ? L->L[c.l][i] : 0.f;
+#pragma unroll
+    for (int k = 0; k < RMAX; k++)
+      if (k < nroot) xr[k] = team_lane(x, k) - tsum(own[k] * (ischain ? x : 0.f));
 #pragma unroll
     for (int k = RMAX - 1; k >= 1; k--)
       if (k < nroot)
@@ -782,23 +786,23 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
       if (k < nroot)
 #pragma unroll
         for (int a = 0; a < k; a++) xr[k] -= L->L[k][a] * xr[a];
-  }
-  x *= Dinv;
-  int e0 = 0;
-  if (nroot > 0) {
-    /* branch dofs: ancestors 0..nroot-1 are the chain */
+    x *= Dinv;
 #pragma unroll
     for (int e = 0; e < RMAX; e++)
-      if (e < nroot && e < ddep) x -= L->L[c.l][e] * xr[e];
+      if (e < nroot) x -= own[e] * xr[e];
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
       if (c.l == k && k < nroot) x = xr[k];
-    e0 = nroot;
+  } else {
+    x *= Dinv;
   }
-  for (int e = e0; e < c.maxdd - 1; e++) {
-    int a = e <= ddep ? ancof(c, e) : 0;
-    float xa = tsh(x, a);
-    if (e < ddep) x -= L->L[c.l][e] * xa;
+  /* backward pass down the limbs: chain position s is final after step s */
+  for (int s = 0; s < nlv - 1; s++) {
+    const bool has = ischain && c.cps > s;
+    const int src = has ? c.chd + s : c.l;
+    const float la = L->L[c.l][has ? nroot + s : 0];
+    const float xa = tsh(x, src);
+    if (has) x -= la * xa;
   }
   return x;
 }
@@ -2022,10 +2026,6 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   }
   c.rowmask = rm;
   c.dk0 = isd ? l - m->body_dofadr[c.dbody] : 0;
-  c.mylevel = -1;
-  for (int lv = 0; lv < m->nlevel; lv++)
-    for (int mi = 0; mi < m->level_nmem[lv]; mi++)
-      if (isd && m->level_mem[lv][mi] == l) c.mylevel = lv;
   c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
   {
     int nr = 0;
@@ -2035,13 +2035,17 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
       else break;
     }
     c.nroot = nr;
-  }
-  if (l == ZROW) {
-    float z[CAP];
-#pragma unroll
-    for (int e = 0; e < CAP; e++) z[e] = 0.f;
-    st_row(&L->L[ZROW][0], z);
-    L->Dk[ZROW] = 0.f;
+    int hd = -1, ln = 0;
+    if (isd && l >= nr) {
+      hd = l;
+      while (m->dof_parent[hd] >= nr) hd = m->dof_parent[hd];
+      int k = hd;
+      while (k + 1 < c.nv && m->dof_parent[k + 1] == k) k++;
+      ln = k - hd + 1;
+    }
+    c.chd = hd;
+    c.cps = hd >= 0 ? l - hd : 0;
+    c.cln = ln;
   }
 }
 
