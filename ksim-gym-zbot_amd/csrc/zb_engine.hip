@@ -112,12 +112,19 @@ template <int CTRL>
 __device__ __forceinline__ int dppi(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
+/* value of lane l ^ 16 (the other 16-lane row of the team) without LDS:
+   v_permlane16_swap exchanges rows 0<->1 and 2<->3 of two copies */
+__device__ __forceinline__ uint32_t xor16(uint32_t v) {
+  auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return (threadIdx.x & 16) ? r[0] : r[1];
+}
+__device__ __forceinline__ float xor16f(float v) { return __uint_as_float(xor16(__float_as_uint(v))); }
 __device__ __forceinline__ float tsum(float v) {
   v += dppf<0xB1>(v);
   v += dppf<0x4E>(v);
   v += dppf<0x141>(v);
   v += dppf<0x140>(v);
-  v += __shfl_xor(v, 16, TEAM);
+  v += xor16f(v);
   return v;
 }
 __device__ __forceinline__ float tmaxf(float v) {
@@ -125,7 +132,7 @@ __device__ __forceinline__ float tmaxf(float v) {
   v = fmaxf(v, dppf<0x4E>(v));
   v = fmaxf(v, dppf<0x141>(v));
   v = fmaxf(v, dppf<0x140>(v));
-  v = fmaxf(v, __shfl_xor(v, 16, TEAM));
+  v = fmaxf(v, xor16f(v));
   return v;
 }
 __device__ __forceinline__ int tmaxi(int v) {
@@ -133,7 +140,7 @@ __device__ __forceinline__ int tmaxi(int v) {
   v = max(v, dppi<0x4E>(v));
   v = max(v, dppi<0x141>(v));
   v = max(v, dppi<0x140>(v));
-  v = max(v, __shfl_xor(v, 16, TEAM));
+  v = max(v, (int)xor16((uint32_t)v));
   return v;
 }
 __device__ __forceinline__ void tsync() { __syncthreads(); }
