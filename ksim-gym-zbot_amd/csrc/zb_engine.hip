@@ -819,16 +819,22 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int j = c.l;
+  const bool ischain = c.chd >= 0;
+  const int nroot = c.nroot;
   if (j < 32) L->vec[slot][j] = x;
   tsync();
-  float y = 0.f;
-  if (j < c.nv) {
+  /* lower part M(j, anc) x_anc: one row load + all ancestor values in flight */
+  float mrow[CAP], vv[CAP];
+  ld_row(&L->M[j & 31][0], mrow);
 #pragma unroll
-    for (int e = 0; e < CAP; e++)
-      if (e <= ddep) y += L->M[j][e] * L->vec[slot][ancof(c, e)];
-    /* transposed part M(k, j) x_k over descendants k, four per pass with
-       all loads issued up front (padded slots repeat k0 and add 0) */
-    uint32_t dm = c.desc;
+  for (int e = 0; e < CAP; e++) vv[e] = L->vec[slot][ancof(c, e)];
+  float y = 0.f;
+#pragma unroll
+  for (int e = 0; e < CAP; e++) y += (j < c.nv && e <= ddep) ? mrow[e] * vv[e] : 0.f;
+  if (j < c.nv) {
+    /* limb lanes: transposed part M(k, j) x_k over the deeper dofs of the
+       chain, four per pass with all loads issued up front */
+    uint32_t dm = ischain ? c.desc : 0u;
     while (dm) {
       int k[4];
       bool h[4];
@@ -845,6 +851,23 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
       for (int i = 0; i < 4; i++) y += h[i] ? a[i] : 0.f;
     }
   }
+  if (nroot > 0) {
+    /* root lanes: limb dofs by one team reduction per root dof (their
+       M(k, root i) = mrow[i]), deeper root dofs from LDS */
+    float sr = 0.f;
+#pragma unroll
+    for (int i = 0; i < RMAX; i++)
+      if (i < nroot) {
+        const float si = tsum(ischain ? mrow[i] * x : 0.f);
+        sr = j == i ? si : sr;
+      }
+    if (j < nroot) {
+#pragma unroll
+      for (int k = 1; k < RMAX; k++)
+        if (k < nroot && k > j) y += L->M[k][j] * L->vec[slot][k];
+      y += sr;
+    }
+  }
   tsync();
   return y;
 }
@@ -852,10 +875,13 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
 /* chain gather: sum_e Jc[e] * vec[slot][anc_e] for a contact row */
 __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) {
   const int kdep = vopq(r.kdep);
+  float jr[CAP], vv[CAP];
+  ld_row(&c.L->u.J[c.l][0], jr);
+#pragma unroll
+  for (int e = 0; e < CAP; e++) vv[e] = c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
   float v = 0.f;
 #pragma unroll
-  for (int e = 0; e < CAP; e++)
-    if (e <= kdep) v += c.L->u.J[c.l][e] * c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
+  for (int e = 0; e < CAP; e++) v += e <= kdep ? jr[e] * vv[e] : 0.f;
   return v;
 }
 

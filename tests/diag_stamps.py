@@ -22,8 +22,7 @@ from zbot_amd.engine import HipEngine  # noqa: E402
 PHASES = ["feetech", "kinematics", "com_crb_M", "factor_M", "rne_bias", "solve_smooth", "constraints",
           "nw_warmstart", "nw_update0", "nw_hessian0", "nw_solve0", "line_search", "update_constraint",
           "hessian_refactor", "newton_solve", "newton_check", "sensors", "integrate", "step_end(obs/reward/reset)",
-          "forward_entry"]
-NS = len(PHASES)
+          "forward_entry", "ls_mul_m", "ls_row_dot", "ls_c1c2", "ls_eval0"]
 
 
 def main():
@@ -31,8 +30,11 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--out", default="")
+    ap.add_argument("--lib", default="libzbot_hip_stamps.so")
+    ap.add_argument("--nslots", type=int, default=20, help="stamp slots of the build (ZB_NSTAMP)")
     args = ap.parse_args()
-    lib = os.path.join(ROOT, "ksim-gym-zbot_amd", "zbot_amd", "libzbot_hip_stamps.so")
+    NS = args.nslots
+    lib = os.path.join(ROOT, "ksim-gym-zbot_amd", "zbot_amd", args.lib)
     cm = compile_model()
     eng = HipEngine(cm, default_config(), args.n, lib_path=lib)
     eng.L.zb_get_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
