@@ -80,6 +80,29 @@ def test_model_validation_errors(hiplib, cmodel):
     assert rc == -4
 
 
+def test_tree_shape_validation(hiplib, cmodel):
+    """The engine's kinematics / subtree sums / factorization rely on the tree
+    shape (one branching body; root dof chain + unbranched limb chains):
+    zb_create must reject models that break it (ZB_EMODEL), not mis-simulate."""
+    h = C.c_void_p()
+    m = cmodel.cmodel
+    # a second branching body: re-parent a hand body onto the first arm link
+    bad = type(m).from_buffer_copy(m)
+    nb = bad.nbody
+    first_leg = [b for b in range(2, nb) if bad.body_parent[b] == 1][0]
+    leaf = [b for b in range(2, nb) if all(bad.body_parent[k] != b for k in range(nb))][-1]
+    bad.body_parent[leaf] = first_leg + 1  # first_leg + 1 already has a child
+    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc == -4 and b"branches" in hiplib.zb_last_error()
+    # a branching limb in the dof tree: hang a limb dof off the middle of another limb
+    bad = type(m).from_buffer_copy(m)
+    heads = [k for k in range(6, bad.nv) if bad.dof_parent[k] == 5]
+    k = heads[1]
+    bad.dof_parent[k] = heads[0] + 1
+    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc == -4 and b"unbranched" in hiplib.zb_last_error()
+
+
 def test_bad_config_rejected(hiplib, cmodel):
     cfg = default_config()
     cfg.struct_bytes = 4
