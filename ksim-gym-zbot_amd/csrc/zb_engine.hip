@@ -67,9 +67,8 @@ struct __align__(16) EnvL {
   float cdof[32][6];
   float M[32][CAP];
   float L[32][CAP];
-  union {
+  struct {
     float J[32][CAP];     /* contact-row Jacobians (constraint phase) */
-    float cdofdot[32][6]; /* velocity phase; recomputed for the sensors */
   } u;
   float sub[32][10];
   float vec[NVEC][32];
@@ -886,87 +885,88 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
 }
 
 /* ----------------------------------- RNE ----------------------------------- */
-/* cvel (lane b), cdofdot (LDS). Requires vec[V_QVEL]. */
-__device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B) {
+/* inclusive prefix sums of per-dof 6-vectors along the dof tree (root ->
+ * dof), by pointer jumping over the parent links: ceil(log2(depth)) rounds of
+ * cross-lane pulls instead of one ancestor gather per depth */
+__device__ __forceinline__ void dof_prefix6(const Ctx& c, float P[6]) {
   const int ddep = vopq(c.ddep);
-  MP m = c.m;
-  EnvL* L = c.L;
-  const int j = c.l;
-  if (j < c.nv) {
-    const int k0 = c.dk0;
-    const bool isfree = c.dfree;
-    int cap = ddep;                     /* hinge: before own contribution */
-    if (isfree) cap = ddep - k0 + 3;    /* free rot: after the translations */
-    float acc[6] = {0, 0, 0, 0, 0, 0}, before[6] = {0, 0, 0, 0, 0, 0};
+  bool live = c.l < c.nv && ddep > 0;
+  int ptr = live ? ancof(c, ddep - 1) : c.l;
+  for (int span = 1; span < c.maxdd; span <<= 1) {
+    float w[6];
 #pragma unroll
-    for (int e = 0; e < CAP; e++) {
-      if (e == cap) {
+    for (int k = 0; k < 6; k++) w[k] = tsh(P[k], ptr);
+    const int nptr = tshi(ptr, ptr);
+    const bool nlive = tshi(live ? 1 : 0, ptr) != 0;
+    if (live) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) before[k] = acc[k];
-      }
-      if (e <= ddep) {
-        int a = ancof(c, e);
-        float qv = L->vec[V_QVEL][a];
-#pragma unroll
-        for (int k = 0; k < 6; k++) acc[k] += L->cdof[a][k] * qv;
-      }
-    }
-    float cdd[6] = {0, 0, 0, 0, 0, 0};
-    if (!(isfree && k0 < 3)) {
-      float cd[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) cd[k] = L->cdof[j][k];
-      cross_motion(cdd, before, cd);
-    }
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      L->u.cdofdot[j][k] = cdd[k];
-      L->sub[j][k] = acc[k];
+      for (int k = 0; k < 6; k++) P[k] += w[k];
+      ptr = nptr;
+      live = nlive;
     }
   }
-  tsync();
-#pragma unroll
-  for (int k = 0; k < 6; k++) B.cv[k] = 0.f;
-  if (c.l < c.nb && c.blast >= 0) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) B.cv[k] = L->sub[c.blast][k];
-  }
-  tsync();
 }
 
-/* cacc per body (lane b) with or without qacc (vec[V_QACC]) */
-__device__ __forceinline__ void com_acc(const Ctx& c, float ca[6], bool with_acc) {
+/* mj_comVel: cvel (lane b, in B.cv) and cdof_dot (lane j, returned).
+   Requires the dof lanes' qvel in ls_v. */
+__device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B, float qv, float cdd[6]) {
   const int ddep = vopq(c.ddep);
+  EnvL* L = c.L;
+  const int j = c.l;
+  const bool isd = j < c.nv;
+  float cd[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) cd[k] = isd ? L->cdof[j][k] : 0.f;
+  float P[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) P[k] = isd ? cd[k] * qv : 0.f;
+  dof_prefix6(c, P);
+  /* velocity before this dof's own contribution: the parent's prefix for a
+     hinge, the translational part (dof 2) for the free joint's rotations */
+  const bool isfree = c.dfree;
+  const int k0 = c.dk0;
+  const int par = (isd && ddep > 0) ? ancof(c, ddep - 1) : j;
+  float before[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const float pp = tsh(P[k], par);
+    const float p2 = team_lane(P[k], 2);
+    before[k] = (isfree && k0 >= 3) ? p2 : (ddep > 0 ? pp : 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) cdd[k] = 0.f;
+  if (isd && !(isfree && k0 < 3)) cross_motion(cdd, before, cd);
+  /* body velocity = prefix at the body's deepest dof */
+  const int bl = (c.l < c.nb && c.blast >= 0) ? c.blast : 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const float v = tsh(P[k], bl);
+    B.cv[k] = (c.l < c.nb && c.blast >= 0) ? v : 0.f;
+  }
+}
+
+/* cacc per body (lane b): -g + prefix of cdof_dot*qvel (+ cdof*qacc) */
+__device__ __forceinline__ void com_acc(const Ctx& c, const float cdd[6], float qv, float qa, float ca[6],
+                                        bool with_acc) {
   MP m = c.m;
   EnvL* L = c.L;
   const int j = c.l;
-  if (j < c.nv) {
-    float acc[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
+  const bool isd = j < c.nv;
+  float P[6];
 #pragma unroll
-    for (int e = 0; e < CAP; e++) {
-      if (e <= ddep) {
-        int a = ancof(c, e);
-        float qv = L->vec[V_QVEL][a];
+  for (int k = 0; k < 6; k++) P[k] = isd ? cdd[k] * qv : 0.f;
+  if (with_acc) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) acc[k] += L->u.cdofdot[a][k] * qv;
-        if (with_acc) {
-          float qa = L->vec[V_QACC][a];
-#pragma unroll
-          for (int k = 0; k < 6; k++) acc[k] += L->cdof[a][k] * qa;
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 6; k++) L->sub[j][k] = acc[k];
+    for (int k = 0; k < 6; k++) P[k] += isd ? L->cdof[j][k] * qa : 0.f;
   }
-  tsync();
-  ca[0] = ca[1] = ca[2] = 0.f;
-  ca[3] = -m->gravity[0]; ca[4] = -m->gravity[1]; ca[5] = -m->gravity[2];
-  if (c.l < c.nb && c.blast >= 0) {
+  dof_prefix6(c, P);
+  const float g[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
+  const int bl = (c.l < c.nb && c.blast >= 0) ? c.blast : 0;
 #pragma unroll
-    for (int k = 0; k < 6; k++) ca[k] = L->sub[c.blast][k];
+  for (int k = 0; k < 6; k++) {
+    const float v = tsh(P[k], bl);
+    ca[k] = g[k] + ((c.l < c.nb && c.blast >= 0) ? v : 0.f);
   }
-  tsync();
 }
 
 /* body force cfrc (lane b) -> subtree sums in sub[] ; returns dof projection cdof_j . sub[body(j)] */
@@ -1434,9 +1434,11 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   /* velocities */
   if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < c.nv ? ls.v : 0.f;
   tsync();
-  com_vel(c, B);
+  const float qv = c.l < c.nv ? ls.v : 0.f;
+  float cdd[6];
+  com_vel(c, B, qv, cdd);
   float ca[6], zero6[6] = {0, 0, 0, 0, 0, 0};
-  com_acc(c, ca, false);
+  com_acc(c, cdd, qv, 0.f, ca, false);
   float bias = rne_project(c, B, ca, zero6);
   /* actuation + passive -> qfrc_smooth, qacc_smooth */
   float act = 0.f;
@@ -1496,10 +1498,11 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   sen.touch[1] = tch1;
   float cacc[6];
   {
-    BodyK B2 = B; /* com_vel rewrites cvel identically; recompute cdofdot (aliased with J) */
-    com_vel(c, B2);
+    BodyK B2 = B; /* cdof_dot again (not kept in registers through the solver) */
+    float cdd2[6];
+    com_vel(c, B2, qv, cdd2);
+    com_acc(c, cdd2, qv, ls.qacc, cacc, true);
   }
-  com_acc(c, cacc, true);
   /* cfrc_int subtree sums (in sub[]) */
   (void)rne_project(c, B, cacc, fext);
   /* imu site: framequat, gyro, accelerometer */
@@ -2268,9 +2271,11 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     float Dinv = factor_ldl(c, X, Xd);
     if (l < 32) L->vec[V_QVEL][l] = l < c.nv ? ls.v : 0.f;
     tsync();
-    com_vel(c, B);
+    const float qv = l < c.nv ? ls.v : 0.f;
+    float cdd[6];
+    com_vel(c, B, qv, cdd);
     float ca[6], z6[6] = {0, 0, 0, 0, 0, 0};
-    com_acc(c, ca, false);
+    com_acc(c, cdd, qv, 0.f, ca, false);
     float bias = rne_project(c, B, ca, z6);
     float act = c.act >= 0 ? m->act_gear[c.act] * ls.actforce : 0.f;
     float fs = (l < c.nv) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
