@@ -1011,6 +1011,7 @@ __device__ __forceinline__ float impedance(PS si, float xabs) {
   } else {
     float x = xabs / width, y;
     if (power == 1.f) y = x;
+    else if (power == 2.f) y = x <= mid ? x * x / mid : 1.f - (1.f - x) * (1.f - x) / (1.f - mid); /* MuJoCo default */
     else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
     else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
     imp = dmin + y * (dmax - dmin);

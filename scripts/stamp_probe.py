@@ -1,0 +1,56 @@
+"""Build a phase-stamp library with extra stamp points injected at code anchors.
+
+    python scripts/stamp_probe.py OUT.so "anchor text::name[::after]" ...
+
+Each spec inserts `STAMP(S_X_<name>);` before (default) or after the first
+occurrence of the anchor text in zb_engine.hip; the new slots extend the S_*
+enum and ZB_NSTAMP. Run the result with
+    python tests/diag_stamps.py --lib OUT.so --nslots N --names name1,name2,...
+Diagnostic only: the product library is never built this way.
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "ksim-gym-zbot_amd", "csrc")
+
+
+def main():
+    out, specs = sys.argv[1], sys.argv[2:]
+    src = open(os.path.join(CSRC, "zb_engine.hip")).read()
+    hdr = open(os.path.join(CSRC, "zb_internal.h")).read()
+    names = []
+    for spec in specs:
+        parts = spec.split("::")
+        anchor, name = parts[0], parts[1]
+        after = len(parts) > 2 and parts[2] == "after"
+        i = src.index(anchor)
+        ins = f"STAMP(S_X_{name});\n"
+        if after:
+            j = i + len(anchor)
+            src = src[:j] + "\n" + ins + src[j:]
+        else:
+            src = src[:i] + ins + src[i:]
+        names.append(name)
+    extra = "".join(f"S_X_{n}, " for n in names)
+    src = src.replace("S_ENTRY, NSTAMP", "S_ENTRY, " + extra + "NSTAMP")
+    n = 20 + len(names)
+    hdr = hdr.replace("#define ZB_NSTAMP      20", f"#define ZB_NSTAMP      {n}")
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "zb_engine.hip"), "w").write(src)
+        open(os.path.join(d, "zb_internal.h"), "w").write(hdr)
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{d}", f"-I{ROOT}/include",
+               "-fno-signed-zeros", "-freciprocal-math", "-fno-math-errno", "-fapprox-func", "-DZB_STAMPS", "-shared",
+               "-o", out, os.path.join(d, "zb_engine.hip"), os.path.join(CSRC, "zb_capi.cpp")]
+        # zb_capi.cpp must see the patched header: compile it from the temp dir copy
+        capi = open(os.path.join(CSRC, "zb_capi.cpp")).read()
+        open(os.path.join(d, "zb_capi.cpp"), "w").write(capi)
+        cmd[-1] = os.path.join(d, "zb_capi.cpp")
+        subprocess.run(cmd, check=True)
+    print(n, ",".join(names))
+
+
+if __name__ == "__main__":
+    main()

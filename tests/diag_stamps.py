@@ -22,7 +22,7 @@ from zbot_amd.engine import HipEngine  # noqa: E402
 PHASES = ["feetech", "kinematics", "com_crb_M", "factor_M", "rne_bias", "solve_smooth", "constraints",
           "nw_warmstart", "nw_update0", "nw_hessian0", "nw_solve0", "line_search", "update_constraint",
           "hessian_refactor", "newton_solve", "newton_check", "sensors", "integrate", "step_end(obs/reward/reset)",
-          "forward_entry", "ls_mul_m", "ls_row_dot", "ls_c1c2", "ls_eval0"]
+          "forward_entry"]
 
 
 def main():
@@ -32,8 +32,11 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--lib", default="libzbot_hip_stamps.so")
     ap.add_argument("--nslots", type=int, default=20, help="stamp slots of the build (ZB_NSTAMP)")
+    ap.add_argument("--names", default="", help="names of the extra slots (scripts/stamp_probe.py)")
     args = ap.parse_args()
     NS = args.nslots
+    if args.names:
+        PHASES.extend(args.names.split(","))
     lib = os.path.join(ROOT, "ksim-gym-zbot_amd", "zbot_amd", args.lib)
     cm = compile_model()
     eng = HipEngine(cm, default_config(), args.n, lib_path=lib)
