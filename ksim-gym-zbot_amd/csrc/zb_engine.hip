@@ -41,7 +41,7 @@ constexpr float MINIMP = 0.0001f;
 constexpr float MAXIMP = 0.9999f;
 constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0); /* train.py:1113-1116 */
 
-enum { V_QVEL = 0, V_QACC = 1, V_TMP = 2, V_TMP2 = 3, V_SOLVE = 4, NVEC = 5 };
+enum { V_QVEL = 0, V_TMP = 1, V_TMP2 = 2, NVEC = 3 };
 constexpr int RMAX = 6;  /* longest root dof chain factored as one dense block (free joint) */
 enum { P_Q0 = 0, P_ARM = 1, P_DAMP = 2, P_FLOSS = 3, P_MSCALE = 4 };
 /* stamp slots: STAMP(i) closes phase i (time since the previous stamp) */
@@ -70,7 +70,10 @@ struct __align__(16) EnvL {
   struct {
     float J[32][CAP];     /* contact-row Jacobians (constraint phase) */
   } u;
-  float sub[32][10];
+  union {
+    float sub[32][10];      /* subtree sums (smooth phase, sensors) */
+    float Hs[32][CAP + 1];  /* unfactored Newton Hessian rows (+ diagonal) */
+  };
   float vec[NVEC][32];
   float rowDA[32];
   float rowF[32];
@@ -143,6 +146,8 @@ __device__ __forceinline__ int tmaxi(int v) {
   return v;
 }
 __device__ __forceinline__ void tsync() { __syncthreads(); }
+/* bitmask over the team's lanes of predicate p */
+__device__ __forceinline__ uint32_t team_ballot(bool p) { return (uint32_t)(__ballot(p) >> (threadIdx.x & 32)); }
 /* An opaque copy of a per-lane constant: stops the compiler from hoisting
    compares against it (e.g. the 12 `e < depth` lane masks) out of the step
    loops, where they would pin SGPR pairs for the whole launch. */
@@ -1223,13 +1228,30 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
 }
 
 /* H = M + J' D_active J rows (depth-indexed), then factor -> Dinv */
-__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
+/* H = M + J' D_active J (depth-indexed rows), then factor -> 1/D_j.
+ * full: from M and every active contact row. Otherwise the stored unfactored
+ * H of the previous build is updated with the rows whose activity changed
+ * (+-D_r J_r J_r') -- MuJoCo's Newton also only re-assembles on a change of
+ * the active set, and the change is usually a handful of rows. */
+__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo,
+                                                int phi) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
-  float H[CAP];
-  float Hd = load_mrow(c, H);
+  float H[CAP], Hd;
+  uint32_t tb;
+  if (full) {
+    Hd = load_mrow(c, H);
+    tb = r.exmask & c.rowmask; /* rowDA (written by update_constraint) holds D or 0 */
+  } else {
+    ld_row(&L->Hs[c.l][0], H);
+    Hd = L->Hs[c.l][CAP];
+    const float dl = r.ex ? ((r.act ? r.D : 0.f) - (pa ? r.D : 0.f)) : 0.f;
+    L->rowF[c.l] = dl; /* rowF is free until the next update_constraint */
+    tb = team_ballot(dl != 0.f) & c.rowmask;
+    tsync();
+  }
+  const float* da = full ? L->rowDA : L->rowF;
   if (c.l < c.nv) {
-    uint32_t tb = r.exmask & c.rowmask;
     while (tb) {
       const int k0 = __ffs(tb) - 1;
       tb &= tb - 1u;
@@ -1240,8 +1262,8 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
       ld_row(&L->u.J[k0][0], j0);
       ld_row(&L->u.J[k1][0], j1);
       const float jd0 = L->u.J[k0][ddep], jd1 = L->u.J[k1][ddep];
-      const float jj0 = L->rowDA[k0] * jd0;
-      const float jj1 = h1 ? L->rowDA[k1] * jd1 : 0.f;
+      const float jj0 = da[k0] * jd0;
+      const float jj1 = h1 ? da[k1] * jd1 : 0.f;
       Hd += jj0 * jd0;
       Hd += jj1 * jd1;
 #pragma unroll
@@ -1251,11 +1273,19 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r) {
       }
     }
     float dd = 0.f;
-    if (r.hf && r.actf) dd += r.Df;
-    if (r.hlo && r.actlo) dd += r.Dlo;
-    if (r.hhi && r.acthi) dd += r.Dhi;
+    if (full) {
+      if (r.hf && r.actf) dd += r.Df;
+      if (r.hlo && r.actlo) dd += r.Dlo;
+      if (r.hhi && r.acthi) dd += r.Dhi;
+    } else {
+      if (r.hf) dd += (float)(r.actf - pf) * r.Df;
+      if (r.hlo) dd += (float)(r.actlo - plo) * r.Dlo;
+      if (r.hhi) dd += (float)(r.acthi - phi) * r.Dhi;
+    }
     Hd += dd;
   }
+  st_row(&L->Hs[c.l][0], H);
+  L->Hs[c.l][CAP] = Hd;
   tsync();
   return factor_ldl(c, H, Hd);
 }
@@ -1343,7 +1373,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float grad;
   float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
-  float Dinv = hessian_factor(c, r);
+  float Dinv = hessian_factor(c, r, true, 0, 0, 0, 0);
   STAMP(S_HESS0);
   float search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
@@ -1367,7 +1397,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = tmaxi((r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1 : 0) != 0;
     STAMP(S_UPD);
-    if (changed) Dinv = hessian_factor(c, r);
+    if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo, phi);
     STAMP(S_HESS);
     float mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
@@ -1468,7 +1498,6 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   STAMP(S_CHECK);
   if (!with_sensors) return;
   /* ------------------- sensors (mj_rnePostConstraint etc.) ------------------ */
-  if (c.l < 32) L->vec[V_QACC][c.l] = ls.qacc;
   tsync();
   /* contact forces per geom -> cfrc_ext on the geom body, touch */
   float fext[6] = {0, 0, 0, 0, 0, 0};
