@@ -1200,25 +1200,40 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
     L->rowF[c.l] = r.f;
     L->rowDA[c.l] = r.act ? r.D : 0.f;
   }
+  /* J'f per dof: the 16 contact rows of a foot are one 16-lane DPP row and
+     share the foot's dof chain, so sum_r J_r[e] f_r (e = chain position) is
+     a row reduction for all 12 positions at once (interleaved DPP, no LDS);
+     a dof adds the sums of every foot whose chain holds it at its depth */
+  float q[CAP];
+  {
+    float jr[CAP];
+    ld_row(&L->u.J[c.l][0], jr);
+    const float fr = r.ex ? r.f : 0.f;
+#pragma unroll
+    for (int e = 0; e < CAP; e++) q[e] = r.ex ? jr[e] * fr : 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < CAP; e++) q[e] += dppf<0xB1>(q[e]);
+#pragma unroll
+  for (int e = 0; e < CAP; e++) q[e] += dppf<0x4E>(q[e]);
+#pragma unroll
+  for (int e = 0; e < CAP; e++) q[e] += dppf<0x141>(q[e]);
+#pragma unroll
+  for (int e = 0; e < CAP; e++) q[e] += dppf<0x140>(q[e]);
+  float so = 0.f, sx = 0.f; /* this row's foot / the other foot, at depth(j) */
+#pragma unroll
+  for (int e = 0; e < CAP; e++) {
+    const float o = xor16f(q[e]);
+    so = e == ddep ? q[e] : so;
+    sx = e == ddep ? o : sx;
+  }
   tsync();
   float qc = 0.f;
   if (c.l < c.nv) {
-    uint32_t tb = r.exmask & c.rowmask;
-    while (tb) {
-      int k[4];
-      bool h[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        h[i] = tb != 0u;
-        k[i] = h[i] ? __ffs(tb) - 1 : k[0];
-        tb &= tb - 1u;
-      }
-      float a[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) a[i] = L->u.J[k[i]][ddep] * L->rowF[k[i]];
-#pragma unroll
-      for (int i = 0; i < 4; i++) qc += h[i] ? a[i] : 0.f;
-    }
+    const int g = (c.l >> 4) & 1;
+    const bool own = (c.rowmask >> (16 * g)) & 0xFFFFu;
+    const bool oth = (c.rowmask >> (16 * (1 - g))) & 0xFFFFu;
+    qc = (own ? so : 0.f) + (oth ? sx : 0.f);
     if (r.hf) qc += r.ff;
     if (r.hlo) qc += r.flo;
     if (r.hhi) qc -= r.fhi;
