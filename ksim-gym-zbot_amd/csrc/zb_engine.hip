@@ -129,6 +129,21 @@ __device__ __forceinline__ float tsum(float v) {
   v += xor16f(v);
   return v;
 }
+/* N independent team sums, stage by stage so the DPP/permlane steps of
+   different values interleave (bit-identical to N separate tsum calls) */
+template <int N>
+__device__ __forceinline__ void tsum_n(float v[N]) {
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] += dppf<0xB1>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] += dppf<0x4E>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] += dppf<0x141>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] += dppf<0x140>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] += xor16f(v[i]);
+}
 __device__ __forceinline__ float tmaxf(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
@@ -539,9 +554,11 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
     quat2mat(iR, iq);
     mulmm3(Ri, BR, iR);
   }
-  float mt = tsum(mass);
+  float ms[4] = {mass, mass * xipos[0], mass * xipos[1], mass * xipos[2]};
+  tsum_n<4>(ms);
+  const float mt = ms[0];
 #pragma unroll
-  for (int k = 0; k < 3; k++) cm[k] = tsum(mass * xipos[k]) / mt;
+  for (int k = 0; k < 3; k++) cm[k] = ms[1 + k] / mt;
   /* cinert: inertia about cm in world orientation (mju_inertCom) */
   float ci[10];
   {
@@ -705,13 +722,30 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
        G[i][e] = sum_k D_k L(k,i) L(k,e) (team reductions), then the dense
        elimination k = nroot-1 .. 0, redundantly in every lane */
     tsync();
+    constexpr int NG = RMAX * (RMAX + 1) / 2;
+    float g[NG];
+    {
+      int t = 0;
+#pragma unroll
+      for (int i = 0; i < RMAX; i++) {
+        const float wi = ischain ? Xd * X[i] : 0.f;
+#pragma unroll
+        for (int j = 0; j <= i; j++) g[t++] = wi * X[j];
+      }
+    }
+    tsum_n<NG>(g);
     float A[RMAX][RMAX], D[RMAX];
+    {
+      int t = 0;
 #pragma unroll
-    for (int i = 0; i < RMAX; i++) {
-      const float wi = ischain ? Xd * X[i] : 0.f;
-      D[i] = i < nroot ? L->Dk[i] - tsum(wi * X[i]) : 1.f;
+      for (int i = 0; i < RMAX; i++) {
 #pragma unroll
-      for (int j = 0; j < RMAX; j++) A[i][j] = (j < i && i < nroot) ? L->L[i][j] - tsum(wi * X[j]) : 0.f;
+        for (int j = 0; j < RMAX; j++) A[i][j] = 0.f;
+#pragma unroll
+        for (int j = 0; j < i; j++) A[i][j] = i < nroot ? L->L[i][j] - g[t + j] : 0.f;
+        D[i] = i < nroot ? L->Dk[i] - g[t + i] : 1.f;
+        t += i + 1;
+      }
     }
     tsync();
 #pragma unroll
@@ -781,9 +815,13 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
     float own[RMAX];
 #pragma unroll
     for (int i = 0; i < RMAX; i++) own[i] = (ischain && i < nroot) ? L->L[c.l][i] : 0.f;
+    float sr[RMAX];
+#pragma unroll
+    for (int k = 0; k < RMAX; k++) sr[k] = own[k] * (ischain ? x : 0.f);
+    tsum_n<RMAX>(sr);
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
-      if (k < nroot) xr[k] = team_lane(x, k) - tsum(own[k] * (ischain ? x : 0.f));
+      if (k < nroot) xr[k] = team_lane(x, k) - sr[k];
 #pragma unroll
     for (int k = RMAX - 1; k >= 1; k--)
       if (k < nroot)
@@ -858,13 +896,13 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   if (nroot > 0) {
     /* root lanes: limb dofs by one team reduction per root dof (their
        M(k, root i) = mrow[i]), deeper root dofs from LDS */
+    float si[RMAX];
+#pragma unroll
+    for (int i = 0; i < RMAX; i++) si[i] = (ischain && i < nroot) ? mrow[i] * x : 0.f;
+    tsum_n<RMAX>(si);
     float sr = 0.f;
 #pragma unroll
-    for (int i = 0; i < RMAX; i++)
-      if (i < nroot) {
-        const float si = tsum(ischain ? mrow[i] * x : 0.f);
-        sr = j == i ? si : sr;
-      }
+    for (int i = 0; i < RMAX; i++) sr = j == i ? si[i] : sr;
     if (j < nroot) {
 #pragma unroll
       for (int k = 1; k < RMAX; k++)
@@ -1312,8 +1350,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
   r.Jv = r.ex ? row_dot(c, r, V_TMP) : 0.f;
   tsync();
-  float c1 = tsum(c.l < c.nv ? search * (Ma - fs) : 0.f);
-  float c2 = tsum(c.l < c.nv ? search * Mv : 0.f);
+  float cc[2] = {c.l < c.nv ? search * (Ma - fs) : 0.f, c.l < c.nv ? search * Mv : 0.f};
+  tsum_n<2>(cc);
+  const float c1 = cc[0], c2 = cc[1];
   auto eval = [&](float alpha, float& d1, float& d2) {
     float g1 = 0.f, g2 = 0.f;
     if (r.ex && r.Jv != 0.f) {
@@ -1337,8 +1376,10 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
         if (x < 0.f) { g1 += r.Dhi * x * (-jv); g2 += r.Dhi * jv * jv; }
       }
     }
-    d1 = c1 + alpha * c2 + tsum(g1);
-    d2 = c2 + tsum(g2);
+    float gg[2] = {g1, g2};
+    tsum_n<2>(gg);
+    d1 = c1 + alpha * c2 + gg[0];
+    d2 = c2 + gg[1];
   };
   float d1, d2;
   eval(0.f, d1, d2);
@@ -1370,9 +1411,10 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float jw = r.ex ? row_dot(c, r, V_TMP) - r.aref : 0.f;
   float js = r.ex ? row_dot(c, r, V_TMP2) - r.aref : 0.f;
   tsync();
-  float cw = tsum((c.l < c.nv ? 0.5f * (Ma - fs) * (x - qs) : 0.f) +
-                  rows_cost(c, r, jw, x - r.af, x - r.alo, -x - r.ahi));
-  float cs = tsum(rows_cost(c, r, js, qs - r.af, qs - r.alo, -qs - r.ahi));
+  float cws[2] = {(c.l < c.nv ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, x - r.alo, -x - r.ahi),
+                  rows_cost(c, r, js, qs - r.af, qs - r.alo, -qs - r.ahi)};
+  tsum_n<2>(cws);
+  const float cw = cws[0], cs = cws[1];
   if (cw > cs) {
     x = qs;
     Ma = mul_m(c, x, V_TMP);
@@ -1530,8 +1572,10 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
       cross3(tq, off, F);
       fn = r.f;
     }
-    float ext[6] = {tsum(tq[0]), tsum(tq[1]), tsum(tq[2]), tsum(F[0]), tsum(F[1]), tsum(F[2])};
-    float fnt = tsum(fn);
+    float ex7[7] = {tq[0], tq[1], tq[2], F[0], F[1], F[2], fn};
+    tsum_n<7>(ex7);
+    float ext[6] = {ex7[0], ex7[1], ex7[2], ex7[3], ex7[4], ex7[5]};
+    float fnt = ex7[6];
     if (c.l == m->geom_body[g]) {
 #pragma unroll
       for (int k = 0; k < 6; k++) fext[k] += ext[k];
@@ -1891,9 +1935,11 @@ __device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, 
       if ((ankle >> c.act) & 1u) p2 = w;
       if ((arm >> c.act) & 1u) p3 = w;
     }
-    t[ZB_T_STRAIGHT_LEG] = tsum(p1);
-    t[ZB_T_ANKLE_KNEE] = tsum(p2);
-    t[ZB_T_ARM_POSE] = tsum(p3);
+    float pp[3] = {p1, p2, p3};
+    tsum_n<3>(pp);
+    t[ZB_T_STRAIGHT_LEG] = pp[0];
+    t[ZB_T_ANKLE_KNEE] = pp[1];
+    t[ZB_T_ARM_POSE] = pp[2];
   }
   total = 0.f;
   for (int i = 0; i < ZB_NUM_TERMS; i++) {
