@@ -147,7 +147,8 @@ static int check_model(const ZbModel* m) {
     if (m->level_nmem[lv] == 1 && m->level_mem[lv][0] == k && m->dof_depth[k] == k) nroot++;
     else break;
   }
-  if (nroot < 1) return fail(ZB_EMODEL, "dof tree has no root chain");
+  if (nroot != 6) return fail(ZB_EMODEL, "dof tree: the free joint's 6 dofs must form the root chain (got %d)", nroot);
+  if (m->nv != 6 + ZB_NJ) return fail(ZB_EMODEL, "task layout needs nv=%d (got %d)", 6 + ZB_NJ, m->nv);
   for (int k = nroot; k < m->nv; k++) {
     const int p = m->dof_parent[k];
     int nchild_prev = 0;

@@ -42,7 +42,12 @@ constexpr float MAXIMP = 0.9999f;
 constexpr float DEADBAND = (float)(2.0 * 0.087 * 3.14159265358979323846 / 180.0); /* train.py:1113-1116 */
 
 enum { V_QVEL = 0, V_TMP = 1, V_TMP2 = 2, NVEC = 3 };
-constexpr int RMAX = 6;  /* longest root dof chain factored as one dense block (free joint) */
+constexpr int RMAX = 6;  /* root dof chain factored as one dense block: the free joint */
+/* task topology, fixed by the C-ABI (zb_create checks the model against it):
+   26 bodies, nv = 6 (free joint) + 20 hinges, root dof chain of length 6 */
+constexpr int NB = ZB_NBODY_TASK;
+constexpr int NV = 6 + ZB_NJ;
+constexpr int NROOT = RMAX;
 enum { P_Q0 = 0, P_ARM = 1, P_DAMP = 2, P_FLOSS = 3, P_MSCALE = 4 };
 /* stamp slots: STAMP(i) closes phase i (time since the previous stamp) */
 enum {
@@ -341,8 +346,7 @@ struct Ctx {
   uint64_t seed;
   uint32_t env;
   int l;
-  int nb, nv, nu, ngeom, maxbd, maxdd;
-  int nroot; /* dofs 0..nroot-1: the unbranched chain at the top of the dof tree (one per top level) */
+  int nu, ngeom, maxbd, maxdd;
   /* lane as a limb-chain dof (dofs >= nroot; each limb is an unbranched chain of
      consecutive dofs hanging off dof nroot-1, checked by zb_create) */
   int chd, cps, cln; /* chain head dof, position in the chain, chain length (chd = -1: not a chain dof) */
@@ -428,7 +432,7 @@ __device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
 __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const LaneS& ls, BodyK& B) {
   MP m = c.m;
   const int b = c.l;
-  const bool isb = b >= 1 && b < c.nb;
+  const bool isb = b >= 1 && b < NB;
   /* relative hinge angle of this body's joint, from its dof lane */
   float qrel_dof = ls.q - c.L->par[P_Q0][c.l];
   float ang = tsh(qrel_dof, c.bdofadr < 0 ? 0 : c.bdofadr);
@@ -501,7 +505,7 @@ __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const La
 template <int K>
 __device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
   EnvL* L = c.L;
-  const bool chain = c.l >= 2 && c.l < c.nb && c.nch == 1;
+  const bool chain = c.l >= 2 && c.l < NB && c.nch == 1;
   int nxt = chain ? childof(c, 0) : c.l;
   bool live = chain;
   for (int span = 1; span < c.maxbd - 1; span <<= 1) {
@@ -539,7 +543,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   MP m = c.m;
   EnvL* L = c.L;
   const int b = c.l;
-  const bool isbody = b >= 1 && b < c.nb;
+  const bool isbody = b >= 1 && b < NB;
   float mass = isbody ? m->body_mass[b][0] * c.L->par[P_MSCALE][c.l] : 0.f;
   float xipos[3], Ri[9];
   {
@@ -600,7 +604,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
     quat2mat(R, xqs);
 #pragma unroll
     for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], bj);
-    if (j < c.nv) {
+    if (j < NV) {
       float cd[6];
       int jt = m->body_jnttype[bj];
       if (jt == ZB_JNT_FREE) {
@@ -637,7 +641,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   /* M rows: M(j, anc_e(j)) = cdof_anc . (crb_body(j) * cdof_j), packed storage */
   {
     const int j = c.l;
-    if (j < c.nv) {
+    if (j < NV) {
       float cr[10], cd[6], F[6], mr[CAP];
 #pragma unroll
       for (int k = 0; k < 10; k++) cr[k] = L->sub[c.dbody][k];
@@ -676,7 +680,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
-  const int nroot = c.nroot;
+  const int nroot = NROOT;
   const bool isroot = c.l < nroot;
   const bool ischain = c.chd >= 0;
   /* root rows are only touched by the dense block at the end: park them */
@@ -784,8 +788,8 @@ __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
   const int j = c.l & 31;
   ld_row(&c.L->M[j][0], X);
 #pragma unroll
-  for (int e = 0; e < CAP; e++) X[e] = (e < ddep && c.l < c.nv) ? X[e] : 0.f;
-  return (c.l < c.nv) ? c.L->M[j][ddep] : 1.f;
+  for (int e = 0; e < CAP; e++) X[e] = (e < ddep && c.l < NV) ? X[e] : 0.f;
+  return (c.l < NV) ? c.L->M[j][ddep] : 1.f;
 }
 
 /* x <- (L'DL)^-1 x, x held by dof lanes. Forward pass by level (a lane's
@@ -795,7 +799,7 @@ __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
 __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
-  const int nroot = c.nroot;
+  const int nroot = NROOT;
   const bool ischain = c.chd >= 0;
   /* forward pass along the limbs (leaves first): pull the pivot's final x */
   const int nlv = c.m->nlevel - nroot;
@@ -862,7 +866,7 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   EnvL* L = c.L;
   const int j = c.l;
   const bool ischain = c.chd >= 0;
-  const int nroot = c.nroot;
+  const int nroot = NROOT;
   if (j < 32) L->vec[slot][j] = x;
   tsync();
   /* lower part M(j, anc) x_anc: one row load + all ancestor values in flight */
@@ -872,8 +876,8 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   for (int e = 0; e < CAP; e++) vv[e] = L->vec[slot][ancof(c, e)];
   float y = 0.f;
 #pragma unroll
-  for (int e = 0; e < CAP; e++) y += (j < c.nv && e <= ddep) ? mrow[e] * vv[e] : 0.f;
-  if (j < c.nv) {
+  for (int e = 0; e < CAP; e++) y += (j < NV && e <= ddep) ? mrow[e] * vv[e] : 0.f;
+  if (j < NV) {
     /* limb lanes: transposed part M(k, j) x_k over the deeper dofs of the
        chain, four per pass with all loads issued up front */
     uint32_t dm = ischain ? c.desc : 0u;
@@ -933,7 +937,7 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
  * cross-lane pulls instead of one ancestor gather per depth */
 __device__ __forceinline__ void dof_prefix6(const Ctx& c, float P[6]) {
   const int ddep = vopq(c.ddep);
-  bool live = c.l < c.nv && ddep > 0;
+  bool live = c.l < NV && ddep > 0;
   int ptr = live ? ancof(c, ddep - 1) : c.l;
   for (int span = 1; span < c.maxdd; span <<= 1) {
     float w[6];
@@ -956,7 +960,7 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B, float qv, float 
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int j = c.l;
-  const bool isd = j < c.nv;
+  const bool isd = j < NV;
   float cd[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) cd[k] = isd ? L->cdof[j][k] : 0.f;
@@ -980,11 +984,11 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B, float qv, float 
   for (int k = 0; k < 6; k++) cdd[k] = 0.f;
   if (isd && !(isfree && k0 < 3)) cross_motion(cdd, before, cd);
   /* body velocity = prefix at the body's deepest dof */
-  const int bl = (c.l < c.nb && c.blast >= 0) ? c.blast : 0;
+  const int bl = (c.l < NB && c.blast >= 0) ? c.blast : 0;
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     const float v = tsh(P[k], bl);
-    B.cv[k] = (c.l < c.nb && c.blast >= 0) ? v : 0.f;
+    B.cv[k] = (c.l < NB && c.blast >= 0) ? v : 0.f;
   }
 }
 
@@ -994,7 +998,7 @@ __device__ __forceinline__ void com_acc(const Ctx& c, const float cdd[6], float 
   MP m = c.m;
   EnvL* L = c.L;
   const int j = c.l;
-  const bool isd = j < c.nv;
+  const bool isd = j < NV;
   float P[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) P[k] = isd ? cdd[k] * qv : 0.f;
@@ -1004,11 +1008,11 @@ __device__ __forceinline__ void com_acc(const Ctx& c, const float cdd[6], float 
   }
   dof_prefix6(c, P);
   const float g[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-  const int bl = (c.l < c.nb && c.blast >= 0) ? c.blast : 0;
+  const int bl = (c.l < NB && c.blast >= 0) ? c.blast : 0;
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     const float v = tsh(P[k], bl);
-    ca[k] = g[k] + ((c.l < c.nb && c.blast >= 0) ? v : 0.f);
+    ca[k] = g[k] + ((c.l < NB && c.blast >= 0) ? v : 0.f);
   }
 }
 
@@ -1016,7 +1020,7 @@ __device__ __forceinline__ void com_acc(const Ctx& c, const float cdd[6], float 
 __device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const float ca[6], const float fext[6]) {
   EnvL* L = c.L;
   float f[6];
-  if (c.l >= 1 && c.l < c.nb) {
+  if (c.l >= 1 && c.l < NB) {
     float f1[6], t[6], f2[6], ci[10];
 #pragma unroll
     for (int k = 0; k < 10; k++) ci[k] = L->ci[c.l][k];
@@ -1031,7 +1035,7 @@ __device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const
   }
   subtree_sum<6>(c, f);
   float r = 0.f;
-  if (c.l < c.nv) {
+  if (c.l < NV) {
     float cd[6], fs[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) {
@@ -1178,7 +1182,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   r.af = r.alo = r.ahi = 0.f;
   r.Rf = 0.f;
   r.fl = 0.f;
-  if (l < c.nv) {
+  if (l < NV) {
     float v = ls.v;
     float dA = m->dof_invweight0[l];
     if (c.L->par[P_FLOSS][c.l] > 0.f) {
@@ -1229,7 +1233,7 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float cost = 0.f;
-  if (c.l < c.nv) cost += 0.5f * (Ma - fs) * (qacc - qs);
+  if (c.l < NV) cost += 0.5f * (Ma - fs) * (qacc - qs);
   if (r.ex) cost += eval_one(r.jar, r.D, r.f, r.act);
   if (r.hf) cost += eval_fric(r.jf, r.Df, r.Rf, r.fl, r.ff, r.actf);
   if (r.hlo) cost += eval_one(r.jlo, r.Dlo, r.flo, r.actlo);
@@ -1267,7 +1271,7 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
   }
   tsync();
   float qc = 0.f;
-  if (c.l < c.nv) {
+  if (c.l < NV) {
     const int g = (c.l >> 4) & 1;
     const bool own = (c.rowmask >> (16 * g)) & 0xFFFFu;
     const bool oth = (c.rowmask >> (16 * (1 - g))) & 0xFFFFu;
@@ -1304,7 +1308,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     tsync();
   }
   const float* da = full ? L->rowDA : L->rowF;
-  if (c.l < c.nv) {
+  if (c.l < NV) {
     while (tb) {
       const int k0 = __ffs(tb) - 1;
       tb &= tb - 1u;
@@ -1350,7 +1354,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
   r.Jv = r.ex ? row_dot(c, r, V_TMP) : 0.f;
   tsync();
-  float cc[2] = {c.l < c.nv ? search * (Ma - fs) : 0.f, c.l < c.nv ? search * Mv : 0.f};
+  float cc[2] = {c.l < NV ? search * (Ma - fs) : 0.f, c.l < NV ? search * Mv : 0.f};
   tsum_n<2>(cc);
   const float c1 = cc[0], c2 = cc[1];
   auto eval = [&](float alpha, float& d1, float& d2) {
@@ -1359,7 +1363,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
       float x = r.jar + alpha * r.Jv;
       if (x < 0.f) { g1 += r.D * x * r.Jv; g2 += r.D * r.Jv * r.Jv; }
     }
-    if (c.l < c.nv && search != 0.f) {
+    if (c.l < NV && search != 0.f) {
       float jv = search;
       if (r.hf) {
         float x = r.jf + alpha * jv, Rf = r.Rf * r.fl;
@@ -1411,7 +1415,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float jw = r.ex ? row_dot(c, r, V_TMP) - r.aref : 0.f;
   float js = r.ex ? row_dot(c, r, V_TMP2) - r.aref : 0.f;
   tsync();
-  float cws[2] = {(c.l < c.nv ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, x - r.alo, -x - r.ahi),
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, x - r.alo, -x - r.ahi),
                   rows_cost(c, r, js, qs - r.af, qs - r.alo, -qs - r.ahi)};
   tsum_n<2>(cws);
   const float cw = cws[0], cs = cws[1];
@@ -1426,7 +1430,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   r.jf = x - r.af;
   r.jlo = x - r.alo;
   r.jhi = -x - r.ahi;
-  float scale = 1.0f / (m->meaninertia * (float)(c.nv > 1 ? c.nv : 1));
+  float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
   float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
@@ -1460,7 +1464,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     STAMP(S_SOLVE);
     it++;
     float improvement = scale * (oldcost - cost);
-    float gradient = scale * sqrtf(tsum(c.l < c.nv ? grad * grad : 0.f));
+    float gradient = scale * sqrtf(tsum(c.l < NV ? grad * grad : 0.f));
     if (improvement < cfg->tolerance || gradient < cfg->tolerance) break;
     search = -mg;
   }
@@ -1520,9 +1524,9 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   float DinvM = factor_ldl(c, X, Xd);
   STAMP(S_FACM);
   /* velocities */
-  if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < c.nv ? ls.v : 0.f;
+  if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < NV ? ls.v : 0.f;
   tsync();
-  const float qv = c.l < c.nv ? ls.v : 0.f;
+  const float qv = c.l < NV ? ls.v : 0.f;
   float cdd[6];
   com_vel(c, B, qv, cdd);
   float ca[6], zero6[6] = {0, 0, 0, 0, 0, 0};
@@ -1537,7 +1541,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   } else {
     ls.actforce = 0.f;
   }
-  float fs = (c.l < c.nv) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
+  float fs = (c.l < NV) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
   STAMP(S_RNE);
   float qs = solve_ldl(c, fs, DinvM);
   STAMP(S_SOLVES);
@@ -1551,7 +1555,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   } else {
     qacc = solve_newton(c, r, qs, fs, ls.w, iters);
   }
-  ls.qacc = (c.l < c.nv) ? qacc : 0.f;
+  ls.qacc = (c.l < NV) ? qacc : 0.f;
   STAMP(S_CHECK);
   if (!with_sensors) return;
   /* ------------------- sensors (mj_rnePostConstraint etc.) ------------------ */
@@ -1648,7 +1652,7 @@ __device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls) {
   const float dt = c.cfg->dt;
   float vn = ls.v + dt * ls.qacc;
   float v0 = tsh(vn, 0), v1 = tsh(vn, 1), v2 = tsh(vn, 2), w0 = tsh(vn, 3), w1 = tsh(vn, 4), w2 = tsh(vn, 5);
-  if (c.l < c.nv) {
+  if (c.l < NV) {
     ls.w = ls.qacc; /* mj_advance: qacc_warmstart */
     ls.v = vn;
     if (c.qadr >= 0) ls.q += dt * vn;
@@ -1675,13 +1679,13 @@ __device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, co
   const bool rz = (c.cfg->flags & ZB_F_RANDOMIZE) && rnd;
   const int l = c.l;
   float arm = 0.f, damp = 0.f, floss = 0.f, q0 = 0.f;
-  if (l < c.nv) {
+  if (l < NV) {
     arm = m->dof_armature[l] * (rz ? rnd[ZB_R_ARMATURE + l] : 1.f);
     damp = m->dof_damping[l] * (rz ? rnd[ZB_R_DAMPING + l] : 1.f);
     floss = m->dof_frictionloss[l] * (rz ? rnd[ZB_R_FRICTION + l] : 1.f);
     if (c.qadr >= 0) q0 = m->qpos0[c.qadr] + ((rz && c.act >= 0) ? rnd[ZB_R_QPOS0 + c.act] : 0.f);
   }
-  c.L->par[P_MSCALE][l] = (rz && l < c.nb) ? rnd[ZB_R_MASS + l] : 1.f;
+  c.L->par[P_MSCALE][l] = (rz && l < NB) ? rnd[ZB_R_MASS + l] : 1.f;
   c.L->par[P_ARM][l] = arm;
   c.L->par[P_DAMP][l] = damp;
   c.L->par[P_FLOSS][l] = floss;
@@ -1820,7 +1824,7 @@ __device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, 
       oc[ZB_NJ + l] = va / 10.f;
       oc[457 + l] = fa / 100.f;
     }
-    if (l >= 1 && l < c.nb) {
+    if (l >= 1 && l < NB) {
       for (int k = 0; k < 10; k++) oc[40 + (l - 1) * 10 + k] = c.L->ci[l][k];
       for (int k = 0; k < 6; k++) oc[290 + (l - 1) * 6 + k] = B.cv[k];
     }
@@ -1976,7 +1980,7 @@ __device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, con
   s.nanflag = fbits(st[ZB_S_NAN]);
   ls.q = ls.v = ls.w = 0.f;
   ls.pp = ls.pv = ls.ptau = 0.f;
-  if (l < c.nv) {
+  if (l < NV) {
     ls.v = st[ZB_S_QVEL + l];
     ls.w = st[ZB_S_QACCW + l];
     if (c.qadr >= 0) ls.q = st[ZB_S_QPOS + c.qadr];
@@ -1993,7 +1997,7 @@ __device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, con
 
 __device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const LaneS& ls, float* st) {
   const int l = c.l;
-  if (l < c.nv) {
+  if (l < NV) {
     st[ZB_S_QVEL + l] = ls.v;
     st[ZB_S_QACCW + l] = ls.w;
     if (c.qadr >= 0) st[ZB_S_QPOS + c.qadr] = ls.q;
@@ -2044,7 +2048,7 @@ __device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, 
     uniform2(c.seed, P_RESET, (uint32_t)(c.act / 2), c.env, episode, u0, u1);
     float u = (c.act & 1) ? u1 : u0;
     ls.v = cfg->reset_qvel_scale * (2.f * u - 1.f);
-  } else if (l < c.nv && c.qadr >= 0) {
+  } else if (l < NV && c.qadr >= 0) {
     ls.q = m->qpos0[c.qadr];
   }
   {
@@ -2090,13 +2094,11 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.env = env;
   const int l = threadIdx.x & (TEAM - 1);
   c.l = l;
-  c.nb = m->nbody;
-  c.nv = m->nv;
   c.nu = m->nu;
   c.ngeom = m->ngeom;
   c.maxdd = m->max_depth;
   /* body role */
-  const bool isb = l < c.nb;
+  const bool isb = l < NB;
   c.bpar = isb ? m->body_parent[l] : 0;
   c.bdep = isb ? m->body_depth[l] : 1000;
   c.bjt = isb ? m->body_jnttype[l] : ZB_JNT_NONE;
@@ -2105,7 +2107,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.maxbd = tmaxi(isb ? c.bdep : 0);
   int nch = 0;
   uint32_t ch0 = 0, ch1 = 0;
-  for (int b = 1; b < c.nb; b++) {
+  for (int b = 1; b < NB; b++) {
     if (isb && m->body_parent[b] == l && nch < 8) {
       if (nch < 4) ch0 |= (uint32_t)b << (8 * nch);
       else ch1 |= (uint32_t)b << (8 * (nch - 4));
@@ -2122,7 +2124,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   }
   c.lvlch = lv;
   /* dof role */
-  const bool isd = l < c.nv;
+  const bool isd = l < NV;
   c.ddep = isd ? m->dof_depth[l] : 0;
   c.dbody = isd ? m->dof_body[l] : 0;
   c.qadr = isd ? m->dof_qposadr[l] : -1;
@@ -2141,7 +2143,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.anc1 = a1;
   c.anc2 = a2;
   uint32_t desc = 0;
-  for (int k = 0; k < c.nv; k++) {
+  for (int k = 0; k < NV; k++) {
     int dk = m->dof_depth[k];
     if (isd && k != l && dk > c.ddep && m->dof_anc[k][c.ddep] == l) desc |= 1u << k;
   }
@@ -2155,19 +2157,13 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.dk0 = isd ? l - m->body_dofadr[c.dbody] : 0;
   c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
   {
-    int nr = 0;
-    for (int k = 0; k < RMAX && k < m->nlevel; k++) {
-      const int lv = m->nlevel - 1 - k;
-      if (m->level_nmem[lv] == 1 && m->level_mem[lv][0] == k && m->dof_depth[k] == k) nr++;
-      else break;
-    }
-    c.nroot = nr;
+    const int nr = NROOT;
     int hd = -1, ln = 0;
     if (isd && l >= nr) {
       hd = l;
       while (m->dof_parent[hd] >= nr) hd = m->dof_parent[hd];
       int k = hd;
-      while (k + 1 < c.nv && m->dof_parent[k + 1] == k) k++;
+      while (k + 1 < NV && m->dof_parent[k + 1] == k) k++;
       ln = k - hd + 1;
     }
     c.chd = hd;
@@ -2232,7 +2228,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       STAMP(S_INT);
       if (++ss < cfg->n_substeps) continue;
       {
-        bool bad = (c.l < c.nv) && !(isfinite(ls.q) && isfinite(ls.v));
+        bool bad = (c.l < NV) && !(isfinite(ls.q) && isfinite(ls.v));
         if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
       }
       bool fail;
@@ -2326,21 +2322,21 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   const int l = c.l;
   EnvL* L = c.L;
   /* dense M from depth-indexed rows */
-  for (int i = l; i < c.nv * c.nv; i += TEAM) d[ZB_DBG_QM + i] = 0.f;
+  for (int i = l; i < NV * NV; i += TEAM) d[ZB_DBG_QM + i] = 0.f;
   __threadfence_block();
   tsync();
-  if (l < c.nv) {
+  if (l < NV) {
     for (int ee = 0; ee <= c.ddep; ee++) {
       int aa = ancof(c, ee);
       float v = L->M[l][ee];
-      d[ZB_DBG_QM + l * c.nv + aa] = v;
-      d[ZB_DBG_QM + aa * c.nv + l] = v;
+      d[ZB_DBG_QM + l * NV + aa] = v;
+      d[ZB_DBG_QM + aa * NV + l] = v;
     }
     d[ZB_DBG_QACC + l] = ls.qacc;
   }
   /* recompute smooth quantities for the dump is avoided: store qacc only; the
      bias/qacc_smooth slots are filled by a second, constraint-free pass below */
-  if (l < c.nb) {
+  if (l < NB) {
     for (int k = 0; k < 3; k++) d[ZB_DBG_XPOS + 3 * l + k] = B.xp[k];
     for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = c.L->ci[l][k];
     for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
@@ -2360,18 +2356,18 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     float X[CAP];
     float Xd = load_mrow(c, X);
     float Dinv = factor_ldl(c, X, Xd);
-    if (l < 32) L->vec[V_QVEL][l] = l < c.nv ? ls.v : 0.f;
+    if (l < 32) L->vec[V_QVEL][l] = l < NV ? ls.v : 0.f;
     tsync();
-    const float qv = l < c.nv ? ls.v : 0.f;
+    const float qv = l < NV ? ls.v : 0.f;
     float cdd[6];
     com_vel(c, B, qv, cdd);
     float ca[6], z6[6] = {0, 0, 0, 0, 0, 0};
     com_acc(c, cdd, qv, 0.f, ca, false);
     float bias = rne_project(c, B, ca, z6);
     float act = c.act >= 0 ? m->act_gear[c.act] * ls.actforce : 0.f;
-    float fs = (l < c.nv) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
+    float fs = (l < NV) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
     float qs = solve_ldl(c, fs, Dinv);
-    if (l < c.nv) {
+    if (l < NV) {
       d[ZB_DBG_BIAS + l] = bias;
       d[ZB_DBG_QACCS + l] = qs;
     }
