@@ -149,6 +149,10 @@ static int check_model(const ZbModel* m) {
   }
   if (nroot != 6) return fail(ZB_EMODEL, "dof tree: the free joint's 6 dofs must form the root chain (got %d)", nroot);
   if (m->nv != 6 + ZB_NJ) return fail(ZB_EMODEL, "task layout needs nv=%d (got %d)", 6 + ZB_NJ, m->nv);
+  /* depths / counts the engine is compiled for (zb_engine.hip NGEOM, MAXBD, MAXDD, NLIMBLV) */
+  if (m->ngeom != 2 || maxbd != 8 || m->max_depth != 12 || m->nlevel != 12)
+    return fail(ZB_EMODEL, "engine compiled for ngeom 2, body depth 8, dof depth 12, 12 levels (got %d, %d, %d, %d)",
+                m->ngeom, maxbd, m->max_depth, m->nlevel);
   for (int k = nroot; k < m->nv; k++) {
     const int p = m->dof_parent[k];
     int nchild_prev = 0;

@@ -48,6 +48,10 @@ constexpr int RMAX = 6;  /* root dof chain factored as one dense block: the free
 constexpr int NB = ZB_NBODY_TASK;
 constexpr int NV = 6 + ZB_NJ;
 constexpr int NROOT = RMAX;
+constexpr int NGEOM = 2;      /* foot sole boxes */
+constexpr int MAXBD = 8;      /* deepest body (world 0, base 1, ..., foot 8) */
+constexpr int MAXDD = 12;     /* dof chain depth: 6 root + 6 leg */
+constexpr int NLIMBLV = 6;    /* elimination levels inside the limbs (longest limb) */
 enum { P_Q0 = 0, P_ARM = 1, P_DAMP = 2, P_FLOSS = 3, P_MSCALE = 4 };
 /* stamp slots: STAMP(i) closes phase i (time since the previous stamp) */
 enum {
@@ -346,7 +350,7 @@ struct Ctx {
   uint64_t seed;
   uint32_t env;
   int l;
-  int nu, ngeom, maxbd, maxdd;
+  int nu;
   /* lane as a limb-chain dof (dofs >= nroot; each limb is an unbranched chain of
      consecutive dofs hanging off dof nroot-1, checked by zb_create) */
   int chd, cps, cln; /* chain head dof, position in the chain, chain length (chd = -1: not a chain dof) */
@@ -469,7 +473,7 @@ __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const La
       anc = c.bpar;
     }
   }
-  for (int span = 1; span < c.maxbd; span <<= 1) {
+  for (int span = 1; span < MAXBD; span <<= 1) {
     float ap[3], aq[4];
 #pragma unroll
     for (int k = 0; k < 3; k++) ap[k] = tsh(p[k], anc);
@@ -508,7 +512,7 @@ __device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
   const bool chain = c.l >= 2 && c.l < NB && c.nch == 1;
   int nxt = chain ? childof(c, 0) : c.l;
   bool live = chain;
-  for (int span = 1; span < c.maxbd - 1; span <<= 1) {
+  for (int span = 1; span < MAXBD - 1; span <<= 1) {
     float w[K];
 #pragma unroll
     for (int i = 0; i < K; i++) w[i] = tsh(v[i], nxt);
@@ -691,7 +695,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
   /* limb levels (height inside the chain, leaves first): the pivot of each
      chain divides its row; every shallower lane of the chain pulls that row
      with ds_bpermute (no LDS round trip) and applies its Schur update */
-  const int nlv = c.m->nlevel - nroot;
+  const int nlv = NLIMBLV;
   for (int lv = 0; lv < nlv; lv++) {
     const int q = c.cln - 1 - lv; /* chain position of this level's pivot */
     if (ischain && q == c.cps) {
@@ -802,7 +806,7 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   const int nroot = NROOT;
   const bool ischain = c.chd >= 0;
   /* forward pass along the limbs (leaves first): pull the pivot's final x */
-  const int nlv = c.m->nlevel - nroot;
+  const int nlv = NLIMBLV;
   for (int lv = 0; lv < nlv; lv++) {
     const int q = c.cln - 1 - lv;
     const bool has = ischain && q > c.cps;
@@ -939,7 +943,7 @@ __device__ __forceinline__ void dof_prefix6(const Ctx& c, float P[6]) {
   const int ddep = vopq(c.ddep);
   bool live = c.l < NV && ddep > 0;
   int ptr = live ? ancof(c, ddep - 1) : c.l;
-  for (int span = 1; span < c.maxdd; span <<= 1) {
+  for (int span = 1; span < MAXDD; span <<= 1) {
     float w[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) w[k] = tsh(P[k], ptr);
@@ -1087,7 +1091,7 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
   MP m = c.m;
   const int l = c.l;
   const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
-  const bool gvalid = g < c.ngeom;
+  const bool gvalid = g < NGEOM;
   const int gg = gvalid ? g : 0;
   const int gb = gvalid ? m->geom_body[g] : 0;
   float R[9], xp[3], xqs[4];
@@ -1124,7 +1128,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   const int l = c.l;
   /* ---- contact rows: lane = 16*geom + 4*corner + edge ---- */
   const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
-  const bool gvalid = g < c.ngeom;
+  const bool gvalid = g < NGEOM;
   const int gb = gvalid ? m->geom_body[g] : 0;
   int kd = gvalid ? m->body_lastdof[gb] : 0;
   if (kd < 0) kd = 0;
@@ -1566,7 +1570,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   (void)contact_point(c, s, B, cpos, cdir, cmu);
   const int rgeom = c.l >> 4;
   float tch0 = 0.f, tch1 = 0.f;
-  for (int g = 0; g < c.ngeom; g++) {
+  for (int g = 0; g < NGEOM; g++) {
     bool mine = r.ex && rgeom == g;
     float F[3] = {0, 0, 0}, tq[3] = {0, 0, 0};
     float fn = 0.f;
@@ -2095,8 +2099,6 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   const int l = threadIdx.x & (TEAM - 1);
   c.l = l;
   c.nu = m->nu;
-  c.ngeom = m->ngeom;
-  c.maxdd = m->max_depth;
   /* body role */
   const bool isb = l < NB;
   c.bpar = isb ? m->body_parent[l] : 0;
@@ -2104,7 +2106,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.bjt = isb ? m->body_jnttype[l] : ZB_JNT_NONE;
   c.bdofadr = isb ? m->body_dofadr[l] : -1;
   c.blast = isb ? m->body_lastdof[l] : -1;
-  c.maxbd = tmaxi(isb ? c.bdep : 0);
+  
   int nch = 0;
   uint32_t ch0 = 0, ch1 = 0;
   for (int b = 1; b < NB; b++) {
@@ -2118,7 +2120,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.ch0 = ch0;
   c.ch1 = ch1;
   uint64_t lv = 0;
-  for (int d = 0; d <= c.maxbd && d < 16; d++) {
+  for (int d = 0; d <= MAXBD && d < 16; d++) {
     int mx = tmaxi(c.bdep == d ? nch : 0);
     lv |= (uint64_t)(mx & 0xf) << (4 * d);
   }
@@ -2149,7 +2151,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   }
   c.desc = desc;
   uint32_t rm = 0;
-  for (int g = 0; g < c.ngeom; g++) {
+  for (int g = 0; g < NGEOM; g++) {
     int kd = m->body_lastdof[m->geom_body[g]];
     if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm |= 0xFFFFu << (16 * g);
   }
