@@ -652,18 +652,25 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 #pragma unroll
       for (int k = 0; k < 6; k++) cd[k] = L->cdof[j][k];
       mul_inert_vec(F, cr, cd);
+      const float arm = c.L->par[P_ARM][c.l];
+      /* branch-free gather, four ancestor rows in flight per chunk (rows past
+         the lane's depth read ancestor slot 0 and are masked) */
 #pragma unroll
-      for (int e = 0; e < CAP; e++) {
-        float v = 0.f;
-        if (e <= ddep) {
-          int a = ancof(c, e);
-          float ca[6];
+      for (int e0 = 0; e0 < CAP; e0 += 4) {
+        float ca[4][6];
 #pragma unroll
-          for (int k = 0; k < 6; k++) ca[k] = L->cdof[a][k];
-          v = dot6(ca, F);
-          if (e == ddep) v += c.L->par[P_ARM][c.l];
+        for (int i = 0; i < 4; i++) {
+          const int a = ancof(c, e0 + i);
+#pragma unroll
+          for (int k = 0; k < 6; k++) ca[i][k] = L->cdof[a][k];
         }
-        mr[e] = v;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int e = e0 + i;
+          float v = dot6(ca[i], F);
+          if (e == ddep) v += arm;
+          mr[e] = e <= ddep ? v : 0.f;
+        }
       }
       st_row(&L->M[j][0], mr);
     }
