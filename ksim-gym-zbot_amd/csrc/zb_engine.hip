@@ -372,6 +372,10 @@ __device__ __forceinline__ int ancof(const Ctx& c, int e) {
   uint32_t w = e < 4 ? c.anc0 : (e < 8 ? c.anc1 : c.anc2);
   return (int)((w >> ((e & 3) * 8)) & 0xffu);
 }
+/* ancestor dof at depth e of a dof whose limb chain starts at dof `head`
+   (root dofs: head < 0): the tree shape makes ancestors dofs 0..NROOT-1
+   followed by a contiguous run of the limb (e past the depth: a valid dummy) */
+__device__ __forceinline__ int anc_lin(int head, int e) { return e < NROOT ? e : (head < 0 ? 0 : head) + e - NROOT; }
 __device__ __forceinline__ int anc_packed(uint32_t a0, uint32_t a1, uint32_t a2, int e) {
   uint32_t w = e < 4 ? a0 : (e < 8 ? a1 : a2);
   return (int)((w >> ((e & 3) * 8)) & 0xffu);
@@ -399,7 +403,7 @@ struct BodyK {
 struct Rows {
   /* contact row (lane = row) */
   bool ex;
-  uint32_t ka0, ka1, ka2; int kdep;
+  int chd; int kdep; /* limb chain head and depth of the row's last dof */
   float aref, D, jar, Jv, f;
   int act;
   /* dof rows: frictionloss, lower, upper limit */
@@ -660,7 +664,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
         float ca[4][6];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          const int a = ancof(c, e0 + i);
+          const int a = anc_lin(c.chd, e0 + i);
 #pragma unroll
           for (int k = 0; k < 6; k++) ca[i][k] = L->cdof[a][k];
         }
@@ -884,7 +888,7 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   float mrow[CAP], vv[CAP];
   ld_row(&L->M[j & 31][0], mrow);
 #pragma unroll
-  for (int e = 0; e < CAP; e++) vv[e] = L->vec[slot][ancof(c, e)];
+  for (int e = 0; e < CAP; e++) vv[e] = L->vec[slot][anc_lin(c.chd, e)];
   float y = 0.f;
 #pragma unroll
   for (int e = 0; e < CAP; e++) y += (j < NV && e <= ddep) ? mrow[e] * vv[e] : 0.f;
@@ -935,7 +939,7 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
   float jr[CAP], vv[CAP];
   ld_row(&c.L->u.J[c.l][0], jr);
 #pragma unroll
-  for (int e = 0; e < CAP; e++) vv[e] = c.L->vec[slot][anc_packed(r.ka0, r.ka1, r.ka2, e)];
+  for (int e = 0; e < CAP; e++) vv[e] = c.L->vec[slot][anc_lin(r.chd, e)];
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < CAP; e++) v += e <= kdep ? jr[e] * vv[e] : 0.f;
@@ -1139,9 +1143,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   const int gb = gvalid ? m->geom_body[g] : 0;
   int kd = gvalid ? m->body_lastdof[gb] : 0;
   if (kd < 0) kd = 0;
-  r.ka0 = (uint32_t)tshi((int)c.anc0, kd);
-  r.ka1 = (uint32_t)tshi((int)c.anc1, kd);
-  r.ka2 = (uint32_t)tshi((int)c.anc2, kd);
+  r.chd = tshi(c.chd, kd);
   r.kdep = tshi(c.ddep, kd);
   r.ex = false;
   r.act = 0;
@@ -1163,7 +1165,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
 #pragma unroll
     for (int e = 0; e < CAP; e++) {
       if (e <= r.kdep) {
-        int a = anc_packed(r.ka0, r.ka1, r.ka2, e);
+        int a = anc_lin(r.chd, e);
         float v = sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
                   dir[0] * L->cdof[a][3] + dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
         Jc[e] = v;
