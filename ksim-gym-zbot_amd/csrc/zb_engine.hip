@@ -360,26 +360,16 @@ struct Ctx {
   uint64_t lvlch; /* per body depth: max #children among bodies at that depth (4 bits each) */
   /* lane as dof */
   int ddep, dbody, qadr, act;
-  uint32_t anc0, anc1, anc2;
-  uint32_t desc; /* strict descendants of dof l */
   uint32_t rowmask; /* contact rows whose Jacobian chain contains dof l */
   int dk0;          /* index of dof l within its body's joint (free joint: 0..5) */
   int dfree;        /* dof l belongs to a free joint */
 };
 
 
-__device__ __forceinline__ int ancof(const Ctx& c, int e) {
-  uint32_t w = e < 4 ? c.anc0 : (e < 8 ? c.anc1 : c.anc2);
-  return (int)((w >> ((e & 3) * 8)) & 0xffu);
-}
 /* ancestor dof at depth e of a dof whose limb chain starts at dof `head`
    (root dofs: head < 0): the tree shape makes ancestors dofs 0..NROOT-1
    followed by a contiguous run of the limb (e past the depth: a valid dummy) */
 __device__ __forceinline__ int anc_lin(int head, int e) { return e < NROOT ? e : (head < 0 ? 0 : head) + e - NROOT; }
-__device__ __forceinline__ int anc_packed(uint32_t a0, uint32_t a1, uint32_t a2, int e) {
-  uint32_t w = e < 4 ? a0 : (e < 8 ? a1 : a2);
-  return (int)((w >> ((e & 3) * 8)) & 0xffu);
-}
 __device__ __forceinline__ int childof(const Ctx& c, int k) {
   uint32_t w = k < 4 ? c.ch0 : c.ch1;
   return (int)((w >> ((k & 3) * 8)) & 0xffu);
@@ -894,23 +884,15 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   for (int e = 0; e < CAP; e++) y += (j < NV && e <= ddep) ? mrow[e] * vv[e] : 0.f;
   if (j < NV) {
     /* limb lanes: transposed part M(k, j) x_k over the deeper dofs of the
-       chain, four per pass with all loads issued up front */
-    uint32_t dm = ischain ? c.desc : 0u;
-    while (dm) {
-      int k[4];
-      bool h[4];
+       chain (consecutive dofs chd+cps+1 .. chd+cln-1), all loads in flight */
+    float a[NLIMBLV - 1];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        h[i] = dm != 0u;
-        k[i] = h[i] ? __ffs(dm) - 1 : k[0];
-        dm &= dm - 1u;
-      }
-      float a[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) a[i] = L->M[k[i]][ddep] * L->vec[slot][k[i]];
-#pragma unroll
-      for (int i = 0; i < 4; i++) y += h[i] ? a[i] : 0.f;
+    for (int q = 1; q < NLIMBLV; q++) {
+      const int k = ischain ? min(c.chd + c.cps + q, NV - 1) : j;
+      a[q - 1] = L->M[k][ddep] * L->vec[slot][k];
     }
+#pragma unroll
+    for (int q = 1; q < NLIMBLV; q++) y += (ischain && c.cps + q < c.cln) ? a[q - 1] : 0.f;
   }
   if (nroot > 0) {
     /* root lanes: limb dofs by one team reduction per root dof (their
@@ -953,7 +935,7 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
 __device__ __forceinline__ void dof_prefix6(const Ctx& c, float P[6]) {
   const int ddep = vopq(c.ddep);
   bool live = c.l < NV && ddep > 0;
-  int ptr = live ? ancof(c, ddep - 1) : c.l;
+  int ptr = live ? anc_lin(c.chd, ddep - 1) : c.l;
   for (int span = 1; span < MAXDD; span <<= 1) {
     float w[6];
 #pragma unroll
@@ -987,7 +969,7 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B, float qv, float 
      hinge, the translational part (dof 2) for the free joint's rotations */
   const bool isfree = c.dfree;
   const int k0 = c.dk0;
-  const int par = (isd && ddep > 0) ? ancof(c, ddep - 1) : j;
+  const int par = (isd && ddep > 0) ? anc_lin(c.chd, ddep - 1) : j;
   float before[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) {
@@ -2142,23 +2124,11 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.act = -1;
   for (int a = 0; a < c.nu; a++)
     if (isd && m->act_dof[a] == l) c.act = a;
-  uint32_t a0 = 0, a1 = 0, a2 = 0;
-  for (int e = 0; e < CAP; e++) {
-    int a = isd ? m->dof_anc[l][e] : -1;
-    uint32_t v = (uint32_t)(a < 0 ? 0 : a) & 0xffu;
-    if (e < 4) a0 |= v << (8 * e);
-    else if (e < 8) a1 |= v << (8 * (e - 4));
-    else a2 |= v << (8 * (e - 8));
-  }
-  c.anc0 = a0;
-  c.anc1 = a1;
-  c.anc2 = a2;
   uint32_t desc = 0;
   for (int k = 0; k < NV; k++) {
     int dk = m->dof_depth[k];
     if (isd && k != l && dk > c.ddep && m->dof_anc[k][c.ddep] == l) desc |= 1u << k;
   }
-  c.desc = desc;
   uint32_t rm = 0;
   for (int g = 0; g < NGEOM; g++) {
     int kd = m->body_lastdof[m->geom_body[g]];
@@ -2338,7 +2308,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   tsync();
   if (l < NV) {
     for (int ee = 0; ee <= c.ddep; ee++) {
-      int aa = ancof(c, ee);
+      int aa = anc_lin(c.chd, ee);
       float v = L->M[l][ee];
       d[ZB_DBG_QM + l * NV + aa] = v;
       d[ZB_DBG_QM + aa * NV + l] = v;
