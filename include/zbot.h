@@ -60,6 +60,13 @@ const char* zb_last_error(void);
 void zb_default_config(ZbEnvConfig* cfg);
 
 /*
+ * The engine is compiled for the Z-Bot task topology and checks the model
+ * against it (ZB_EMODEL otherwise): 26 bodies of which only the floating base
+ * (body 1, free joint) branches; nu = 20 hinge actuators, nv = 26; the free
+ * joint's 6 dofs form the root of the dof tree and every limb is an
+ * unbranched chain of consecutive dofs; 2 foot sole boxes; body depth 8,
+ * dof depth 12.
+ *
  * Create a handle simulating `n_envs` environments whose global ids are
  * [env_offset, env_offset + n_envs) — RNG streams are keyed by global id, so
  * results for a given env do not depend on how envs are sharded over GPUs.
