@@ -1201,25 +1201,34 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
 }
 
 /* ------------------------------ Newton solver ------------------------------ */
+/* row cost / force / activity (mj_constraintUpdate), branch-free selects */
 __device__ __forceinline__ float eval_fric(float jar, float D, float R, float fl, float& force, int& act) {
-  float Rf = R * fl;
-  if (jar <= -Rf) { force = fl; act = 0; return -fl * (0.5f * Rf + jar); }
-  if (jar >= Rf) { force = -fl; act = 0; return fl * (jar - 0.5f * Rf); }
-  force = -D * jar; act = 1; return 0.5f * D * jar * jar;
+  const float Rf = R * fl;
+  const bool lo = jar <= -Rf, hi = jar >= Rf;
+  force = lo ? fl : (hi ? -fl : -D * jar);
+  act = (lo || hi) ? 0 : 1;
+  return lo ? -fl * (0.5f * Rf + jar) : (hi ? fl * (jar - 0.5f * Rf) : 0.5f * D * jar * jar);
 }
 __device__ __forceinline__ float eval_one(float jar, float D, float& force, int& act) {
-  if (jar < 0.f) { force = -D * jar; act = 1; return 0.5f * D * jar * jar; }
-  force = 0.f; act = 0; return 0.f;
+  const bool on = jar < 0.f;
+  force = on ? -D * jar : 0.f;
+  act = on ? 1 : 0;
+  return on ? 0.5f * D * jar * jar : 0.f;
 }
 
 /* row costs at given jar values (no state change) */
 __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jlo_, float jhi_) {
-  float cost = 0.f, f;
+  float f;
   int a;
-  if (r.ex) cost += eval_one(jc, r.D, f, a);
-  if (r.hf) cost += eval_fric(jf_, r.Df, r.Rf, r.fl, f, a);
-  if (r.hlo) cost += eval_one(jlo_, r.Dlo, f, a);
-  if (r.hhi) cost += eval_one(jhi_, r.Dhi, f, a);
+  const float k0 = eval_one(jc, r.D, f, a);
+  const float k1 = eval_fric(jf_, r.Df, r.Rf, r.fl, f, a);
+  const float k2 = eval_one(jlo_, r.Dlo, f, a);
+  const float k3 = eval_one(jhi_, r.Dhi, f, a);
+  float cost = 0.f;
+  cost += r.ex ? k0 : 0.f;
+  cost += r.hf ? k1 : 0.f;
+  cost += r.hlo ? k2 : 0.f;
+  cost += r.hhi ? k3 : 0.f;
   return cost;
 }
 
@@ -1229,10 +1238,27 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
   EnvL* L = c.L;
   float cost = 0.f;
   if (c.l < NV) cost += 0.5f * (Ma - fs) * (qacc - qs);
-  if (r.ex) cost += eval_one(r.jar, r.D, r.f, r.act);
-  if (r.hf) cost += eval_fric(r.jf, r.Df, r.Rf, r.fl, r.ff, r.actf);
-  if (r.hlo) cost += eval_one(r.jlo, r.Dlo, r.flo, r.actlo);
-  if (r.hhi) cost += eval_one(r.jhi, r.Dhi, r.fhi, r.acthi);
+  {
+    /* all four row kinds evaluated, results kept only for rows that exist */
+    float f0, f1, f2, f3;
+    int a0, a1, a2, a3;
+    const float k0 = eval_one(r.jar, r.D, f0, a0);
+    const float k1 = eval_fric(r.jf, r.Df, r.Rf, r.fl, f1, a1);
+    const float k2 = eval_one(r.jlo, r.Dlo, f2, a2);
+    const float k3 = eval_one(r.jhi, r.Dhi, f3, a3);
+    cost += r.ex ? k0 : 0.f;
+    cost += r.hf ? k1 : 0.f;
+    cost += r.hlo ? k2 : 0.f;
+    cost += r.hhi ? k3 : 0.f;
+    r.f = r.ex ? f0 : r.f;
+    r.act = r.ex ? a0 : r.act;
+    r.ff = r.hf ? f1 : r.ff;
+    r.actf = r.hf ? a1 : r.actf;
+    r.flo = r.hlo ? f2 : r.flo;
+    r.actlo = r.hlo ? a2 : r.actlo;
+    r.fhi = r.hhi ? f3 : r.fhi;
+    r.acthi = r.hhi ? a3 : r.acthi;
+  }
   if (r.ex) {
     L->rowF[c.l] = r.f;
     L->rowDA[c.l] = r.act ? r.D : 0.f;
@@ -1353,27 +1379,33 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   tsum_n<2>(cc);
   const float c1 = cc[0], c2 = cc[1];
   auto eval = [&](float alpha, float& d1, float& d2) {
+    /* piecewise-quadratic row terms, branch-free (rows with a zero
+       direction contribute exact zeros, as the branchy form skips them) */
     float g1 = 0.f, g2 = 0.f;
-    if (r.ex && r.Jv != 0.f) {
-      float x = r.jar + alpha * r.Jv;
-      if (x < 0.f) { g1 += r.D * x * r.Jv; g2 += r.D * r.Jv * r.Jv; }
+    {
+      const float x = r.jar + alpha * r.Jv;
+      const bool on = r.ex && x < 0.f;
+      g1 += on ? r.D * x * r.Jv : 0.f;
+      g2 += on ? r.D * r.Jv * r.Jv : 0.f;
     }
-    if (c.l < NV && search != 0.f) {
-      float jv = search;
-      if (r.hf) {
-        float x = r.jf + alpha * jv, Rf = r.Rf * r.fl;
-        if (x <= -Rf) g1 -= r.fl * jv;
-        else if (x >= Rf) g1 += r.fl * jv;
-        else { g1 += r.Df * x * jv; g2 += r.Df * jv * jv; }
-      }
-      if (r.hlo) {
-        float x = r.jlo + alpha * jv;
-        if (x < 0.f) { g1 += r.Dlo * x * jv; g2 += r.Dlo * jv * jv; }
-      }
-      if (r.hhi) {
-        float x = r.jhi - alpha * jv;
-        if (x < 0.f) { g1 += r.Dhi * x * (-jv); g2 += r.Dhi * jv * jv; }
-      }
+    const float jv = c.l < NV ? search : 0.f;
+    {
+      const float x = r.jf + alpha * jv, Rf = r.Rf * r.fl;
+      const bool lo = x <= -Rf, hi = x >= Rf;
+      g1 += r.hf ? (lo ? -(r.fl * jv) : (hi ? r.fl * jv : r.Df * x * jv)) : 0.f;
+      g2 += (r.hf && !lo && !hi) ? r.Df * jv * jv : 0.f;
+    }
+    {
+      const float x = r.jlo + alpha * jv;
+      const bool on = r.hlo && x < 0.f;
+      g1 += on ? r.Dlo * x * jv : 0.f;
+      g2 += on ? r.Dlo * jv * jv : 0.f;
+    }
+    {
+      const float x = r.jhi - alpha * jv;
+      const bool on = r.hhi && x < 0.f;
+      g1 += on ? r.Dhi * x * (-jv) : 0.f;
+      g2 += on ? r.Dhi * jv * jv : 0.f;
     }
     float gg[2] = {g1, g2};
     tsum_n<2>(gg);
