@@ -1048,18 +1048,21 @@ __device__ __forceinline__ float rne_project(const Ctx& c, const BodyK& B, const
 /* --------------------------- constraint model ------------------------------ */
 template <typename PS>
 __device__ __forceinline__ float impedance(PS si, float xabs) {
-  float dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
-  float imp;
-  if (width <= MINVAL || xabs >= width) {
-    imp = dmax;
+  const float dmin = si[0], dmax = si[1], width = si[2], mid = si[3], power = si[4];
+  /* mj_makeImpedance; branch-free in the per-lane distance, the power is a
+     model constant (uniform branch; 2 is MuJoCo's default, without powf) */
+  const bool sat = width <= MINVAL || xabs >= width;
+  const float x = sat ? 0.f : xabs / width;
+  float y;
+  if (power == 1.f) {
+    y = x;
+  } else if (power == 2.f) {
+    const float ylo = x * x / mid, yhi = 1.f - (1.f - x) * (1.f - x) / (1.f - mid);
+    y = x <= mid ? ylo : yhi;
   } else {
-    float x = xabs / width, y;
-    if (power == 1.f) y = x;
-    else if (power == 2.f) y = x <= mid ? x * x / mid : 1.f - (1.f - x) * (1.f - x) / (1.f - mid); /* MuJoCo default */
-    else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
-    else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
-    imp = dmin + y * (dmax - dmin);
+    y = x <= mid ? powf(x, power) / powf(mid, power - 1.f) : 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
   }
+  const float imp = sat ? dmax : dmin + y * (dmax - dmin);
   return fminf(fmaxf(imp, MINIMP), MAXIMP);
 }
 template <typename PR, typename PS>
@@ -1178,24 +1181,28 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   r.Rf = 0.f;
   r.fl = 0.f;
   if (l < NV) {
-    float v = ls.v;
-    float dA = m->dof_invweight0[l];
-    if (c.L->par[P_FLOSS][c.l] > 0.f) {
-      r.hf = true;
-      r.fl = c.L->par[P_FLOSS][c.l];
-      row_params(m->dof_solref, m->dof_solimp, 0.f, dA, v, cfg->dt, r.Df, r.Rf, r.af);
-    }
-    if (m->dof_limited[l]) {
-      float dlo = ls.q - m->dof_range[l][0], dhi = m->dof_range[l][1] - ls.q, Rt;
-      if (dlo < 0.f) {
-        r.hlo = true;
-        row_params(m->dof_solref, m->dof_solimp, dlo, dA, v, cfg->dt, r.Dlo, Rt, r.alo);
-      }
-      if (dhi < 0.f) {
-        r.hhi = true;
-        row_params(m->dof_solref, m->dof_solimp, dhi, dA, -v, cfg->dt, r.Dhi, Rt, r.ahi);
-      }
-    }
+    /* frictionloss and both joint-limit rows evaluated for every dof lane,
+       kept where they exist (no per-lane branches) */
+    const float v = ls.v;
+    const float dA = m->dof_invweight0[l];
+    const float floss = c.L->par[P_FLOSS][c.l];
+    const bool lim = m->dof_limited[l] != 0;
+    const float dlo = ls.q - m->dof_range[l][0], dhi = m->dof_range[l][1] - ls.q;
+    float D0, R0, a0, D1, R1, a1, D2, R2, a2;
+    row_params(m->dof_solref, m->dof_solimp, 0.f, dA, v, cfg->dt, D0, R0, a0);
+    row_params(m->dof_solref, m->dof_solimp, dlo, dA, v, cfg->dt, D1, R1, a1);
+    row_params(m->dof_solref, m->dof_solimp, dhi, dA, -v, cfg->dt, D2, R2, a2);
+    r.hf = floss > 0.f;
+    r.fl = r.hf ? floss : 0.f;
+    r.Df = r.hf ? D0 : 0.f;
+    r.Rf = r.hf ? R0 : 0.f;
+    r.af = r.hf ? a0 : 0.f;
+    r.hlo = lim && dlo < 0.f;
+    r.Dlo = r.hlo ? D1 : 0.f;
+    r.alo = r.hlo ? a1 : 0.f;
+    r.hhi = lim && dhi < 0.f;
+    r.Dhi = r.hhi ? D2 : 0.f;
+    r.ahi = r.hhi ? a2 : 0.f;
   }
   tsync();
 }
