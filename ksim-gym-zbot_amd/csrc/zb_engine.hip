@@ -519,18 +519,21 @@ __device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
       live = nl;
     }
   }
+  /* the base (the one branching body) adds its children's chain sums: one
+     batched team reduction instead of a gather loop */
+  {
+    const bool bchild = c.l >= 2 && c.l < NB && c.bpar == 1;
+    float w[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) w[i] = bchild ? v[i] : 0.f;
+    tsum_n<K>(w);
+    if (c.l == 1) {
+#pragma unroll
+      for (int i = 0; i < K; i++) v[i] += w[i];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < K; i++) L->sub[c.l][i] = v[i];
-  tsync();
-  if (c.l == 1) {
-    for (int k = 0; k < c.nch; k++) {
-      const int ch = childof(c, k);
-#pragma unroll
-      for (int i = 0; i < K; i++) v[i] += L->sub[ch][i];
-    }
-#pragma unroll
-    for (int i = 0; i < K; i++) L->sub[1][i] = v[i];
-  }
   tsync();
 }
 
