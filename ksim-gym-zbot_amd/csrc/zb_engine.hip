@@ -130,13 +130,25 @@ __device__ __forceinline__ uint32_t xor16(uint32_t v) {
   return (threadIdx.x & 16) ? r[0] : r[1];
 }
 __device__ __forceinline__ float xor16f(float v) { return __uint_as_float(xor16(__float_as_uint(v))); }
+/* the two 16-lane rows of each team, broadcast: r[0] = row 0's value, r[1] =
+   row 1's, in every lane. A symmetric combine of the pair needs no select. */
+__device__ __forceinline__ void rows2(float v, float& a, float& b) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ int rows2max(int v) {
+  auto r = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  return max((int)r[0], (int)r[1]);
+}
 __device__ __forceinline__ float tsum(float v) {
   v += dppf<0xB1>(v);
   v += dppf<0x4E>(v);
   v += dppf<0x141>(v);
   v += dppf<0x140>(v);
-  v += xor16f(v);
-  return v;
+  float a, b;
+  rows2(v, a, b);
+  return a + b;
 }
 /* N independent team sums, stage by stage so the DPP/permlane steps of
    different values interleave (bit-identical to N separate tsum calls) */
@@ -151,23 +163,27 @@ __device__ __forceinline__ void tsum_n(float v[N]) {
 #pragma unroll
   for (int i = 0; i < N; i++) v[i] += dppf<0x140>(v[i]);
 #pragma unroll
-  for (int i = 0; i < N; i++) v[i] += xor16f(v[i]);
+  for (int i = 0; i < N; i++) {
+    float a, b;
+    rows2(v[i], a, b);
+    v[i] = a + b;
+  }
 }
 __device__ __forceinline__ float tmaxf(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
   v = fmaxf(v, dppf<0x141>(v));
   v = fmaxf(v, dppf<0x140>(v));
-  v = fmaxf(v, xor16f(v));
-  return v;
+  float a, b;
+  rows2(v, a, b);
+  return fmaxf(a, b);
 }
 __device__ __forceinline__ int tmaxi(int v) {
   v = max(v, dppi<0xB1>(v));
   v = max(v, dppi<0x4E>(v));
   v = max(v, dppi<0x141>(v));
   v = max(v, dppi<0x140>(v));
-  v = max(v, (int)xor16((uint32_t)v));
-  return v;
+  return rows2max(v);
 }
 __device__ __forceinline__ void tsync() { __syncthreads(); }
 /* bitmask over the team's lanes of predicate p */

@@ -42,7 +42,7 @@ def main():
         open(os.path.join(d, "zb_engine.hip"), "w").write(src)
         open(os.path.join(d, "zb_internal.h"), "w").write(hdr)
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{d}", f"-I{ROOT}/include",
-               "-fno-signed-zeros", "-freciprocal-math", "-fno-math-errno", "-fapprox-func", "-DZB_STAMPS", "-shared",
+               "-fno-signed-zeros", "-freciprocal-math", "-fno-math-errno", "-fapprox-func", "-fno-slp-vectorize", "-DZB_STAMPS", "-shared",
                "-o", out, os.path.join(d, "zb_engine.hip"), os.path.join(CSRC, "zb_capi.cpp")]
         # zb_capi.cpp must see the patched header: compile it from the temp dir copy
         capi = open(os.path.join(CSRC, "zb_capi.cpp")).read()
