@@ -712,34 +712,38 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
     st_row(&L->L[c.l][0], X);
     L->Dk[c.l] = Xd;
   }
-  /* limb levels (height inside the chain, leaves first): the pivot of each
-     chain divides its row; every shallower lane of the chain pulls that row
-     with ds_bpermute (no LDS round trip) and applies its Schur update */
-  const int nlv = NLIMBLV;
-  for (int lv = 0; lv < nlv; lv++) {
-    const int q = c.cln - 1 - lv; /* chain position of this level's pivot */
-    if (ischain && q == c.cps) {
-      const float Dkv = fmaxf(Xd, MINVAL);
-      const float inv = 1.0f / Dkv;
+  /* limb levels by chain position q = NLIMBLV-1 .. 1 (leaves first; chains
+     shorter than q+1 idle): every shallower lane of a chain pulls the pivot's
+     unscaled row with ds_bpermute (only the NROOT+q entries a receiver uses),
+     scales by 1/D_k itself (mj_factorI order: update with A(k,j)/D_k, divide
+     the pivot row afterwards) and applies its Schur update. Position 0 has no
+     receivers inside the chain. */
+  const int cps = vopq(c.cps);
 #pragma unroll
-      for (int e = 0; e < CAP; e++) X[e] = X[e] * inv;
-      Xd = Dkv;
-    }
-    const bool has = ischain && q > c.cps;
+  for (int q = NLIMBLV - 1; q >= 1; q--) {
+    const bool has = ischain && cps < q && q < c.cln;
     const int src = has ? c.chd + q : c.l;
-    float r[CAP];
+    float r[NROOT + NLIMBLV];
 #pragma unroll
-    for (int e = 0; e < CAP; e++) r[e] = tsh(X[e], src);
+    for (int e = 0; e < NROOT + q; e++) r[e] = tsh(X[e], src);
     const float dk = tsh(Xd, src);
-    if (has) {
-      float lk = 0.f; /* L(k, j) = r[depth(j)] */
+    /* A(k, j) = r[depth(j)], depth(j) = NROOT + cps, cps < q */
+    float t = r[NROOT];
 #pragma unroll
-      for (int e = 0; e < CAP; e++) lk = e == ddep ? r[e] : lk;
-      const float t = lk * dk; /* A(k, j) after k's subtree */
-      Xd -= t * lk;
+    for (int p = 1; p < q; p++) t = cps == p ? r[NROOT + p] : t;
+    const float sc = has ? t / fmaxf(dk, MINVAL) : 0.f;
+    Xd -= sc * t;
 #pragma unroll
-      for (int e = 0; e < CAP; e++) X[e] -= (e < ddep ? t : 0.f) * r[e];
-    }
+    for (int e = 0; e < NROOT; e++) X[e] -= sc * r[e];
+#pragma unroll
+    for (int e = NROOT; e < NROOT + q - 1; e++) X[e] -= (e < ddep ? sc : 0.f) * r[e];
+  }
+  if (ischain) {
+    const float Dkv = fmaxf(Xd, MINVAL);
+    const float inv = 1.0f / Dkv;
+#pragma unroll
+    for (int e = 0; e < CAP; e++) X[e] = X[e] * inv;
+    Xd = Dkv;
   }
   if (ischain) {
     st_row(&L->L[c.l][0], X);
@@ -827,11 +831,12 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   const bool ischain = c.chd >= 0;
   /* forward pass along the limbs (leaves first): pull the pivot's final x */
   const int nlv = NLIMBLV;
-  for (int lv = 0; lv < nlv; lv++) {
-    const int q = c.cln - 1 - lv;
-    const bool has = ischain && q > c.cps;
+  const int cps = vopq(c.cps);
+#pragma unroll
+  for (int q = NLIMBLV - 1; q >= 1; q--) {
+    const bool has = ischain && cps < q && q < c.cln;
     const int src = has ? c.chd + q : c.l;
-    const float lk = L->L[has ? src : c.l][ddep];
+    const float lk = L->L[src][ddep];
     const float xk = tsh(x, src);
     if (has) x -= lk * xk;
   }
