@@ -1290,10 +1290,8 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
     r.fhi = r.hhi ? f3 : r.fhi;
     r.acthi = r.hhi ? a3 : r.acthi;
   }
-  if (r.ex) {
-    L->rowF[c.l] = r.f;
-    L->rowDA[c.l] = r.act ? r.D : 0.f;
-  }
+  if (r.ex) L->rowF[c.l] = r.f;
+  L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
   /* J'f per dof: the 16 contact rows of a foot are one 16-lane DPP row and
      share the foot's dof chain, so sum_r J_r[e] f_r (e = chain position) is
      a row reduction for all 12 positions at once (interleaved DPP, no LDS);
@@ -1336,6 +1334,47 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
   return tsum(cost);
 }
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+/* G_f = sum_{r in foot f} D_r J_r J_r' (depth-indexed 12x12) for both feet of
+ * both envs of the wave on the matrix cores: per (env, foot) four
+ * v_mfma_f32_16x16x4_f32 over the foot's 16 contact rows (K = 4 rows each;
+ * lane l supplies row 4*chunk + l/16, entry l%16). Staged in the env's L[][]
+ * as [foot][12][12]; L[][] is free until factor_ldl writes it. D is rowDA
+ * (0 for absent / inactive rows). Wave-uniform: call with every lane active. */
+__device__ __forceinline__ void jdj_mfma() {
+  const int l = threadIdx.x & 63;
+  const int e = l & 15, k = l >> 4;
+  const int ec = e < CAP ? e : CAP - 1;
+  v4f acc[NTEAM][NGEOM];
+#pragma unroll
+  for (int t = 0; t < NTEAM; t++)
+#pragma unroll
+    for (int f = 0; f < NGEOM; f++) acc[t][f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < 4; ch++)
+#pragma unroll
+    for (int t = 0; t < NTEAM; t++)
+#pragma unroll
+      for (int f = 0; f < NGEOM; f++) {
+        const int r = 16 * f + 4 * ch + k;
+        const float jv = g_lds[t].u.J[r][ec];
+        const float dv = g_lds[t].rowDA[r];
+        const bool on = dv != 0.f && e < CAP;
+        const float a = on ? dv * jv : 0.f, b = on ? jv : 0.f;
+        acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t][f], 0, 0, 0);
+      }
+  /* lane l holds G[4*(l/16) + v][l%16] */
+#pragma unroll
+  for (int t = 0; t < NTEAM; t++)
+#pragma unroll
+    for (int f = 0; f < NGEOM; f++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        const int i = 4 * k + v;
+        if (i < CAP && e < CAP) (&g_lds[t].L[0][0])[f * CAP * CAP + i * CAP + e] = acc[t][f][v];
+      }
+}
+
 /* H = M + J' D_active J rows (depth-indexed), then factor -> Dinv */
 /* H = M + J' D_active J (depth-indexed rows), then factor -> 1/D_j.
  * full: from M and every active contact row. Otherwise the stored unfactored
@@ -1350,7 +1389,20 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
   uint32_t tb;
   if (full) {
     Hd = load_mrow(c, H);
-    tb = r.exmask & c.rowmask; /* rowDA (written by update_constraint) holds D or 0 */
+    tb = 0u;
+    jdj_mfma();
+    tsync();
+    if (c.l < NV) {
+      const float* G = &L->L[0][0] + ddep * CAP;
+      const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
+      float g0[CAP], g1[CAP];
+      ld_row(G, g0);
+      ld_row(G + CAP * CAP, g1);
+      const float d0 = G[ddep], d1 = G[CAP * CAP + ddep];
+#pragma unroll
+      for (int e = 0; e < CAP; e++) H[e] += e < ddep ? (f0 ? g0[e] : 0.f) + (f1 ? g1[e] : 0.f) : 0.f;
+      Hd += (f0 ? d0 : 0.f) + (f1 ? d1 : 0.f);
+    }
   } else {
     ld_row(&L->Hs[c.l][0], H);
     Hd = L->Hs[c.l][CAP];
@@ -1461,7 +1513,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
 }
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
-__device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters) {
+__device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters,
+                                              bool live) {
   CP cfg = c.cfg;
   MP m = c.m;
   EnvL* L = c.L;
@@ -1497,7 +1550,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
   int it = 0;
-  while (it < cfg->iterations) {
+  while (live && it < cfg->iterations) {
     float Mv;
     STAMP(S_CHECK);
     float alpha = line_search(c, r, search, Ma, fs, Mv);
@@ -1608,10 +1661,17 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   STAMP(S_CON);
   int nrows = tmaxi(r.nrow + (r.hf || r.hlo || r.hhi ? 1 : 0));
   float qacc;
-  if (nrows == 0) {
-    qacc = qs;
-  } else {
-    qacc = solve_newton(c, r, qs, fs, ls.w, iters);
+  /* entered by the whole wave when either env has rows (the full Hessian
+     build runs on the matrix cores and needs every lane); an env without
+     rows leaves the Newton loop at once and keeps qacc_smooth */
+  qacc = qs;
+  if (__ballot(nrows > 0) != 0ull) {
+    int it2 = 0;
+    const float qn = solve_newton(c, r, qs, fs, ls.w, it2, nrows > 0);
+    if (nrows > 0) {
+      qacc = qn;
+      iters += it2;
+    }
   }
   ls.qacc = (c.l < NV) ? qacc : 0.f;
   STAMP(S_CHECK);
