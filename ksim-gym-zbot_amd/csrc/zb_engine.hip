@@ -928,12 +928,15 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
     float sr = 0.f;
 #pragma unroll
     for (int i = 0; i < RMAX; i++) sr = j == i ? si[i] : sr;
-    if (j < nroot) {
+    /* deeper root dofs: all loads in flight, masked */
+    const int jr = j < nroot ? j : 0;
+    float yr = 0.f;
 #pragma unroll
-      for (int k = 1; k < RMAX; k++)
-        if (k < nroot && k > j) y += L->M[k][j] * L->vec[slot][k];
-      y += sr;
+    for (int k = 1; k < RMAX; k++) {
+      const float mk = L->M[k][jr] * L->vec[slot][k];
+      yr += (k < nroot && k > j) ? mk : 0.f;
     }
+    if (j < nroot) y += yr + sr;
   }
   tsync();
   return y;
