@@ -60,6 +60,70 @@ def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int = 256) -> 
     }
 
 
+def bench_ppo_inputs(n: int, T: int, reps: int, dev, world: int) -> dict:
+    """Post-rollout PPO inputs over a [T, n] rollout resident in HBM:
+    zb_gae (GAE reverse scan + value targets + moment partials), the moment tree, the
+    cross-rank combine (RCCL all_gather when world > 1) and zb_adv_normalize."""
+    import ctypes as C  # noqa: PLC0415
+
+    import torch  # noqa: PLC0415
+    from zbot_amd import ppo as P  # noqa: PLC0415
+    from zbot_amd.metrics import HBM_PEAK_GBS  # noqa: PLC0415
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    rew = torch.randn(T, n, device=dev, generator=g)
+    val = torch.randn(T, n, device=dev, generator=g)
+    done = (torch.rand(T, n, device=dev, generator=g) < 0.01).to(torch.uint8)
+    L = P.load_library()
+    gae = torch.empty(T, n, device=dev)
+    vt = torch.empty(T, n, device=dev)
+    part = torch.empty(int(L.zb_gae_partials_words(n)), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def gae_only():
+        rc = L.zb_gae(rew.data_ptr(), val.data_ptr(), done.data_ptr(), None, None, T, n, C.c_float(P.DEFAULT_GAMMA),
+                      C.c_float(P.DEFAULT_LAMBDA), gae.data_ptr(), vt.data_ptr(), part.data_ptr(), None, sp)
+        assert rc == 0
+
+    for _ in range(3):
+        gae_only()
+        P.compute_ppo_inputs(val, rew, done)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        gae_only()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    gae_ms = sum(a.elapsed_time(b) for a, b in ev) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = P.compute_ppo_inputs(val, rew, done)
+    torch.cuda.synchronize(dev)
+    full_ms = (time.perf_counter() - t0) * 1e3 / reps
+    bpu = 17  # per (t, env): reward 4 + value 4 + done 1 read; gae 4 + value target 4 written
+    achieved = bpu * T * n / (gae_ms * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic_gae.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("envs") == n and tj.get("T") == T:
+            traffic = tj.get("hbm_bytes_per_launch")
+    assert torch.isfinite(out.advantages_t).all()
+    return {
+        "workload": f"GAE + value targets + global advantage normalization over a [{T}, {n}] rollout per GPU "
+                    f"(x{world} ranks, moments combined over RCCL)",
+        "gae_kernel_ms": gae_ms,
+        "compute_ppo_inputs_ms": full_ms,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "zb::gae_kernel",
+                     "algorithmic_bytes_per_unit": bpu, "unit_note": "one (step, env) element"},
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,6 +134,7 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-baseline-sec", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
     args = ap.parse_args()
 
     import torch  # noqa: PLC0415
@@ -154,6 +219,8 @@ def main() -> None:
             traffic = tj.get("hbm_bytes_per_launch")
             flop_per_env_step = tj.get("issued_fp32_flop_per_env_step")
 
+    ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
+
     if rank == 0:
         value = world * n * args.steps / elapsed
         out = {
@@ -204,6 +271,8 @@ def main() -> None:
                 "mean_return": float((total_stats[0] / total_stats[2].clamp(min=1)).item()),
             },
         }
+        if ppo_leg is not None:
+            out["ppo_inputs"] = ppo_leg
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper())
         print(json.dumps(out), flush=True)

@@ -351,6 +351,65 @@ int zb_debug_forward(ZbHandle* h, float* state_dev, const float* ctrl_dev, float
   return ZB_OK;
 }
 
+/* ---- post-rollout PPO inputs (include/zbot_ppo.h) ---- */
+
+size_t zb_gae_partials_words(int n) {
+  return n > 0 ? 2 * (size_t)((n + ZB_GAE_ENVS_PER_BLOCK - 1) / ZB_GAE_ENVS_PER_BLOCK) : 0;
+}
+
+int zb_gae(const float* reward, const float* values, const uint8_t* done, const uint8_t* success,
+           const float* bootstrap, int T, int n, float gamma, float lam, float* gae_out, float* value_targets,
+           double* partials, double* moments_out, void* stream) {
+  if (T < 0 || n < 0) return fail(ZB_EARG, "zb_gae: negative size (T=%d n=%d)", T, n);
+  if (moments_out && !partials) return fail(ZB_EARG, "zb_gae: moments_out needs the partials scratch");
+  if ((size_t)zb_gae_partials_words(n) / 2 > (size_t)1024 * 1024)
+    return fail(ZB_EARG, "zb_gae: n=%d exceeds the moment tree (%d envs)", n, 1024 * 1024 * ZB_GAE_ENVS_PER_BLOCK);
+  if (T == 0 || n == 0) {
+    if (moments_out) HIPCHK(hipMemsetAsync(moments_out, 0, 2 * sizeof(double), (hipStream_t)stream));
+    return ZB_OK;
+  }
+  if (!reward || !values || !done || !gae_out) return fail(ZB_EARG, "zb_gae: null input/output pointer");
+  zb::GaeArgs a;
+  a.reward = reward;
+  a.values = values;
+  a.done = done;
+  a.success = success;
+  a.bootstrap = bootstrap;
+  a.T = T;
+  a.n = n;
+  a.gamma = gamma;
+  a.gl = gamma * lam;
+  a.gae = gae_out;
+  a.vtarget = value_targets;
+  a.partials = partials;
+  hipError_t e = zb::launch_gae(a, moments_out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_gae launch: %s", hipGetErrorString(e));
+  return ZB_OK;
+}
+
+int zb_moments_combine(const double* moments, int k, double* out, void* stream) {
+  if (!out || k < 0 || (k > 0 && !moments)) return fail(ZB_EARG, "zb_moments_combine: bad argument");
+  if (k > 1024 * 1024) return fail(ZB_EARG, "zb_moments_combine: k=%d > %d", k, 1024 * 1024);
+  if (k == 0) {
+    HIPCHK(hipMemsetAsync(out, 0, 2 * sizeof(double), (hipStream_t)stream));
+    return ZB_OK;
+  }
+  hipError_t e = zb::launch_moments(moments, k, out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_moments_combine launch: %s", hipGetErrorString(e));
+  return ZB_OK;
+}
+
+int zb_adv_normalize(const float* gae, float* advantages, long long count, const double* moments, double total,
+                     float eps, void* stream) {
+  if (count < 0) return fail(ZB_EARG, "zb_adv_normalize: negative count");
+  if (count == 0) return ZB_OK;
+  if (!gae || !advantages || !moments) return fail(ZB_EARG, "zb_adv_normalize: null pointer");
+  if (!(total > 0.0)) return fail(ZB_EARG, "zb_adv_normalize: total must be > 0");
+  hipError_t e = zb::launch_normalize(gae, advantages, count, moments, total, eps, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_adv_normalize launch: %s", hipGetErrorString(e));
+  return ZB_OK;
+}
+
 #ifdef ZB_STAMPS
 int zb_get_stamps(ZbHandle* h, void* out_dev, void* stream) {
   if (!h || !h->stamps) return fail(ZB_EARG, "no stamps");

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "zbot.h"
+#include "zbot_ppo.h"
 
 /* debug forward dump layout (zb_debug_forward), fp32 words per env */
 #define ZB_DBG_QM      0     /* [nv*nv] dense symmetric mass matrix */
@@ -50,6 +51,27 @@ struct StepArgs {
 hipError_t launch_step(const StepArgs& a, hipStream_t s);
 hipError_t launch_reset(const StepArgs& a, hipStream_t s);
 hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s);
+
+/* post-rollout PPO inputs (zb_ppo.hip, include/zbot_ppo.h) */
+struct GaeArgs {
+  const float* reward;      /* [T, n] */
+  const float* values;      /* [T, n] */
+  const uint8_t* done;      /* [T, n] */
+  const uint8_t* success;   /* [T, n] or null */
+  const float* bootstrap;   /* [n] or null */
+  int T;
+  int n;
+  float gamma;
+  float gl;                 /* gamma * lam, rounded once as the reference does */
+  float* gae;               /* [T, n] */
+  float* vtarget;           /* [T, n] or null */
+  double* partials;         /* [ceil(n / ZB_GAE_ENVS_PER_BLOCK)][2] or null */
+};
+
+hipError_t launch_gae(const GaeArgs& a, double* moments_out, hipStream_t s);
+hipError_t launch_moments(const double* in, int k, double* out, hipStream_t s);
+hipError_t launch_normalize(const float* gae, float* adv, long long count, const double* mom, double total,
+                            float eps, hipStream_t s);
 
 }  // namespace zb
 

@@ -66,6 +66,14 @@ def load_library(path: str | None = None) -> C.CDLL:
     for f in ("zb_create", "zb_destroy", "zb_reset", "zb_step", "zb_rollout", "zb_get_state", "zb_set_state",
               "zb_get_rand", "zb_set_rand", "zb_get_stats", "zb_get_solver_iters", "zb_debug_forward"):
         getattr(L, f).restype = C.c_int
+    # post-rollout PPO inputs (include/zbot_ppo.h)
+    L.zb_gae_partials_words.argtypes = [C.c_int]
+    L.zb_gae_partials_words.restype = C.c_size_t
+    L.zb_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_float, vp, vp, vp, vp, vp]
+    L.zb_moments_combine.argtypes = [vp, C.c_int, vp, vp]
+    L.zb_adv_normalize.argtypes = [vp, vp, C.c_longlong, vp, C.c_double, C.c_float, vp]
+    for f in ("zb_gae", "zb_moments_combine", "zb_adv_normalize"):
+        getattr(L, f).restype = C.c_int
     if L.zb_model_struct_bytes() != C.sizeof(cs.ZbModel):
         raise ZbError("ZbModel layout mismatch between cstructs.py and the library")
     if L.zb_config_struct_bytes() != C.sizeof(cs.ZbEnvConfig):

@@ -18,7 +18,7 @@ _LIBS: dict[str, C.CDLL] = {}
 
 def build(force: bool = False) -> None:
     """Compile the oracle libraries with the committed Makefile."""
-    targets = [os.path.join(HERE, "liboracle_zbot.so"), os.path.join(HERE, "liboracle_zbot_f64.so")]
+    targets = [os.path.join(HERE, n) for n in ("liboracle_zbot.so", "liboracle_zbot_f64.so", "liboracle_ppo.so")]
     if force or not all(os.path.exists(t) for t in targets):
         subprocess.run(["make", "-C", HERE, "-s"], check=True)
 
@@ -168,3 +168,51 @@ def simulate(cmodel, cfg, qpos, qvel, nsteps: int, ctrl=None, qaccw=None, precis
     ctrl = None if ctrl is None else np.ascontiguousarray(ctrl, dtype=np.float32)
     lib(precision).zbo_simulate(C.byref(cmodel), C.byref(cfg), _p(qpos), _p(qvel), _p(qaccw), _p(ctrl), nsteps)
     return qpos, qvel, qaccw
+
+
+# ---- post-rollout PPO inputs (zb_oracle_ppo.c) ----
+
+def ppo_lib() -> C.CDLL:
+    if "ppo" in _LIBS:
+        return _LIBS["ppo"]
+    path = os.path.join(HERE, "liboracle_ppo.so")
+    if not os.path.exists(path):
+        build()
+    L = C.CDLL(path)
+    fp, u8p, dp = C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.POINTER(C.c_double)
+    L.zbo_gae.argtypes = [fp, fp, u8p, u8p, fp, C.c_int, C.c_int, C.c_float, C.c_float, fp, fp, dp]
+    L.zbo_moments_tree.argtypes = [dp, C.c_int, dp]
+    L.zbo_adv_normalize.argtypes = [fp, fp, C.c_longlong, dp, C.c_double, C.c_float]
+    _LIBS["ppo"] = L
+    return L
+
+
+def gae(reward, values, done, gamma: float, lam: float, success=None, bootstrap=None):
+    """Serial reverse-scan GAE over [T, n] arrays -> (gae, value_targets, per-env moments [n, 2])."""
+    f32 = lambda x: None if x is None else np.ascontiguousarray(x, dtype=np.float32)  # noqa: E731
+    u8 = lambda x: None if x is None else np.ascontiguousarray(x, dtype=np.uint8)  # noqa: E731
+    reward, values, bootstrap = f32(reward), f32(values), f32(bootstrap)
+    done, success = u8(done), u8(success)
+    T, n = reward.shape
+    g = np.zeros((T, n), np.float32)
+    vt = np.zeros((T, n), np.float32)
+    mom = np.zeros((n, 2), np.float64)
+    ppo_lib().zbo_gae(_p(reward), _p(values), _p(done, C.c_uint8), _p(success, C.c_uint8), _p(bootstrap), T, n,
+                      gamma, lam, _p(g), _p(vt), _p(mom, C.c_double))
+    return g, vt, mom
+
+
+def moments_tree(pairs) -> np.ndarray:
+    """Pairwise tree over [k, 2] (sum, sum^2) rows, zero-padded to a power of two."""
+    p = np.ascontiguousarray(pairs, dtype=np.float64).reshape(-1, 2)
+    out = np.zeros(2, np.float64)
+    ppo_lib().zbo_moments_tree(_p(p, C.c_double), p.shape[0], _p(out, C.c_double))
+    return out
+
+
+def adv_normalize(g, moments, total: float, eps: float = 1e-6) -> np.ndarray:
+    g = np.ascontiguousarray(g, dtype=np.float32)
+    out = np.zeros_like(g)
+    m = np.ascontiguousarray(moments, dtype=np.float64)
+    ppo_lib().zbo_adv_normalize(_p(g), _p(out), g.size, _p(m, C.c_double), float(total), eps)
+    return out

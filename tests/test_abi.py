@@ -35,13 +35,17 @@ def test_every_field_offset_matches_c(oracle_mod, which, cls):
 
 
 def _declared_symbols():
-    txt = open(os.path.join(ROOT, "include", "zbot.h")).read()
-    return sorted(set(re.findall(r"\b(zb_[a-z_]+)\s*\(", txt)))
+    syms = set()
+    for h in ("zbot.h", "zbot_ppo.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        syms |= set(re.findall(r"\b(zb_[a-z_]+)\s*\(", txt))
+    return sorted(syms)
 
 
 def test_library_exports_every_declared_symbol(hiplib):
     syms = _declared_symbols()
-    assert len(syms) >= 15
+    assert len(syms) >= 19
+    assert {"zb_gae", "zb_moments_combine", "zb_adv_normalize", "zb_gae_partials_words"} <= set(syms)
     for s in syms:
         assert hasattr(hiplib, s), f"libzbot_hip.so does not export {s}"
 
