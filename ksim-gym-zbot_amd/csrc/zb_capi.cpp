@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "zb_internal.h"
 
@@ -408,6 +409,153 @@ int zb_adv_normalize(const float* gae, float* advantages, long long count, const
   hipError_t e = zb::launch_normalize(gae, advantages, count, moments, total, eps, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_adv_normalize launch: %s", hipGetErrorString(e));
   return ZB_OK;
+}
+
+/* ---- GRU policy / value networks (include/zbot_policy.h) ---- */
+
+struct ZbPolicy {
+  int kind;
+  int device;
+  float* wpack;
+  float* bias;
+};
+
+static int pol_in(int kind) { return kind == ZB_POL_ACTOR ? ZB_POL_ACTOR_IN : ZB_POL_CRITIC_IN; }
+static int pol_out(int kind) { return kind == ZB_POL_ACTOR ? ZB_POL_ACTOR_OUT : 1; }
+
+size_t zb_policy_param_count(int kind) {
+  if (kind != ZB_POL_ACTOR && kind != ZB_POL_CRITIC) return 0;
+  const size_t H = ZB_POL_HIDDEN, D = ZB_POL_DEPTH, I = (size_t)pol_in(kind), O = (size_t)pol_out(kind);
+  return H * I + H + D * (6 * H * H + 4 * H) + O * H + O + (kind == ZB_POL_ACTOR ? ZB_POL_JOINTS : 0);
+}
+
+/* W [N][K] (natural layout) -> matrix-core B fragments [ceil(N/32)][ceil(K/8)][64][4]:
+   element u of lane l in k-group g of tile t is W[32t + (l & 31)][8g + 2u + (l >> 5)]
+   (zero outside W), so a lane reads 4 consecutive MFMA k-steps with one 16-B load */
+static void pack_b(const float* W, int N, int K, std::vector<float>& out) {
+  const int NT = (N + 31) / 32, G = (K + 7) / 8;
+  for (int t = 0; t < NT; t++)
+    for (int g = 0; g < G; g++)
+      for (int l = 0; l < 64; l++)
+        for (int u = 0; u < 4; u++) {
+          const int row = 32 * t + (l & 31), k = 8 * g + 2 * u + (l >> 5);
+          out.push_back(row < N && k < K ? W[(size_t)row * K + k] : 0.f);
+        }
+}
+
+int zb_policy_create(int kind, const float* params, size_t n_params, int device, ZbPolicy** out) {
+  if (!out || !params) return fail(ZB_EARG, "zb_policy_create: null argument");
+  *out = nullptr;
+  if (kind != ZB_POL_ACTOR && kind != ZB_POL_CRITIC) return fail(ZB_EARG, "zb_policy_create: unknown kind %d", kind);
+  const size_t need = zb_policy_param_count(kind);
+  if (n_params != need) return fail(ZB_EARG, "zb_policy_create: %zu parameters, expected %zu", n_params, need);
+  const int H = ZB_POL_HIDDEN, D = ZB_POL_DEPTH, I = pol_in(kind), O = pol_out(kind);
+  std::vector<float> wp, bias;
+  const float* p = params;
+  pack_b(p, H, I, wp); /* input_proj.weight */
+  p += (size_t)H * I;
+  bias.insert(bias.end(), p, p + H); /* input_proj.bias */
+  p += H;
+  for (int l = 0; l < D; l++) {
+    pack_b(p, 3 * H, H, wp); /* weight_ih */
+    p += (size_t)3 * H * H;
+    pack_b(p, 3 * H, H, wp); /* weight_hh */
+    p += (size_t)3 * H * H;
+    bias.insert(bias.end(), p, p + 4 * H); /* bias [3H], bias_n [H] */
+    p += 4 * H;
+  }
+  const float* wout = p;
+  p += (size_t)O * H;
+  bias.insert(bias.end(), p, p + O); /* output_proj.bias */
+  p += O;
+  if (kind == ZB_POL_ACTOR) {
+    pack_b(wout, O, H, wp);
+    bias.insert(bias.end(), p, p + ZB_POL_JOINTS); /* mean offsets (JOINT_BIASES) */
+  } else {
+    bias.insert(bias.end(), wout, wout + H); /* value head, natural layout */
+  }
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(ZB_EDEVICE, "device %d not available (%d devices)", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  ZbPolicy* h = new ZbPolicy();
+  h->kind = kind;
+  h->device = device;
+  h->wpack = nullptr;
+  h->bias = nullptr;
+  hipError_t e = hipMalloc(&h->wpack, wp.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(&h->bias, bias.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(h->wpack, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(h->bias, bias.data(), bias.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    zb_policy_destroy(h);
+    return fail(ZB_EDEVICE, "zb_policy_create: %s", hipGetErrorString(e));
+  }
+  *out = h;
+  return ZB_OK;
+}
+
+int zb_policy_destroy(ZbPolicy* h) {
+  if (!h) return ZB_OK;
+  (void)hipSetDevice(h->device);
+  if (h->wpack) (void)hipFree(h->wpack);
+  if (h->bias) (void)hipFree(h->bias);
+  delete h;
+  return ZB_OK;
+}
+
+static int policy_run(ZbPolicy* h, int kind, const float* obs, int T, int n, float* carry, const uint8_t* reset,
+                      int mode, uint64_t seed, int env_offset, uint32_t step0, float* actions, float* log_prob,
+                      float* value, void* stream) {
+  if (!h) return fail(ZB_EARG, "null policy handle");
+  if (h->kind != kind) return fail(ZB_EARG, "policy handle is a%s", h->kind == ZB_POL_ACTOR ? "n actor" : " critic");
+  if (T < 0 || n < 0 || env_offset < 0) return fail(ZB_EARG, "bad size (T=%d n=%d offset=%d)", T, n, env_offset);
+  if (T == 0 || n == 0) return ZB_OK;
+  if (!obs || !carry) return fail(ZB_EARG, "null obs or carry");
+  if (kind == ZB_POL_ACTOR) {
+    if (!actions) return fail(ZB_EARG, "actor: null actions");
+    if (mode != ZB_POL_SAMPLE && mode != ZB_POL_MODE && mode != ZB_POL_EVAL)
+      return fail(ZB_EARG, "actor: unknown mode %d", mode);
+  } else if (!value) {
+    return fail(ZB_EARG, "critic: null value");
+  }
+  if ((uintptr_t)carry % 16) return fail(ZB_EARG, "carry must be 16-byte aligned");
+  int cur = -1;
+  HIPCHK(hipGetDevice(&cur));
+  if (cur != h->device) HIPCHK(hipSetDevice(h->device));
+  const size_t I = (size_t)pol_in(kind);
+  for (int t = 0; t < T; t++) {
+    zb::PolicyArgs a;
+    memset(&a, 0, sizeof a);
+    a.obs = obs + (size_t)t * n * I;
+    a.carry = carry;
+    a.reset = reset ? reset + (size_t)t * n : nullptr;
+    a.n = n;
+    a.mode = mode;
+    a.seed = seed;
+    a.env_offset = env_offset;
+    a.step = step0 + (uint32_t)t;
+    a.actions = actions ? actions + (size_t)t * n * ZB_POL_JOINTS : nullptr;
+    a.log_prob = log_prob ? log_prob + (size_t)t * n * ZB_POL_JOINTS : nullptr;
+    a.value = value ? value + (size_t)t * n : nullptr;
+    a.wpack = h->wpack;
+    a.bias = h->bias;
+    hipError_t e = zb::launch_policy(kind, a, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(ZB_ELAUNCH, "policy launch: %s", hipGetErrorString(e));
+  }
+  return ZB_OK;
+}
+
+int zb_policy_actor(ZbPolicy* p, const float* obs, int T, int n, float* carry, const uint8_t* reset, int mode,
+                    uint64_t seed, int env_offset, uint32_t step0, float* actions, float* log_prob, void* stream) {
+  return policy_run(p, ZB_POL_ACTOR, obs, T, n, carry, reset, mode, seed, env_offset, step0, actions, log_prob,
+                    nullptr, stream);
+}
+
+int zb_policy_critic(ZbPolicy* p, const float* obs, int T, int n, float* carry, const uint8_t* reset, float* value,
+                     void* stream) {
+  return policy_run(p, ZB_POL_CRITIC, obs, T, n, carry, reset, ZB_POL_SAMPLE, 0, 0, 0, nullptr, nullptr, value,
+                    stream);
 }
 
 #ifdef ZB_STAMPS

@@ -2290,13 +2290,17 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
-  if (e >= a.n_envs) return;
+  /* Both teams of a wave stay live to the end: forward()'s J'DJ runs on the
+     matrix cores with operands from all 64 lanes (jdj_mfma). A team past the
+     last env (odd n) runs as a ghost copy of env n-1 that stores nothing. */
+  const bool live = e < a.n_envs;
+  const int ee = live ? e : a.n_envs - 1;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + e));
-  float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
-  float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
+  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
+  float* rnd = live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)ee * ZB_RAND_STRIDE : nullptr;
 #ifdef ZB_STAMPS
   if (c.l < NSTAMP) c.L->stamp[c.l] = 0;
   if (c.l == 0) c.L->stamp_last = __builtin_amdgcn_s_memtime();
@@ -2316,65 +2320,78 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const bool rollout = nsteps > 1;
   for (int t = 0; t < nsteps; t++) {
     const bool last_t = t == nsteps - 1;
-    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + e) * ZB_NJ + c.act];
+    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + ee) * ZB_NJ + c.act];
     if (cfg->flags & ZB_F_PUSH) push_event(c, s, ls, a.curriculum);
     float total = 0.f;
     int ss = 0;
-    bool resetting = false;
-    /* 20 substeps; when the env terminates, one more pass of the same code path
-       runs the reset forward (mjx.forward after MjxEngine.reset) */
+    bool resetting = false; /* this team re-enters forward() for its reset state */
+    bool ghost = false;     /* the other team resets: a discarded forward() pass */
+    bool done_reset = false;
+    /* 20 substeps; a terminated env then runs one more pass of the same code
+       path for the reset forward (mjx.forward after MjxEngine.reset). That pass
+       is wave-uniform: when one team resets, the other takes its observation
+       first and then runs the same forward() on its state, discarded. */
     while (true) {
       c.m = opaque((MP)m);
       c.cfg = opaque((CP)cfg);
       STAMP(S_STEPEND);
-      if (!resetting) feetech(c, ls);
+      if (!resetting && !ghost) feetech(c, ls);
       STAMP(S_FEETECH);
-      forward(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, iters);
-      if (resetting) break;
-      integrate(c, s, ls);
-      STAMP(S_INT);
-      if (++ss < cfg->n_substeps) continue;
-      {
-        bool bad = (c.l < NV) && !(isfinite(ls.q) && isfinite(ls.v));
-        if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
-      }
-      bool fail;
-      float* terms = (a.reward_terms && !rollout) ? a.reward_terms + (size_t)e * ZB_NUM_TERMS : nullptr;
-      done = rewards(c, s, ls, B, a.curriculum, terms, total, fail);
-      rsum += total;
-      if (a.stats && c.l == 0) {
-        float* sp = a.stats + (size_t)e * ZB_NUM_STATS;
-        sp[ZB_ST_REWARD] += total;
-        if (done) {
-          sp[ZB_ST_RETURN] += s.ep_ret;
-          sp[ZB_ST_LENGTH] += (float)s.ep_steps;
-          sp[ZB_ST_DONE] += 1.f;
+      int it_pass = 0;
+      forward(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, it_pass);
+      if (!ghost) iters += it_pass;
+      if (!resetting && !ghost) {
+        integrate(c, s, ls);
+        STAMP(S_INT);
+        if (++ss < cfg->n_substeps) continue;
+        {
+          bool bad = (c.l < NV) && !(isfinite(ls.q) && isfinite(ls.v));
+          if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
         }
+        bool fail;
+        float* terms = (live && a.reward_terms && !rollout) ? a.reward_terms + (size_t)e * ZB_NUM_TERMS : nullptr;
+        done = rewards(c, s, ls, B, a.curriculum, terms, total, fail);
+        rsum += total;
+        if (live && a.stats && c.l == 0) {
+          float* sp = a.stats + (size_t)e * ZB_NUM_STATS;
+          sp[ZB_ST_REWARD] += total;
+          if (done) {
+            sp[ZB_ST_RETURN] += s.ep_ret;
+            sp[ZB_ST_LENGTH] += (float)s.ep_steps;
+            sp[ZB_ST_DONE] += 1.f;
+          }
+        }
+        done_reset = done && (cfg->flags & ZB_F_AUTORESET);
       }
-      if (!(done && (cfg->flags & ZB_F_AUTORESET))) break;
-      reset_prepare(c, s, ls, rnd);
-      resetting = true;
-    }
-    c.m = opaque((MP)m);
-    c.cfg = opaque((CP)cfg);
-    if (last_t) {
-      observe(c, s, ls, B, sen, a.obs_actor ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
-              a.obs_critic ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
-              a.obs_extra ? a.obs_extra + (size_t)e * ZB_OBS_EXTRA : nullptr);
-    } else {
-      observe(c, s, ls, B, sen, nullptr, nullptr, nullptr);
+      /* observation point: the stepped state, or the reset state */
+      c.m = opaque((MP)m);
+      c.cfg = opaque((CP)cfg);
+      if (!ghost && (resetting || !done_reset)) {
+        const bool out = live && last_t;
+        observe(c, s, ls, B, sen, (out && a.obs_actor) ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
+                (out && a.obs_critic) ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
+                (out && a.obs_extra) ? a.obs_extra + (size_t)e * ZB_OBS_EXTRA : nullptr);
+      }
+      if (resetting || ghost) break;
+      if (__ballot(done_reset) == 0ull) break;
+      if (done_reset) {
+        reset_prepare(c, s, ls, rnd);
+        resetting = true;
+      } else {
+        ghost = true;
+      }
     }
     s.rng_step += 1u;
-    if (c.l == 0 && last_t) {
+    if (live && c.l == 0 && last_t) {
       if (a.reward) a.reward[e] = rollout ? rsum : total;
       if (a.done) a.done[e] = done ? 1 : 0;
     }
   }
-  if (a.iters && c.l == 0) a.iters[e] = iters;
-  store_state(c, s, ls, st);
+  if (live && a.iters && c.l == 0) a.iters[e] = iters;
+  if (live) store_state(c, s, ls, st);
 #ifdef ZB_STAMPS
   STAMP(S_STEPEND);
-  if (a.dbg && c.l == 0)
+  if (live && a.dbg && c.l == 0)
     for (int i = 0; i < NSTAMP; i++) reinterpret_cast<unsigned long long*>(a.dbg)[(size_t)e * NSTAMP + i] = c.L->stamp[i];
 #endif
 }
@@ -2382,14 +2399,18 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
 __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
-  if (e >= a.n_envs) return;
-  if (a.reset_mask && !a.reset_mask[e]) return;
+  /* a team that is masked out (or past n) runs a discarded forward() on its
+     current state: the matrix-core J'DJ needs all 64 lanes of the wave */
+  const bool inb = e < a.n_envs;
+  const bool live = inb && !(a.reset_mask && !a.reset_mask[e]);
+  if (__ballot(live) == 0ull) return;
+  const int ee = inb ? e : a.n_envs - 1;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + e));
-  float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
-  float* rnd = (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)e * ZB_RAND_STRIDE : nullptr;
+  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
+  float* rnd = live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)ee * ZB_RAND_STRIDE : nullptr;
   EnvS& s = c.L->s;
   LaneS ls;
   load_state(c, s, ls, st);
@@ -2397,8 +2418,10 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   Rows r;
   Sensors& sen = c.L->sen;
   int it = 0;
-  reset_prepare(c, s, ls, rnd);
-  forward(c, s, ls, B, r, true, sen, it);
+  if (live) reset_prepare(c, s, ls, rnd);
+  else load_params(c, s, ls, nullptr);
+  forward(c, s, ls, B, r, live, sen, it);
+  if (!live) return;
   observe(c, s, ls, B, sen, a.obs_actor ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
           a.obs_critic ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
           a.obs_extra ? a.obs_extra + (size_t)e * ZB_OBS_EXTRA : nullptr);
@@ -2409,22 +2432,24 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
 __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
-  if (e >= a.n_envs) return;
+  const bool live = e < a.n_envs; /* a ghost team (odd n) keeps the wave whole through forward() */
+  const int ee = live ? e : a.n_envs - 1;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + e));
-  float* st = a.state + (size_t)e * ZB_STATE_STRIDE;
+  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   EnvS& s = c.L->s;
   LaneS ls;
   load_state(c, s, ls, st);
   load_params(c, s, ls, nullptr);
-  ls.ctrl = (c.act >= 0 && a.action) ? a.action[(size_t)e * ZB_NJ + c.act] : 0.f;
+  ls.ctrl = (c.act >= 0 && a.action) ? a.action[(size_t)ee * ZB_NJ + c.act] : 0.f;
   BodyK B;
   Rows r;
   Sensors& sen = c.L->sen;
   int it = 0;
   forward(c, s, ls, B, r, true, sen, it);
+  if (!live) return;
   float* d = a.dbg + (size_t)e * ZB_DBG_STRIDE;
   const int l = c.l;
   EnvL* L = c.L;

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "zbot.h"
+#include "zbot_policy.h"
 #include "zbot_ppo.h"
 
 /* debug forward dump layout (zb_debug_forward), fp32 words per env */
@@ -70,6 +71,24 @@ struct GaeArgs {
 
 hipError_t launch_gae(const GaeArgs& a, double* moments_out, hipStream_t s);
 hipError_t launch_moments(const double* in, int k, double* out, hipStream_t s);
+/* GRU actor / critic, one step (zb_policy.hip, include/zbot_policy.h) */
+struct PolicyArgs {
+  const float* obs;       /* [n][I] of this step */
+  float* carry;           /* [n][depth][hidden], read and written */
+  const uint8_t* reset;   /* [n] or null: carry zeroed first */
+  int n;
+  int mode;               /* ZB_POL_SAMPLE / MODE / EVAL (actor) */
+  uint64_t seed;
+  int env_offset;
+  uint32_t step;
+  float* actions;         /* [n][20] (actor) */
+  float* log_prob;        /* [n][20] or null (actor) */
+  float* value;           /* [n] (critic) */
+  const float* wpack;     /* fragment-packed weights */
+  const float* bias;      /* biases and head constants */
+};
+hipError_t launch_policy(int kind, const PolicyArgs& a, hipStream_t s);
+
 hipError_t launch_normalize(const float* gae, float* adv, long long count, const double* mom, double total,
                             float eps, hipStream_t s);
 

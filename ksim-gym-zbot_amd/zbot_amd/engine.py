@@ -74,6 +74,16 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.zb_adv_normalize.argtypes = [vp, vp, C.c_longlong, vp, C.c_double, C.c_float, vp]
     for f in ("zb_gae", "zb_moments_combine", "zb_adv_normalize"):
         getattr(L, f).restype = C.c_int
+    # GRU actor / critic (include/zbot_policy.h)
+    L.zb_policy_param_count.argtypes = [C.c_int]
+    L.zb_policy_param_count.restype = C.c_size_t
+    L.zb_policy_create.argtypes = [C.c_int, C.POINTER(C.c_float), C.c_size_t, C.c_int, C.POINTER(vp)]
+    L.zb_policy_destroy.argtypes = [vp]
+    L.zb_policy_actor.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_uint64, C.c_int, C.c_uint32, vp, vp,
+                                  vp]
+    L.zb_policy_critic.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, vp]
+    for f in ("zb_policy_create", "zb_policy_destroy", "zb_policy_actor", "zb_policy_critic"):
+        getattr(L, f).restype = C.c_int
     if L.zb_model_struct_bytes() != C.sizeof(cs.ZbModel):
         raise ZbError("ZbModel layout mismatch between cstructs.py and the library")
     if L.zb_config_struct_bytes() != C.sizeof(cs.ZbEnvConfig):

@@ -18,7 +18,8 @@ _LIBS: dict[str, C.CDLL] = {}
 
 def build(force: bool = False) -> None:
     """Compile the oracle libraries with the committed Makefile."""
-    targets = [os.path.join(HERE, n) for n in ("liboracle_zbot.so", "liboracle_zbot_f64.so", "liboracle_ppo.so")]
+    targets = [os.path.join(HERE, n) for n in ("liboracle_zbot.so", "liboracle_zbot_f64.so", "liboracle_ppo.so",
+                                               "liboracle_policy.so")]
     if force or not all(os.path.exists(t) for t in targets):
         subprocess.run(["make", "-C", HERE, "-s"], check=True)
 
@@ -216,3 +217,105 @@ def adv_normalize(g, moments, total: float, eps: float = 1e-6) -> np.ndarray:
     m = np.ascontiguousarray(moments, dtype=np.float64)
     ppo_lib().zbo_adv_normalize(_p(g), _p(out), g.size, _p(m, C.c_double), float(total), eps)
     return out
+
+
+# ---- GRU actor / critic + mixture head (zb_oracle_policy.c) ----
+
+def policy_lib() -> C.CDLL:
+    if "policy" in _LIBS:
+        return _LIBS["policy"]
+    path = os.path.join(HERE, "liboracle_policy.so")
+    if not os.path.exists(path):
+        build()
+    L = C.CDLL(path)
+    fp, u8p, u32p = C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.POINTER(C.c_uint32)
+    L.zbo_policy_param_count.argtypes = [C.c_int]
+    L.zbo_policy_param_count.restype = C.c_size_t
+    L.zbo_policy_actor.argtypes = [fp, fp, C.c_int, C.c_int, fp, u8p, C.c_int, C.c_uint64, C.c_int, C.c_uint32, fp, fp]
+    L.zbo_policy_critic.argtypes = [fp, fp, C.c_int, C.c_int, fp, u8p, fp]
+    for name in ("exp", "log", "tanh", "sigmoid", "softplus"):
+        f = getattr(L, "zbo_fm_" + name)
+        f.argtypes = [C.c_float]
+        f.restype = C.c_float
+    L.zbo_fm_sincos_turns.argtypes = [C.c_float, fp, fp]
+    L.zbo_fm_threefry.argtypes = [C.c_uint32] * 4 + [u32p]
+    L.zbo_fm_normal.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+    L.zbo_fm_normal.restype = C.c_float
+    L.zbo_fm_mix_log_prob.argtypes = [fp, fp, fp, C.c_float]
+    L.zbo_fm_mix_log_prob.restype = C.c_float
+    L.zbo_fm_mix_sample_batch.argtypes = [fp, fp, fp, C.c_int, C.c_uint64, C.c_int, C.c_uint32, C.c_int, fp]
+    L.zbo_fm_normal_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_int, fp]
+    _LIBS["policy"] = L
+    return L
+
+
+def policy_param_count(kind: int) -> int:
+    return int(policy_lib().zbo_policy_param_count(kind))
+
+
+def policy_actor(params, obs, carry, reset=None, mode: int = 0, seed: int = 0, env_offset: int = 0, step0: int = 0,
+                 actions=None, log_prob: bool = False):
+    """obs [T, n, 50], carry [n, 5, 128] (a copy is updated and returned).
+    Returns (actions [T, n, 20], log_prob [T, n, 20] or None, carry)."""
+    P = np.ascontiguousarray(params, dtype=np.float32)
+    obs = np.ascontiguousarray(obs, dtype=np.float32)
+    T, n, _ = obs.shape
+    c = np.array(carry, dtype=np.float32, copy=True, order="C")
+    r = None if reset is None else np.ascontiguousarray(np.asarray(reset).reshape(T, n), dtype=np.uint8)
+    a = (np.zeros((T, n, 20), np.float32) if actions is None
+         else np.array(actions, dtype=np.float32, copy=True, order="C").reshape(T, n, 20))
+    lp = np.zeros((T, n, 20), np.float32) if log_prob else None
+    policy_lib().zbo_policy_actor(_p(P), _p(obs), T, n, _p(c), _p(r, C.c_uint8), mode, seed, env_offset, step0, _p(a),
+                                  _p(lp))
+    return a, lp, c
+
+
+def policy_critic(params, obs, carry, reset=None):
+    """obs [T, n, 484], carry [n, 5, 128] -> (value [T, n], carry)."""
+    P = np.ascontiguousarray(params, dtype=np.float32)
+    obs = np.ascontiguousarray(obs, dtype=np.float32)
+    T, n, _ = obs.shape
+    c = np.array(carry, dtype=np.float32, copy=True, order="C")
+    r = None if reset is None else np.ascontiguousarray(np.asarray(reset).reshape(T, n), dtype=np.uint8)
+    v = np.zeros((T, n), np.float32)
+    policy_lib().zbo_policy_critic(_p(P), _p(obs), T, n, _p(c), _p(r, C.c_uint8), _p(v))
+    return v, c
+
+
+def fm(name: str, x) -> np.ndarray:
+    f = getattr(policy_lib(), "zbo_fm_" + name)
+    return np.array([f(float(v)) for v in np.asarray(x, dtype=np.float32).ravel()], dtype=np.float32)
+
+
+def fm_sincos(t):
+    L = policy_lib()
+    s, c = C.c_float(), C.c_float()
+    out = []
+    for v in np.asarray(t, dtype=np.float32).ravel():
+        L.zbo_fm_sincos_turns(float(v), C.byref(s), C.byref(c))
+        out.append((s.value, c.value))
+    return np.array(out, dtype=np.float32).T
+
+
+def fm_threefry(k0, k1, c0, c1):
+    o = (C.c_uint32 * 2)()
+    policy_lib().zbo_fm_threefry(k0 & 0xFFFFFFFF, k1 & 0xFFFFFFFF, c0 & 0xFFFFFFFF, c1 & 0xFFFFFFFF, o)
+    return o[0], o[1]
+
+
+def fm_normals(seed: int, purpose: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.float32)
+    policy_lib().zbo_fm_normal_batch(seed, purpose, n, _p(out))
+    return out
+
+
+def mix_sample_batch(mu, sd, lg, seed: int, n: int, step: int = 0, j: int = 0, argmax: bool = False):
+    mu, sd, lg = (np.ascontiguousarray(x, dtype=np.float32) for x in (mu, sd, lg))
+    out = np.zeros(n, np.float32)
+    policy_lib().zbo_fm_mix_sample_batch(_p(mu), _p(sd), _p(lg), int(argmax), seed, n, step, j, _p(out))
+    return out
+
+
+def mix_log_prob(mu, sd, lg, a: float) -> float:
+    mu, sd, lg = (np.ascontiguousarray(x, dtype=np.float32) for x in (mu, sd, lg))
+    return float(policy_lib().zbo_fm_mix_log_prob(_p(mu), _p(sd), _p(lg), float(a)))

@@ -49,8 +49,8 @@ def main():
         open(os.path.join(d, "zb_capi.cpp"), "w").write(capi)
         cmd[-1] = os.path.join(d, "zb_capi.cpp")
         # the PPO kernels share the library's C ABI file; the stamp build links the product object
-        subprocess.run(["make", "-C", CSRC, "-s", "build/zb_ppo.o"], check=True)
-        cmd.append(os.path.join(CSRC, "build", "zb_ppo.o"))
+        subprocess.run(["make", "-C", CSRC, "-s", "build/zb_ppo.o", "build/zb_policy.o"], check=True)
+        cmd += [os.path.join(CSRC, "build", "zb_ppo.o"), os.path.join(CSRC, "build", "zb_policy.o")]
         subprocess.run(cmd, check=True)
     print(n, ",".join(names))
 

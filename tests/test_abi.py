@@ -36,7 +36,7 @@ def test_every_field_offset_matches_c(oracle_mod, which, cls):
 
 def _declared_symbols():
     syms = set()
-    for h in ("zbot.h", "zbot_ppo.h"):
+    for h in ("zbot.h", "zbot_ppo.h", "zbot_policy.h"):
         txt = open(os.path.join(ROOT, "include", h)).read()
         syms |= set(re.findall(r"\b(zb_[a-z_]+)\s*\(", txt))
     return sorted(syms)
@@ -44,7 +44,8 @@ def _declared_symbols():
 
 def test_library_exports_every_declared_symbol(hiplib):
     syms = _declared_symbols()
-    assert len(syms) >= 19
+    assert len(syms) >= 25
+    assert {"zb_policy_create", "zb_policy_actor", "zb_policy_critic", "zb_policy_destroy"} <= set(syms)
     assert {"zb_gae", "zb_moments_combine", "zb_adv_normalize", "zb_gae_partials_words"} <= set(syms)
     for s in syms:
         assert hasattr(hiplib, s), f"libzbot_hip.so does not export {s}"

@@ -269,3 +269,54 @@ def test_ksim_shaped_env(torch_gpu, cmodel):
     assert torch.allclose(total, r.reward, atol=1e-5)
     stats = env.episode_stats()
     assert stats["episodes"] >= 0
+
+
+def test_team_divergence_is_exact(torch_gpu, cmodel, oracle_mod):
+    """The two envs of a wavefront (teams 2k, 2k+1) are independent: an odd env count, a
+    masked reset and a single-team auto-reset give the bits of the unconstrained runs.
+    (The contact Hessian's J'DJ runs on the matrix cores with operands from all 64
+    lanes, so a team that sits out must still run forward() as a ghost.)"""
+    torch = torch_gpu
+    cfg = default_config()
+    acts = [torch.from_numpy(oracle_mod.synthetic_actions(cmodel.cmodel, 3, 34, 0, t)).cuda() for t in range(4)]
+    res = {}
+    for n in (33, 34):
+        eng = engine(cmodel, cfg, n, seed=3)
+        eng.reset()
+        for a in acts:
+            o = eng.step(a[:n].contiguous())
+        torch.cuda.synchronize()
+        res[n] = (eng.get_state().cpu().numpy(), o["obs_critic"].cpu().numpy().copy())
+    assert np.array_equal(res[33][0], res[34][0][:33])
+    assert np.array_equal(res[33][1], res[34][1][:33])
+    # masked reset (odd envs keep running) == full reset, on the reset envs
+    n = 16
+    A, B = engine(cmodel, cfg, n, seed=4), engine(cmodel, cfg, n, seed=4)
+    for eng in (A, B):
+        eng.reset()
+        eng.step(acts[0][:n].contiguous())
+    mask = torch.zeros(n, dtype=torch.uint8)
+    mask[::2] = 1
+    oa = A.reset(mask=mask)["obs_critic"].cpu().numpy().copy()
+    ob = B.reset()["obs_critic"].cpu().numpy().copy()
+    sa, sb = A.get_state().cpu().numpy(), B.get_state().cpu().numpy()
+    assert np.array_equal(sa[::2], sb[::2]) and np.array_equal(oa[::2], ob[::2])
+    # one env of a wave auto-resets while its partner steps on: both match the oracle
+    cfg2 = default_config(obs_noise=False)
+    n = 8
+    env = warm_states(oracle_mod, cmodel, cfg2, n, steps=6)
+    st = env.state.copy()
+    st[3, 2] = 0.7  # BadZ: team 1 of wave 1
+    st[4, 2] = 0.7  # BadZ: team 0 of wave 2
+    env.state[:] = st
+    eng = engine(cmodel, cfg2, n, seed=7)
+    eng.set_state(torch.from_numpy(st))
+    a = oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 50)
+    ref = env.step(a)
+    out = eng.step(torch.from_numpy(a).cuda())
+    torch.cuda.synchronize()
+    assert out["done"].cpu().numpy().tolist() == ref["done"].tolist() and ref["done"][[3, 4]].all()
+    np.testing.assert_allclose(out["obs_critic"].cpu().numpy(), ref["obs_critic"], atol=2e-2, rtol=1e-3)
+    gs = eng.get_state().cpu().numpy()
+    np.testing.assert_allclose(gs[:, cs.S_QACCW:cs.S_QACCW + 26], env.state[:, cs.S_QACCW:cs.S_QACCW + 26],
+                               atol=5e-2, rtol=1e-2)

@@ -1,0 +1,104 @@
+"""GPU parity of the GRU actor / critic, through the C
+ABI (include/zbot_policy.h) via zbot_amd.policy.
+
+Bar: bit-exact against the CPU oracle (oracle/zb_oracle_policy.c): the matrix
+cores compute each product as the k-ordered fp32 fmaf chain the oracle runs,
+and both sides share include/zbot_fmath.h for every transcendental and the RNG.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from zbot_amd.policy import ACTOR, CRITIC, EVAL, MODE, SAMPLE, init_params
+
+pytestmark = pytest.mark.gpu
+D, H = 5, 128
+
+
+@pytest.fixture(scope="module")
+def pol():
+    from zbot_amd import policy as P
+
+    assert torch.cuda.is_available()
+    return P
+
+
+def _inputs(T, n, I, seed):
+    rng = np.random.default_rng(seed)
+    obs = rng.normal(size=(T, n, I)).astype(np.float32)
+    carry = (0.5 * rng.normal(size=(n, D, H))).astype(np.float32)
+    reset = (rng.random((T, n)) < 0.2).astype(np.uint8)
+    return obs, carry, reset
+
+
+@pytest.mark.parametrize("n,T,mode", [(1, 1, SAMPLE), (33, 3, SAMPLE), (256, 2, MODE), (70, 2, EVAL), (2048, 1, SAMPLE)])
+def test_actor_bit_exact(pol, oracle_mod, n, T, mode):
+    P = init_params(ACTOR, seed=3)
+    obs, carry, reset = _inputs(T, n, 50, n + T)
+    acts_in = (0.4 * np.random.default_rng(1).normal(size=(T, n, 20))).astype(np.float32) if mode == EVAL else None
+    a_ref, lp_ref, c_ref = oracle_mod.policy_actor(P, obs, carry, reset, mode=mode, seed=9, env_offset=5, step0=17,
+                                                   actions=acts_in, log_prob=True)
+    net = pol.GruPolicy(ACTOR, P)
+    c = torch.from_numpy(carry).cuda()
+    a, lp = net.actor(torch.from_numpy(obs).cuda(), c, reset=torch.from_numpy(reset).cuda(), mode=mode, seed=9,
+                      env_offset=5, step=17, actions=None if acts_in is None else torch.from_numpy(acts_in).cuda(),
+                      log_prob=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(c.cpu().numpy(), c_ref)
+    np.testing.assert_array_equal(a.cpu().numpy(), a_ref)
+    np.testing.assert_array_equal(lp.cpu().numpy(), lp_ref)
+
+
+@pytest.mark.parametrize("n,T", [(5, 2), (64, 3)])
+def test_critic_bit_exact(pol, oracle_mod, n, T):
+    P = init_params(CRITIC, seed=4)
+    obs, carry, reset = _inputs(T, n, 484, 7 * n)
+    v_ref, c_ref = oracle_mod.policy_critic(P, obs, carry, reset)
+    net = pol.GruPolicy(CRITIC, P)
+    c = torch.from_numpy(carry).cuda()
+    v = net.critic(torch.from_numpy(obs).cuda(), c, reset=torch.from_numpy(reset).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(v.cpu().numpy(), v_ref)
+    np.testing.assert_array_equal(c.cpu().numpy(), c_ref)
+
+
+def test_actor_shard_invariant(pol):
+    """Envs keep their RNG streams and results whatever batch / offset they run in."""
+    net = pol.GruPolicy(ACTOR, init_params(ACTOR, seed=6))
+    obs, carry, _ = _inputs(1, 96, 50, 2)
+    o = torch.from_numpy(obs[0]).cuda()
+    c = torch.from_numpy(carry).cuda()
+    full, _ = net.actor(o, c.clone(), seed=1, env_offset=0, step=3)
+    part, _ = net.actor(o[40:].contiguous(), c[40:].clone(), seed=1, env_offset=40, step=3)
+    assert torch.equal(full[40:], part)
+
+
+def test_errors(pol):
+    net = pol.GruPolicy(ACTOR, init_params(ACTOR))
+    with pytest.raises(pol.ZbError):
+        net.critic(torch.zeros(2, 484, device="cuda"), net.initial_carry(2))
+    with pytest.raises(pol.ZbError):
+        net.actor(torch.zeros(2, 50, device="cuda"), net.initial_carry(3))
+    with pytest.raises(pol.ZbError):
+        pol.GruPolicy(ACTOR, np.zeros(10, np.float32))
+
+
+def test_policy_in_the_rollout_loop(pol, cmodel):
+    """actor -> zb_step per control step, rows straight into [T, n] buffers; reproducible."""
+    from zbot_amd import default_config
+    from zbot_amd.engine import HipEngine
+
+    runs = []
+    for _ in range(2):
+        eng = HipEngine(cmodel, default_config(), 64, seed=2)
+        ro = pol.PolicyRollout(eng, pol.GruPolicy(ACTOR, init_params(ACTOR, seed=8)), seed=5)
+        out = ro.run(6)
+        torch.cuda.synchronize()
+        runs.append({k: v.cpu().numpy() for k, v in out.items()})
+    for k in runs[0]:
+        np.testing.assert_array_equal(runs[0][k], runs[1][k])
+    r = runs[0]
+    assert np.isfinite(r["actions"]).all() and np.isfinite(r["reward"]).all() and np.isfinite(r["log_prob"]).all()
+    assert r["obs_actor"].shape == (7, 64, 50)
+    assert not np.array_equal(r["actions"][0, 0], r["actions"][0, 1])
