@@ -124,6 +124,51 @@ def bench_ppo_inputs(n: int, T: int, reps: int, dev, world: int) -> dict:
     }
 
 
+def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int) -> dict:
+    """The GRU actor in the rollout loop: per control step the actor samples
+    every env's action from its observation on the f32 matrix cores, then zb_step advances the
+    envs (ksim sample_action -> env.step, train.py:1737-1763)."""
+    import torch  # noqa: PLC0415
+    from zbot_amd import policy as P  # noqa: PLC0415
+    from zbot_amd.metrics import FP32_PEAK_TFLOPS  # noqa: PLC0415
+
+    actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), device=dev.index)
+    carry = actor.initial_carry(n)
+    acts = torch.empty(n, P.JOINTS, device=dev)
+    eng.reset(extras=False)
+    stream = torch.cuda.current_stream(dev)
+
+    def one(t, ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        actor.actor(eng.obs_actor, carry, reset=eng.done if t > 0 else None, seed=1, env_offset=rank * n, step=t,
+                    actions=acts)
+        if ev is not None:
+            ev[1].record(stream)
+        eng.step(acts, extras=False)
+
+    for t in range(2):
+        one(t)
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for t in range(steps):
+        one(2 + t, evs[t])
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    actor_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
+    tf = P.FLOP_ACTOR * n / (actor_ms * 1e-3) / 1e12
+    return {
+        "workload": f"GRU actor (5 x GRU 128, mixture-of-Gaussians head) sampling the actions of {n} envs, then "
+                    "zb_step, per control step",
+        "env_steps_per_s_with_policy": n * steps / wall,
+        "actor_kernel_ms": actor_ms,
+        "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tf / FP32_PEAK_TFLOPS, "kernel": "zb::pol::policy_kernel<50, 300, true>",
+                     "flop_per_env_step": P.FLOP_ACTOR, "dtype": "f32 (v_mfma_f32_32x32x2_f32)"},
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,6 +180,7 @@ def main() -> None:
     ap.add_argument("--cpu-baseline-sec", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
+    ap.add_argument("--no-policy", action="store_true", help="skip the policy-in-the-loop leg")
     args = ap.parse_args()
 
     import torch  # noqa: PLC0415
@@ -220,6 +266,7 @@ def main() -> None:
             flop_per_env_step = tj.get("issued_fp32_flop_per_env_step")
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
+    policy_leg = None if args.no_policy else bench_policy_in_loop(eng, n, 16, dev, rank)
 
     if rank == 0:
         value = world * n * args.steps / elapsed
@@ -273,6 +320,8 @@ def main() -> None:
         }
         if ppo_leg is not None:
             out["ppo_inputs"] = ppo_leg
+        if policy_leg is not None:
+            out["policy_in_loop"] = policy_leg
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper())
         print(json.dumps(out), flush=True)

@@ -24,6 +24,12 @@
 #define ZBF_FN static inline
 #endif
 
+/* No implicit multiply-add contraction in anything below (the oracle is built
+   with -ffp-contract=off; hipcc would otherwise fuse e.g. mu + sd * z). */
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
 #define ZBF_LN2_HI 0.693145751953125f   /* 0x3f317200: ln 2, 15 significant bits */
 #define ZBF_LN2_LO 1.42860682e-06f      /* ln 2 - ZBF_LN2_HI */
 #define ZBF_LOG2E 1.44269504088896341f
