@@ -1,0 +1,539 @@
+"""MJCF <-> robot descriptor.
+
+The reference builds its model from the K-Scale Z-Bot MJCF (train.py:1326-1331:
+`ksim.get_mujoco_model_path("zbot")` + `mujoco_scenes.mjcf.load_mjmodel`, floor
+`geom_priority = 2`) and reads the Feetech servo parameters from the K-Scale
+metadata (train.py:1333-1338, 1340-1437). Both are network-fetched and absent
+here, so the engine runs on the documented Z-Bot-like descriptor
+(assets/zbot_like.json). This module lets an MJCF file take its place offline:
+
+    desc = load_mjcf("zbot.xml", servo_classes=..., joint_servo=...)
+    cm = compile_model(desc)               # -> ZbModel for zb_create
+
+It reads the MJCF subset the engine's task topology uses, following MuJoCo's
+MJCF semantics (XML reference, MuJoCo 3.3.4 [U]):
+  * <compiler angle="degree|radian"> (MuJoCo's default is degree) and
+    eulerseq (intrinsic "xyz" by default);
+  * <default> classes, nested, applied through `class` / `childclass` with
+    explicit attributes winning (joint: axis, range, armature, damping,
+    frictionloss, pos; geom: type, size, pos, contype, conaffinity);
+  * <body pos quat|euler|axisangle>, one <joint type="hinge"> or a
+    <freejoint/> per body, <inertial pos quat mass diaginertia>;
+  * box <geom>s with a nonzero contype/conaffinity as the foot-sole colliders,
+    the <geom type="plane"> of the worldbody as the floor (friction, solref,
+    solimp, margin);
+  * <site>s; <option timestep gravity>.
+The servo model (FeetechParams, train.py:1121-1134) is not part of MJCF: it
+comes from `servo_classes` + `joint_servo` (joint -> class; by default the
+joint's MJCF class when it names a servo class, else the Z-Bot-like
+descriptor's assignment for that joint name). `to_mjcf` writes a descriptor
+back out, so a descriptor and its MJCF compile to the same ZbModel
+(tests/test_mjcf.py).
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+from .model import load_description
+
+
+def _floats(s: str | None, n: int | None = None) -> list[float] | None:
+    if s is None:
+        return None
+    v = [float(x) for x in s.split()]
+    if n is not None and len(v) != n:
+        raise ValueError(f"expected {n} numbers, got {s!r}")
+    return v
+
+
+def _qmul(a, b):
+    w1, x1, y1, z1 = a
+    w2, x2, y2, z2 = b
+    return [w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+            w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2]
+
+
+def _axis_quat(axis, angle):
+    a = np.asarray(axis, dtype=np.float64)
+    a = a / np.linalg.norm(a)
+    s = math.sin(angle / 2)
+    return [math.cos(angle / 2), a[0] * s, a[1] * s, a[2] * s]
+
+
+def _quat_mat(q):
+    w, x, y, z = q
+    return [[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+            [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+            [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]]
+
+
+def _mat_quat(R: np.ndarray) -> list[float]:
+    t = R[0, 0] + R[1, 1] + R[2, 2]
+    if t > 0:
+        w = math.sqrt(1.0 + t) / 2
+        q = [w, (R[2, 1] - R[1, 2]) / (4 * w), (R[0, 2] - R[2, 0]) / (4 * w), (R[1, 0] - R[0, 1]) / (4 * w)]
+    else:
+        i = int(np.argmax([R[0, 0], R[1, 1], R[2, 2]]))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        r = math.sqrt(max(0.0, 1.0 + R[i, i] - R[j, j] - R[k, k]))
+        v = [0.0, 0.0, 0.0]
+        v[i] = r / 2
+        v[j] = (R[j, i] + R[i, j]) / (2 * r)
+        v[k] = (R[k, i] + R[i, k]) / (2 * r)
+        q = [(R[k, j] - R[j, k]) / (2 * r)] + v
+    if q[0] < 0:
+        q = [-x for x in q]
+    n = math.sqrt(sum(x * x for x in q))
+    return [x / n for x in q]
+
+
+def _principal(inertia: np.ndarray) -> tuple[list[float], list[float]]:
+    """Principal moments and the frame holding them (MJCF diaginertia + inertial quat)."""
+    off = abs(inertia[0, 1]) + abs(inertia[0, 2]) + abs(inertia[1, 2])
+    if off <= 1e-14 * max(1e-300, float(np.trace(inertia))):
+        return [float(inertia[k, k]) for k in range(3)], [1.0, 0.0, 0.0, 0.0]
+    w, V = np.linalg.eigh(inertia)
+    if np.linalg.det(V) < 0:
+        V[:, 2] = -V[:, 2]
+    return [float(x) for x in w], _mat_quat(V)
+
+
+def _geom_mass_inertia(ga: dict, quat: list[float]):
+    """(mass, centre, rotation, principal moments) of one solid geom, as MuJoCo's compiler
+    takes it for inertiafromgeom: uniform density (default 1000) or the geom's explicit mass."""
+    gt = ga.get("type", "sphere")
+    size = _floats(ga.get("size", "0 0 0"))
+    pos = np.array(_floats(ga.get("pos", "0 0 0"), 3))
+    R = np.array(_quat_mat(quat))
+    if "fromto" in ga:
+        if gt not in ("capsule", "cylinder", "box", "ellipsoid"):
+            raise ValueError(f"geom {ga.get('name')}: fromto on a {gt}")
+        ft = np.array(_floats(ga["fromto"], 6))
+        d = ft[3:] - ft[:3]
+        L = float(np.linalg.norm(d))
+        pos = (ft[:3] + ft[3:]) / 2
+        z = d / L
+        axis = np.cross([0.0, 0.0, 1.0], z)
+        sn, cs_ = float(np.linalg.norm(axis)), float(z[2])
+        if sn > 1e-12:
+            R = np.array(_quat_mat(_axis_quat(axis, math.atan2(sn, cs_))))
+        else:
+            R = np.eye(3) if cs_ > 0 else np.diag([1.0, -1.0, -1.0])
+        size = [size[0], L / 2] if gt in ("capsule", "cylinder") else [size[0], size[1], L / 2]
+    if gt == "sphere":
+        r = size[0]
+        vol = 4.0 / 3.0 * math.pi * r ** 3
+
+        def f(m):
+            return [0.4 * m * r * r] * 3
+    elif gt == "box":
+        x, y, z = size[:3]
+        vol = 8.0 * x * y * z
+
+        def f(m):
+            return [m / 3 * (y * y + z * z), m / 3 * (x * x + z * z), m / 3 * (x * x + y * y)]
+    elif gt == "ellipsoid":
+        a, b_, c = size[:3]
+        vol = 4.0 / 3.0 * math.pi * a * b_ * c
+
+        def f(m):
+            return [m / 5 * (b_ * b_ + c * c), m / 5 * (a * a + c * c), m / 5 * (a * a + b_ * b_)]
+    elif gt == "cylinder":
+        r, h = size[0], size[1]
+        vol = math.pi * r * r * 2 * h
+
+        def f(m):
+            return [m * (3 * r * r + 4 * h * h) / 12] * 2 + [m * r * r / 2]
+    elif gt == "capsule":
+        r, h = size[0], size[1]
+        vcyl, vsph = math.pi * r * r * 2 * h, 4.0 / 3.0 * math.pi * r ** 3
+        vol = vcyl + vsph
+
+        def f(m):
+            # cylinder about its centre + two solid hemispheres, each with its centroid 3r/8
+            # beyond the cylinder's end and a transverse moment (83/320) m_h r^2 about it
+            mc, hemi = m * vcyl / vol, m * vsph / vol / 2
+            it = mc * (3 * r * r + 4 * h * h) / 12 + 2 * (83.0 / 320.0 * hemi * r * r + hemi * (h + 3 * r / 8) ** 2)
+            return [it, it, mc * r * r / 2 + 2 * 0.4 * hemi * r * r]
+    else:
+        raise ValueError(f"geom {ga.get('name')}: inertia from a {gt} geom is not supported")
+    m = float(ga["mass"]) if "mass" in ga else float(ga.get("density", "1000")) * vol
+    return m, pos, R, f(m)
+
+
+def _compose(parts):
+    """Sum geom masses and inertias about the common centre of mass (parallel axes)."""
+    M = sum(p[0] for p in parts)
+    if M <= 0:
+        raise ValueError("geom-derived body mass must be positive")
+    com = sum(p[0] * p[1] for p in parts) / M
+    inertia = np.zeros((3, 3))
+    for m, pos, R, diag in parts:
+        d = pos - com
+        inertia += R @ np.diag(diag) @ R.T + m * (float(d @ d) * np.eye(3) - np.outer(d, d))
+    diag, iq = _principal(inertia)
+    return float(M), [float(x) for x in com], diag, iq
+
+
+
+class _Defaults:
+    """MJCF default classes: class name -> {element tag -> attributes}, inherited down the tree."""
+
+    def __init__(self, root: ET.Element | None):
+        self.cls: dict[str, dict[str, dict[str, str]]] = {"main": {}}
+        if root is not None:
+            self._walk(root, "main", {})
+
+    def _walk(self, el: ET.Element, name: str, inherited: dict):
+        own = {tag: dict(attrs) for tag, attrs in inherited.items()}
+        for child in el:
+            if child.tag != "default":
+                own.setdefault(child.tag, {}).update(child.attrib)
+        self.cls[name] = own
+        for child in el:
+            if child.tag == "default":
+                self._walk(child, child.get("class", name), own)
+
+    def attrs(self, el: ET.Element, cls: str) -> dict[str, str]:
+        c = el.get("class", cls)
+        if c not in self.cls:
+            raise ValueError(f"unknown default class {c!r}")
+        out = dict(self.cls[c].get(el.tag, {}))
+        out.update(el.attrib)
+        return out
+
+
+def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | None = None,
+              base_clearance: float | None = None, template: dict | None = None) -> dict:
+    """Parse an MJCF file (path or XML text) into the descriptor compile_model() takes.
+
+    template: descriptor supplying what MJCF does not hold (servo classes, the joint -> servo
+    map, base clearance, constraint solref/solimp); default assets/zbot_like.json."""
+    tmpl = template or load_description()
+    text = open(src).read() if os.path.exists(src) else src
+    root = ET.fromstring(text)
+    if root.tag != "mujoco":
+        raise ValueError("not an MJCF document (<mujoco> root expected)")
+    comp = root.find("compiler")
+    degree = (comp.get("angle", "degree") if comp is not None else "degree") == "degree"
+    eulerseq = comp.get("eulerseq", "xyz") if comp is not None else "xyz"
+    ang = (lambda v: v * math.pi / 180.0) if degree else (lambda v: v)
+    fromgeom = comp.get("inertiafromgeom", "auto") if comp is not None else "auto"
+    grp = [int(x) for x in comp.get("inertiagrouprange", "0 5").split()] if comp is not None else [0, 5]
+    defaults = _Defaults(root.find("default"))
+
+    servo_classes = dict(servo_classes if servo_classes is not None else tmpl.get("servo_classes", {}))
+    tmpl_servo = {b["joint"]["name"]: b["joint"].get("servo") for b in tmpl["bodies"] if "joint" in b}
+
+    desc: dict = {
+        "name": root.get("model", "mjcf"),
+        "description": "imported from MJCF by zbot_amd.mjcf.load_mjcf",
+        "option": {"timestep": 0.002, "gravity": [0.0, 0.0, -9.81]},
+        "floor": dict(tmpl.get("floor", {})),
+        "joint_constraint": dict(tmpl.get("joint_constraint", {})),
+        "base_clearance": tmpl.get("base_clearance", 0.0) if base_clearance is None else base_clearance,
+        "servo_classes": servo_classes,
+        "bodies": [],
+        "geoms": [],
+        "sites": [],
+    }
+    opt = root.find("option")
+    if opt is not None:
+        if opt.get("timestep"):
+            desc["option"]["timestep"] = float(opt.get("timestep"))
+        if opt.get("gravity"):
+            desc["option"]["gravity"] = _floats(opt.get("gravity"), 3)
+
+    def orientation(el, attrs) -> list[float]:
+        if "quat" in attrs:
+            q = _floats(attrs["quat"], 4)
+            n = math.sqrt(sum(x * x for x in q))
+            return [x / n for x in q]
+        if "axisangle" in attrs:
+            v = _floats(attrs["axisangle"], 4)
+            return _axis_quat(v[:3], ang(v[3]))
+        if "euler" in attrs:
+            e = [ang(x) for x in _floats(attrs["euler"], 3)]
+            q = [1.0, 0.0, 0.0, 0.0]
+            for ch, a in zip(eulerseq, e):
+                axis = {"x": [1, 0, 0], "y": [0, 1, 0], "z": [0, 0, 1]}[ch.lower()]
+                r = _axis_quat(axis, a)
+                q = _qmul(q, r) if ch.islower() else _qmul(r, q)  # intrinsic (moving) vs extrinsic
+            return q
+        return [1.0, 0.0, 0.0, 0.0]
+
+    def parse_body(el: ET.Element, parent: str, cls: str):
+        cls = el.get("childclass", cls)
+        name = el.get("name")
+        if not name:
+            raise ValueError("every body needs a name")
+        b: dict = {"name": name, "parent": parent, "pos": _floats(el.get("pos", "0 0 0"), 3)}
+        q = orientation(el, el.attrib)
+        if q != [1.0, 0.0, 0.0, 0.0]:
+            b["quat"] = q
+        joints = [c for c in el if c.tag in ("joint", "freejoint")]
+        if len(joints) > 1:
+            raise ValueError(f"body {name}: one joint per body is supported (got {len(joints)})")
+        for j in joints:
+            ja = defaults.attrs(j, cls) if j.tag == "joint" else dict(j.attrib)
+            jt = "free" if j.tag == "freejoint" else ja.get("type", "hinge")
+            if jt == "free":
+                b["joint"] = {"name": ja.get("name", name + "_free"), "type": "free"}
+                continue
+            if jt != "hinge":
+                raise ValueError(f"joint {ja.get('name')}: type {jt} is not supported (hinge / free)")
+            jd = {"name": ja["name"], "type": "hinge", "axis": _floats(ja.get("axis", "0 0 1"), 3)}
+            if "pos" in ja:
+                jd["pos"] = _floats(ja["pos"], 3)
+            limited = ja.get("limited", "auto")
+            if "range" in ja and limited != "false":
+                jd["range"] = [ang(x) for x in _floats(ja["range"], 2)]
+            servo = (joint_servo or {}).get(jd["name"])
+            if servo is None and j.get("class", cls) in servo_classes:
+                servo = j.get("class", cls)
+            if servo is None:
+                servo = tmpl_servo.get(jd["name"])
+            if servo is not None:
+                jd["servo"] = servo
+            base = servo_classes.get(servo, {}) if servo else {}
+            mj = {k: float(ja[k]) for k in ("armature", "damping", "frictionloss")
+                  if k in ja and float(ja[k]) != float(base.get(k, 0.0))}
+            if mj:  # MJCF joint dynamics that differ from the servo class's own values win
+                key = f"{servo or 'mjcf'}@{jd['name']}"
+                base = dict(servo_classes.get(servo, {})) if servo else {}
+                base.update(mj)
+                servo_classes[key] = base
+                jd["servo"] = key
+            b["joint"] = jd
+        inert = el.find("inertial")
+        if inert is not None and fromgeom != "true":
+            b["mass"] = float(inert.get("mass"))
+            b["ipos"] = _floats(inert.get("pos", "0 0 0"), 3)
+            if inert.get("diaginertia"):
+                b["inertia"] = _floats(inert.get("diaginertia"), 3)
+                iq = orientation(inert, inert.attrib)
+            elif inert.get("fullinertia"):
+                xx, yy, zz, xy, xz, yz = _floats(inert.get("fullinertia"), 6)
+                diag, iq = _principal(np.array([[xx, xy, xz], [xy, yy, yz], [xz, yz, zz]]))
+                b["inertia"] = diag
+            else:
+                raise ValueError(f"body {name}: <inertial> needs diaginertia or fullinertia")
+        elif fromgeom == "false":
+            raise ValueError(f"body {name}: no <inertial> and inertiafromgeom is false")
+        else:  # MuJoCo's inertiafromgeom: mass and inertia of the body's geoms at their density
+            parts = []
+            for c in el:
+                if c.tag == "geom":
+                    ga = defaults.attrs(c, cls)
+                    if grp[0] <= int(ga.get("group", "0")) <= grp[1]:
+                        parts.append(_geom_mass_inertia(ga, orientation(c, ga)))
+            if not parts:
+                raise ValueError(f"body {name}: no <inertial> element and no geoms to infer it from")
+            mass, com, diag, iq = _compose(parts)
+            b["mass"], b["ipos"], b["inertia"] = mass, com, diag
+        if iq != [1.0, 0.0, 0.0, 0.0]:
+            b["iquat"] = iq
+        desc["bodies"].append(b)
+        for c in el:
+            if c.tag == "geom":
+                ga = defaults.attrs(c, cls)
+                if ga.get("type", "sphere") != "box":
+                    continue
+                if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
+                    continue
+                gd = {"name": ga.get("name", f"{name}_geom{len(desc['geoms'])}"), "body": name, "type": "box",
+                      "size": _floats(ga["size"], 3)}
+                if "pos" in ga:
+                    gd["pos"] = _floats(ga["pos"], 3)
+                gq = orientation(c, ga)
+                if gq != [1.0, 0.0, 0.0, 0.0]:
+                    gd["quat"] = gq
+                desc["geoms"].append(gd)
+            elif c.tag == "site":
+                sa = defaults.attrs(c, cls)
+                sd = {"name": sa["name"], "body": name, "pos": _floats(sa.get("pos", "0 0 0"), 3)}
+                sq = orientation(c, sa)
+                if sq != [1.0, 0.0, 0.0, 0.0]:
+                    sd["quat"] = sq
+                desc["sites"].append(sd)
+        for c in el:
+            if c.tag == "body":
+                parse_body(c, name, cls)
+
+    wb = root.find("worldbody")
+    if wb is None:
+        raise ValueError("no <worldbody>")
+    for c in wb:
+        if c.tag == "body":
+            parse_body(c, "world", c.get("childclass", "main"))
+        elif c.tag == "geom":
+            ga = defaults.attrs(c, "main")
+            if ga.get("type") == "plane":
+                fl = desc["floor"]
+                if "friction" in ga:
+                    fr = _floats(ga["friction"])
+                    fl["friction"] = (fr + [0.005, 0.0001][len(fr) - 1:])[:3] if len(fr) < 3 else fr
+                for k in ("solref", "solimp"):
+                    if k in ga:
+                        fl[k] = _floats(ga[k])
+                if "margin" in ga:
+                    fl["margin"] = float(ga["margin"])
+    # actuators: a motor (or gain-1 general actuator) per hinge; ctrl order is the joint order
+    # the engine requires (JOINT_BIASES, train.py:61-82), whatever the actuator order here
+    act = root.find("actuator")
+    if act is not None:
+        hinges = {b["joint"]["name"]: b["joint"] for b in desc["bodies"]
+                  if b.get("joint", {}).get("type") == "hinge"}
+        seen = set()
+        for a in act:
+            aa = defaults.attrs(a, "main")
+            if a.tag not in ("motor", "general"):
+                raise ValueError(f"actuator {aa.get('name')}: <{a.tag}> is not supported (motor / general)")
+            if a.tag == "general" and (aa.get("biastype", "none") != "none"
+                                       or _floats(aa.get("gainprm", "1"))[0] != 1.0):
+                raise ValueError(f"actuator {aa.get('name')}: only a plain-gain general actuator is supported")
+            jn = aa.get("joint")
+            if jn not in hinges:
+                raise ValueError(f"actuator {aa.get('name')}: joint {jn!r} is not a hinge of the model")
+            if jn in seen:
+                raise ValueError(f"joint {jn}: more than one actuator")
+            seen.add(jn)
+            jd = hinges[jn]
+            gear = _floats(aa.get("gear", "1"))[0]
+            if gear != 1.0:
+                jd["gear"] = gear
+            limited = aa.get("ctrllimited", "auto")
+            mt = servo_classes.get(jd.get("servo"), {}).get("max_torque")
+            if "ctrlrange" in aa and limited != "false":
+                cr = _floats(aa["ctrlrange"], 2)
+                if mt is None or cr != [-mt, mt]:
+                    jd["ctrlrange"] = cr
+            else:
+                jd["ctrlrange"] = [-1e30, 1e30]  # unlimited: the servo's torque is not clamped
+        missing = set(hinges) - seen
+        if missing:
+            raise ValueError(f"hinge joints without an actuator: {sorted(missing)}")
+    # touch sensors (the TouchSensor foot zones, train.py:1511-1516) read the collision box on
+    # the site's body; without a <sensor> section every site on a body with a box is a zone
+    sens = root.find("sensor")
+    touched = {t.get("site") for t in sens.iter("touch")} if sens is not None else None
+    for sd in desc["sites"]:
+        if touched is not None and sd["name"] not in touched:
+            continue
+        box = next((g["name"] for g in desc["geoms"] if g["body"] == sd["body"]), None)
+        if box is not None:
+            sd["touch_geom"] = box
+        elif touched is not None:
+            raise ValueError(f"touch sensor on site {sd['name']}: no collision box on body {sd['body']}")
+    return desc
+
+
+def _fmt(v) -> str:
+    return " ".join(repr(float(x)) for x in v)
+
+
+def to_mjcf(desc: dict) -> str:
+    """Write a descriptor as MJCF (radians, one default class per servo class)."""
+    lines = [f'<mujoco model="{desc.get("name", "zbot")}">', '  <compiler angle="radian"/>']
+    opt = desc.get("option", {})
+    lines.append(f'  <option timestep="{opt.get("timestep", 0.001)!r}" gravity="{_fmt(opt.get("gravity", [0, 0, -9.81]))}"/>')
+    lines.append("  <default>")
+    for cname, sc in desc.get("servo_classes", {}).items():
+        attrs = " ".join(f'{k}="{float(sc[k])!r}"' for k in ("armature", "damping", "frictionloss") if k in sc)
+        lines.append(f'    <default class="{cname}"><joint {attrs}/></default>')
+    lines.append("  </default>")
+    lines.append("  <worldbody>")
+    fl = desc.get("floor", {})
+    fattr = " ".join(f'{k}="{_fmt(fl[k])}"' for k in ("friction", "solref", "solimp") if k in fl)
+    lines.append(f'    <geom name="floor" type="plane" size="0 0 0.05" {fattr} margin="{float(fl.get("margin", 0.0))!r}"/>')
+    root_z = None
+    if any(b["pos"][2] == "auto" for b in desc["bodies"]):
+        from .model import compile_model  # "auto" start height -> the compiled value
+
+        root_z = float(compile_model(desc).qpos0[2])
+    children: dict[str, list[dict]] = {}
+    for b in desc["bodies"]:
+        children.setdefault(b["parent"], []).append(b)
+    geoms: dict[str, list[dict]] = {}
+    for g in desc.get("geoms", []):
+        geoms.setdefault(g["body"], []).append(g)
+    sites: dict[str, list[dict]] = {}
+    for s in desc.get("sites", []):
+        sites.setdefault(s["body"], []).append(s)
+
+    def body(b: dict, ind: str):
+        pos = list(b["pos"])
+        if pos[2] == "auto":
+            pos[2] = root_z
+        q = f' quat="{_fmt(b["quat"])}"' if "quat" in b else ""
+        lines.append(f'{ind}<body name="{b["name"]}" pos="{_fmt(pos)}"{q}>')
+        j = b.get("joint")
+        if j is not None:
+            if j["type"] == "free":
+                lines.append(f'{ind}  <freejoint name="{j["name"]}"/>')
+            else:
+                cls = f' class="{j["servo"]}"' if "servo" in j else ""
+                rng = f' range="{_fmt(j["range"])}"' if "range" in j else ""
+                jp = f' pos="{_fmt(j["pos"])}"' if "pos" in j else ""
+                lines.append(f'{ind}  <joint name="{j["name"]}" type="hinge"{cls} axis="{_fmt(j["axis"])}"{rng}{jp}/>')
+        if "inertia" in b:
+            di = b["inertia"]
+        else:
+            lx, ly, lz = b["box"]
+            m = float(b["mass"])
+            di = [m / 12 * (ly * ly + lz * lz), m / 12 * (lx * lx + lz * lz), m / 12 * (lx * lx + ly * ly)]
+        iq = f' quat="{_fmt(b["iquat"])}"' if "iquat" in b else ""
+        lines.append(f'{ind}  <inertial pos="{_fmt(b.get("ipos", [0, 0, 0]))}"{iq} mass="{float(b["mass"])!r}" '
+                     f'diaginertia="{_fmt(di)}"/>')
+        for g in geoms.get(b["name"], []):
+            gp = f' pos="{_fmt(g["pos"])}"' if "pos" in g else ""
+            gq = f' quat="{_fmt(g["quat"])}"' if "quat" in g else ""
+            lines.append(f'{ind}  <geom name="{g["name"]}" type="box" size="{_fmt(g["size"])}"{gp}{gq}/>')
+        for s in sites.get(b["name"], []):
+            sq = f' quat="{_fmt(s["quat"])}"' if "quat" in s else ""
+            lines.append(f'{ind}  <site name="{s["name"]}" pos="{_fmt(s.get("pos", [0, 0, 0]))}"{sq}/>')
+        for c in children.get(b["name"], []):
+            body(c, ind + "  ")
+        lines.append(f"{ind}</body>")
+
+    for b in children.get("world", []):
+        body(b, "    ")
+    lines.append("  </worldbody>")
+    touch = [sd for sd in desc.get("sites", []) if "touch_geom" in sd]
+    if touch:
+        lines.append("  <sensor>")
+        for sd in touch:
+            lines.append(f'    <touch name="{sd["name"]}_touch" site="{sd["name"]}"/>')
+        lines.append("  </sensor>")
+    lines.append("  <actuator>")
+    for b in desc["bodies"]:
+        j = b.get("joint")
+        if j is not None and j["type"] == "hinge":
+            mt = desc.get("servo_classes", {}).get(j.get("servo"), {}).get("max_torque", 1e6)
+            cr = j.get("ctrlrange", [-mt, mt])
+            lines.append(f'    <motor name="{j["name"]}_ctrl" joint="{j["name"]}" gear="{float(j.get("gear", 1.0))!r}" '
+                         f'ctrllimited="true" ctrlrange="{_fmt(cr)}"/>')
+    lines.append("  </actuator>")
+    lines.append("</mujoco>")
+    return "\n".join(lines) + "\n"
+
+
+if __name__ == "__main__":
+    import argparse
+    import json
+
+    ap = argparse.ArgumentParser(description="convert between MJCF and the zbot_amd robot descriptor")
+    ap.add_argument("src", help="an .xml (MJCF -> descriptor JSON) or .json (descriptor -> MJCF)")
+    ap.add_argument("dst")
+    a = ap.parse_args()
+    if a.src.endswith(".json"):
+        out = to_mjcf(load_description(a.src))
+    else:
+        out = json.dumps(load_mjcf(a.src), indent=1) + "\n"
+    with open(a.dst, "w") as f:
+        f.write(out)

@@ -77,12 +77,15 @@ class Body:
     mass: float
     ipos: np.ndarray
     inertia: np.ndarray
+    iquat: np.ndarray = field(default_factory=lambda: np.array([1.0, 0.0, 0.0, 0.0]))  # inertial frame
     jnt_type: int = cs.JNT_NONE
     jnt_name: str = ""
     axis: np.ndarray = field(default_factory=lambda: np.zeros(3))
     jpos: np.ndarray = field(default_factory=lambda: np.zeros(3))
     jrange: tuple[float, float] | None = None
     servo: dict | None = None
+    gear: float = 1.0  # actuator on this hinge (MJCF <motor gear ctrlrange>)
+    ctrlrange: tuple[float, float] | None = None  # None: +-servo max_torque
     depth: int = 0
     dofadr: int = -1
     dofnum: int = 0
@@ -173,7 +176,7 @@ def mass_matrix(bodies: list[Body], qpos: np.ndarray, nv: int, dof_body, armatur
             continue
         com = xpos[i] + xmat[i] @ b.ipos
         jp, jr = _point_jacobian(bodies, xpos, xmat, nv, dof_body, i, com)
-        Ri = xmat[i] @ quat_to_mat(np.array([1.0, 0, 0, 0]))
+        Ri = xmat[i] @ quat_to_mat(b.iquat)
         Iw = Ri @ np.diag(b.inertia) @ Ri.T
         M += b.mass * jp.T @ jp + jr.T @ Iw @ jr
     return M
@@ -218,6 +221,9 @@ def compile_model(desc: dict | str | None = None) -> CompiledModel:
             if "inertia" in bd
             else _box_inertia(float(bd["mass"]), bd["box"]),
         )
+        if "iquat" in bd:  # principal axes of the inertia (MJCF <inertial quat>)
+            iq = np.array(bd["iquat"], dtype=np.float64)
+            b.iquat = iq / np.linalg.norm(iq)
         j = bd.get("joint")
         if j is not None:
             b.jnt_name = j["name"]
@@ -232,6 +238,8 @@ def compile_model(desc: dict | str | None = None) -> CompiledModel:
                 b.jpos = np.array(j.get("pos", [0.0, 0.0, 0.0]), dtype=np.float64)
                 b.jrange = tuple(j["range"]) if "range" in j else None
                 b.servo = servo_classes[j["servo"]] if "servo" in j else None
+                b.gear = float(j.get("gear", 1.0))
+                b.ctrlrange = tuple(float(x) for x in j["ctrlrange"]) if "ctrlrange" in j else None
             else:
                 raise ValueError(f"unsupported joint type {j['type']}")
         names[b.name] = len(bodies)
@@ -378,7 +386,8 @@ def compile_model(desc: dict | str | None = None) -> CompiledModel:
             m.jnt_pos[i][k] = b.jpos[k]
         for k in range(4):
             m.body_quat[i][k] = b.quat[k]
-        m.body_iquat[i][0] = 1.0
+        for k in range(4):
+            m.body_iquat[i][k] = b.iquat[k]
         m.body_mass[i][0] = b.mass
         m.body_invweight0[i][0] = body_invweight[i, 0]
         m.body_invweight0[i][1] = body_invweight[i, 1]
@@ -424,10 +433,11 @@ def compile_model(desc: dict | str | None = None) -> CompiledModel:
     for a, b in enumerate(hinge_bodies):
         s = b.servo or {}
         m.act_dof[a] = b.dofadr
-        m.act_gear[a] = 1.0
+        m.act_gear[a] = b.gear
         mt = s.get("max_torque", 1e6)
-        m.act_ctrlrange[a][0] = -mt
-        m.act_ctrlrange[a][1] = mt
+        cr = b.ctrlrange if b.ctrlrange is not None else (-mt, mt)
+        m.act_ctrlrange[a][0] = cr[0]
+        m.act_ctrlrange[a][1] = cr[1]
         m.fe_kp[a] = s.get("kp", 0.0)
         m.fe_kd[a] = s.get("kd", 0.0)
         m.fe_error_gain[a] = s.get("error_gain", 1.0)
