@@ -271,6 +271,41 @@ def test_ksim_shaped_env(torch_gpu, cmodel):
     assert stats["episodes"] >= 0
 
 
+def test_mjcf_variant_model_parity(torch_gpu, cmodel_mjcf, oracle_mod):
+    """A model imported through zbot_amd.mjcf with rotated inertial frames, geom-derived arm
+    inertia, a gear of 1.25 and an asymmetric ctrlrange (conftest.mjcf_variant_desc) steps like
+    the oracle on the same model (tolerances as test_one_step_parity)."""
+    torch = torch_gpu
+    cm = cmodel_mjcf
+    cfg = default_config()
+    n = 32
+    env = warm_states(oracle_mod, cm, cfg, n, steps=8)
+    eng = engine(cm, cfg, n, seed=7)
+    dbg_st = env.state.copy()
+    ctrl = (np.random.default_rng(1).normal(size=(n, 20)) * 1.5).astype(np.float32)
+    from zbot_amd.engine import DBG
+
+    g = eng.debug_forward(torch.from_numpy(dbg_st), torch.from_numpy(ctrl)).cpu().numpy()
+    for e in range(0, n, 7):
+        ref = oracle_mod.forward_debug(cm.cmodel, cfg, dbg_st[e, :27], dbg_st[e, 32:58], ctrl[e], precision="f64")
+        assert close(g[e, DBG["qM"]:DBG["qM"] + 26 * 26].reshape(26, 26), ref["qM"], 1e-3).all(), e
+        assert close(g[e, DBG["bias"]:DBG["bias"] + 26], ref["qfrc_bias"], 1e-2).all(), e
+        assert close(g[e, DBG["qacc_smooth"]:DBG["qacc_smooth"] + 26], ref["qacc_smooth"], 10.0).all(), e
+    for t in range(2):
+        eng.set_state(torch.from_numpy(env.state.copy()))
+        eng.set_rand(torch.from_numpy(env.rand.copy()))
+        a = oracle_mod.synthetic_actions(cm.cmodel, 7, n, 0, 100 + t)
+        ref = env.step(a)
+        out = eng.step(torch.from_numpy(a).cuda())
+        torch.cuda.synchronize()
+        gs = eng.get_state().cpu().numpy()
+        np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
+        np.testing.assert_allclose(gs[:, :27], env.state[:, :27], atol=1e-4)
+        np.testing.assert_allclose(gs[:, 32:58], env.state[:, 32:58], atol=1e-2)
+        np.testing.assert_allclose(out["obs_actor"].cpu().numpy(), ref["obs_actor"], atol=1e-3)
+        np.testing.assert_allclose(out["reward"].cpu().numpy(), ref["reward"], atol=1e-3)
+
+
 def test_team_divergence_is_exact(torch_gpu, cmodel, oracle_mod):
     """The two envs of a wavefront (teams 2k, 2k+1) are independent: an odd env count, a
     masked reset and a single-team auto-reset give the bits of the unconstrained runs.

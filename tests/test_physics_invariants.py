@@ -72,6 +72,27 @@ def test_gravity_bias_matches_jacobian_form(oracle_mod, cmodel, seed):
     np.testing.assert_allclose(d["qfrc_bias"], bias, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+def test_mjcf_variant_dynamics_match_jacobian_form(oracle_mod, cmodel_mjcf, seed):
+    """A model imported from MJCF with rotated inertial frames and geom-derived inertia
+    (conftest.mjcf_variant_desc): the oracle's mass matrix and gravity bias still equal the
+    independent Jacobian forms, so body_iquat is honoured end to end."""
+    cm = cmodel_mjcf
+    assert any(list(cm.cmodel.body_iquat[i]) != [1.0, 0.0, 0.0, 0.0] for i in range(len(cm.bodies)))
+    rng = np.random.default_rng(seed)
+    q = _random_qpos(cm, rng)
+    d = oracle_mod.forward_debug(cm.cmodel, default_config(), q, np.zeros(26), precision="f64")
+    arm = np.array([cm.cmodel.dof_armature[i] for i in range(26)])
+    np.testing.assert_allclose(d["qM"], mass_matrix(cm.bodies, q, 26, cm.dof_body, arm), rtol=1e-5, atol=1e-7)
+    xpos, xmat = _kinematics(cm.bodies, q)
+    bias = np.zeros(26)
+    for i, b in enumerate(cm.bodies):
+        if i:
+            jp, _ = _point_jacobian(cm.bodies, xpos, xmat, 26, cm.dof_body, i, xpos[i] + xmat[i] @ b.ipos)
+            bias -= b.mass * jp.T @ np.array([0.0, 0.0, -9.81])
+    np.testing.assert_allclose(d["qfrc_bias"], bias, rtol=1e-5, atol=1e-6)
+
+
 def _conservative_model(cmodel):
     m = _model_copy(cmodel.cmodel)
     for i in range(26):
