@@ -102,3 +102,33 @@ def test_policy_in_the_rollout_loop(pol, cmodel):
     assert np.isfinite(r["actions"]).all() and np.isfinite(r["reward"]).all() and np.isfinite(r["log_prob"]).all()
     assert r["obs_actor"].shape == (7, 64, 50)
     assert not np.array_equal(r["actions"][0, 0], r["actions"][0, 1])
+
+
+def test_kinfer_step_matches_gpu_actor(pol):
+    """The exported deployment step (zbot_amd.kinfer.ActorStep) and the GPU actor
+    in MODE agree on the same observations and carries (tolerance: fp32 eager vs the matrix-core
+    k-ordered chain, 2e-5)."""
+    from zbot_amd import kinfer as K
+
+    P = init_params(ACTOR, seed=5)
+    rng = np.random.default_rng(4)
+    off = K.param_count(ACTOR) - K.JOINTS - K.ACTOR_OUT  # b_out: spread the logits (no near-ties)
+    P[off + 200:off + 300] += rng.normal(scale=2.0, size=100).astype(np.float32)
+    step = K.ActorStep(P)
+    n = 16
+    obs, carry = [], []
+    for _ in range(n):
+        q = rng.normal(size=4)
+        xs = (rng.uniform(-1, 1, 20), rng.normal(size=20), q, rng.uniform(-3, 3, 1), rng.uniform(-1, 1, 6))
+        obs.append(step.observation(*(torch.tensor(x, dtype=torch.float32) for x in xs)))
+        carry.append(torch.tensor(0.5 * rng.normal(size=(D, H)), dtype=torch.float32))
+    obs, carry = torch.stack(obs), torch.stack(carry)
+    with torch.no_grad():
+        ref = [step.act(obs[e], carry[e]) for e in range(n)]
+    g = pol.GruPolicy(ACTOR, P)
+    c = carry.cuda().contiguous()
+    a, _ = g.actor(obs.cuda(), c, mode=MODE)
+    torch.cuda.synchronize()
+    for e in range(n):
+        np.testing.assert_allclose(a[e].cpu().numpy(), ref[e][0].numpy(), rtol=0, atol=2e-5)
+        np.testing.assert_allclose(c[e].cpu().numpy(), ref[e][1].numpy(), rtol=0, atol=2e-5)
