@@ -52,15 +52,15 @@ ZBF_FN float zbf_exp(float x) {
   return ldexpf(p, (int)n);
 }
 
-/* natural log for x > 0 (x <= 0 returns -87.3, the log of the smallest value zbf_exp makes) */
+/* natural log for x > 0 (x <= 0 returns -87.3, the log of the smallest value zbf_exp makes).
+   Branch-free (selects), so a wavefront's lanes never diverge inside it. */
 ZBF_FN float zbf_log(float x) {
-  if (!(x > 0.0f)) return -87.3365447f;
+  const int bad = !(x > 0.0f);
   int e;
-  float m = frexpf(x, &e); /* x = m 2^e, m in [0.5, 1) */
-  if (m < 0.70710678f) {
-    m = m * 2.0f;
-    e = e - 1;
-  }
+  float m = frexpf(bad ? 1.0f : x, &e); /* x = m 2^e, m in [0.5, 1) */
+  const int lo = m < 0.70710678f;
+  m = lo ? m * 2.0f : m;
+  e = lo ? e - 1 : e;
   /* log m = 2 atanh(s), s = (m - 1) / (m + 1), |s| < 0.1716 */
   const float s = (m - 1.0f) / (m + 1.0f);
   const float s2 = s * s;
@@ -72,7 +72,8 @@ ZBF_FN float zbf_log(float x) {
   p = fmaf(p, s2, 0.66666669e0f);
   const float lm = fmaf(s * s2, p, 2.0f * s);
   const float fe = (float)e;
-  return fmaf(fe, ZBF_LN2_HI, fmaf(fe, ZBF_LN2_LO, lm));
+  const float r = fmaf(fe, ZBF_LN2_HI, fmaf(fe, ZBF_LN2_LO, lm));
+  return bad ? -87.3365447f : r;
 }
 
 ZBF_FN float zbf_sigmoid(float x) { return 1.0f / (1.0f + zbf_exp(-x)); }
@@ -80,16 +81,16 @@ ZBF_FN float zbf_sigmoid(float x) { return 1.0f / (1.0f + zbf_exp(-x)); }
 /* tanh(x) = sign(x) (1 - 2 / (e^{2|x|} + 1)); |x| < 2^-12 returns x */
 ZBF_FN float zbf_tanh(float x) {
   const float ax = fabsf(x);
-  if (ax < 2.44140625e-4f) return x;
   const float t = 1.0f - 2.0f / (zbf_exp(2.0f * ax) + 1.0f);
-  return x < 0.0f ? -t : t;
+  return ax < 2.44140625e-4f ? x : (x < 0.0f ? -t : t);
 }
 
 /* log(1 + y), y >= 0: log(u) * y / (u - 1) with u = 1 + y corrects the rounding of u */
 ZBF_FN float zbf_log1p(float y) {
   const float u = 1.0f + y;
-  if (u == 1.0f) return y;
-  return zbf_log(u) * (y / (u - 1.0f));
+  const float d = u - 1.0f;
+  const float r = zbf_log(u) * (y / (d == 0.0f ? 1.0f : d));
+  return u == 1.0f ? y : r;
 }
 
 /* softplus(x) = max(x, 0) + log1p(e^{-|x|})  (jax.nn.softplus = logaddexp(x, 0)) */
@@ -211,13 +212,13 @@ ZBF_FN float zbf_mix_sample(const float* mu, const float* sd, const float* lg, i
   zbf_rng_bits(seed, purpose, k_cat, env, step, &a, &b);
   const float target = zbf_u01(a) * S;
   int pick = ZBF_NMIX - 1;
+  int found = 0;
   float c = 0.0f;
-  for (int m = 0; m < ZBF_NMIX; m++) {
+  for (int m = 0; m < ZBF_NMIX; m++) { /* first m with target < c_m, as selects */
     c = c + e[m];
-    if (target < c) {
-      pick = m;
-      break;
-    }
+    const int hit = !found && target < c;
+    pick = hit ? m : pick;
+    found = found || hit;
   }
   const float z = zbf_normal(seed, purpose, k_normal, env, step);
   return mu[pick] + sd[pick] * z;

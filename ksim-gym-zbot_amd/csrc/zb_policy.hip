@@ -19,8 +19,9 @@
  *   [tile][group of 4 k-steps][lane][4] — so each lane streams one 16-B load
  *   per 4 MFMA steps per matrix; every workgroup reads the whole weight set
  *   (2.0 MB actor, 2.2 MB critic), which stays L2-resident across the chip.
- *   The carry of layer l is read from HBM at the layer's start and written at
- *   its end ([n][5][128] fp32, 2.5 KB per env per step).
+ *   The carry of layer l + 1 is loaded from HBM into registers while layer l
+ *   runs (its latency hides behind the MFMAs) and layer l's new carry is
+ *   written at its end ([n][5][128] fp32, 2.5 KB per env per step).
  *
  * Numerics (bit-identical to the oracle): every product is the matrix core's
  * k-ordered fp32 fmaf chain from 0, biases are added afterwards, elementwise
@@ -116,20 +117,33 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   const size_t off_gru = (size_t)(H / 32) * GIN * 64;  /* float4 offset of layer 0's W_ih pack */
   constexpr size_t MAT = (size_t)12 * GH * 64;         /* one packed [3H][H] matrix, float4 */
   int cur = 0;
-  for (int l = 0; l < D; ++l) {
-    /* carry of layer l -> sh; zero for envs whose episode restarts at this step */
-    for (int i = tid; i < M * (H / 4); i += NTHR) {
+  constexpr int CPT = M * (H / 4) / NTHR;
+  float4 cr[CPT];
+  auto load_carry = [&](int l) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int i = tid + j * NTHR;
       const int e = i / (H / 4), q = i - e * (H / 4);
       const int ge = e0 + e;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      cr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (ge < a.n && !(a.reset && a.reset[ge]))
-        v = *reinterpret_cast<const float4*>(a.carry + ((size_t)ge * D + l) * H + 4 * q);
-      sh[(4 * q) * LDA + e] = v.x;
-      sh[(4 * q + 1) * LDA + e] = v.y;
-      sh[(4 * q + 2) * LDA + e] = v.z;
-      sh[(4 * q + 3) * LDA + e] = v.w;
+        cr[j] = *reinterpret_cast<const float4*>(a.carry + ((size_t)ge * D + l) * H + 4 * q);
+    }
+  };
+  load_carry(0);
+  for (int l = 0; l < D; ++l) {
+    /* carry of layer l (prefetched during layer l - 1) -> sh */
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int i = tid + j * NTHR;
+      const int e = i / (H / 4), q = i - e * (H / 4);
+      sh[(4 * q) * LDA + e] = cr[j].x;
+      sh[(4 * q + 1) * LDA + e] = cr[j].y;
+      sh[(4 * q + 2) * LDA + e] = cr[j].z;
+      sh[(4 * q + 3) * LDA + e] = cr[j].w;
     }
     __syncthreads();
+    if (l + 1 < D) load_carry(l + 1);
 
     const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
     const float4* whh = wih + MAT;
