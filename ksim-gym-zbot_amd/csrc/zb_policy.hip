@@ -68,6 +68,7 @@ __device__ __forceinline__ f32x16 tile_gemm(const float* xs, const float4* wp, i
   float4 b = wp[0];
   for (int g = 0; g < G; ++g) {
     const float4 bn = wp[(size_t)(g + 1 < G ? g + 1 : g) * 64];
+    __builtin_amdgcn_sched_barrier(0); /* next group's load stays a group ahead */
     const float* xp = xs + (8 * g + h2) * LDA + c32;
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc = mma(xp[2 * u * LDA], q4(b, u), acc);
@@ -156,6 +157,9 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
       const size_t gn = (size_t)(g + 1 < GH ? g + 1 : g) * 64;
       const float4 n0 = wih[tr + gn], n1 = wih[tz + gn], n2 = wih[tn + gn];
       const float4 n3 = whh[tr + gn], n4 = whh[tz + gn], n5 = whh[tn + gn];
+      /* keep the next group's loads here, a whole group (24 MFMAs) ahead of their use: the
+         fully unrolled loop otherwise lets the scheduler sink them next to their first MFMA */
+      __builtin_amdgcn_sched_barrier(0);
       const float* xp = xs + (8 * g + h2) * LDA + c32;
       const float* hp = sh + (8 * g + h2) * LDA + c32;
 #pragma unroll

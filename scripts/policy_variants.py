@@ -78,12 +78,37 @@ def _prefetch(s):
     return s[:a] + PF_BODY_NEW + s[b:]
 
 
+GLOOP = "    for (int g = 0; g < GH; ++g) {"
+TLOOP = "  for (int g = 0; g < G; ++g) {"
+TLOAD_END = "    const float4 bn = wp[(size_t)(g + 1 < G ? g + 1 : g) * 64];"
+LOOP_OLD = """      const float* xp = xs + (8 * g + h2) * LDA + c32;
+      const float* hp = sh + (8 * g + h2) * LDA + c32;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float ax = xp[2 * u * LDA], ah = hp[2 * u * LDA];"""
+GLOAD_END = "      const float4 n3 = whh[tr + gn], n4 = whh[tz + gn], n5 = whh[tn + gn];"
+
 VARIANTS = {
     "base": [],
     "nocarryload": [(CARRY_LOAD, NO_CARRY_LOAD)],
     "noepi": [(EPI, NO_EPI)],
     "nohead": [(HEAD, NO_HEAD)],
     "prefetch": "prefetch",  # adopted into the product in r01_v17
+    # (r01_v17: "unroll1"/"unroll2" 150/143 us, "schedbar2" 111 us vs 119 -> adopted)
+    # A operands (LDS) of the next group read one group ahead, like the weights
+    "ldsahead": [("    for (int g = 0; g < GH; ++g) {\n      const size_t gn",
+                  "    float axs[4], ahs[4];\n#pragma unroll\n    for (int u = 0; u < 4; ++u) {\n"
+                  "      axs[u] = xs[(h2 + 2 * u) * LDA + c32];\n      ahs[u] = sh[(h2 + 2 * u) * LDA + c32];\n    }\n"
+                  "    for (int g = 0; g < GH; ++g) {\n      const size_t gn"),
+                 (GLOAD_END, GLOAD_END + "\n      const int gq = g + 1 < GH ? g + 1 : g;\n      float axn[4], ahn[4];\n"
+                  "#pragma unroll\n      for (int u = 0; u < 4; ++u) {\n"
+                  "        axn[u] = xs[(8 * gq + h2 + 2 * u) * LDA + c32];\n"
+                  "        ahn[u] = sh[(8 * gq + h2 + 2 * u) * LDA + c32];\n      }"),
+                 (LOOP_OLD, "#pragma unroll\n      for (int u = 0; u < 4; ++u) {\n        const float ax = axs[u], ah = ahs[u];"),
+                 ("      b0 = n0; b1 = n1; b2 = n2; b3 = n3; b4 = n4; b5 = n5;\n",
+                  "      b0 = n0; b1 = n1; b2 = n2; b3 = n3; b4 = n4; b5 = n5;\n#pragma unroll\n"
+                  "      for (int u = 0; u < 4; ++u) { axs[u] = axn[u]; ahs[u] = ahn[u]; }\n")],
+    "base2": [],
 }
 
 
@@ -122,7 +147,7 @@ def run():
     dev = torch.device("cuda", 0)
     P = np.ascontiguousarray(init_params(ACTOR, 0), dtype=np.float32)
     obs = torch.randn(n, 50, device=dev)
-    ref = None
+    libs = {}
     for name in VARIANTS:
         L = C.CDLL(os.path.join(OUT, f"libpol_{name}.so"))
         vp = C.c_void_p
@@ -131,26 +156,39 @@ def run():
                                       vp, vp, vp]
         h = vp()
         assert L.zb_policy_create(ACTOR, P.ctypes.data, P.size, 0, C.byref(h)) == 0
-        carry = torch.zeros(n, 5, 128, device=dev)
-        act = torch.empty(n, 20, device=dev)
-        lp = torch.empty(n, 20, device=dev)
-        ts = []
-        for rep in range(30):
-            if rep == 1:
-                carry.zero_()
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            assert L.zb_policy_actor(h, obs.data_ptr(), 1, n, carry.data_ptr(), None, 0, 7, 0, rep, act.data_ptr(),
-                                     lp.data_ptr(), None) == 0
-            b.record()
-            torch.cuda.synchronize()
-            ts.append(a.elapsed_time(b) * 1e3)
-        ts = sorted(ts[3:])
-        same = None
-        if name == "base":
-            ref = (act.clone(), carry.clone())
-        elif name == "prefetch":
-            same = bool(torch.equal(act, ref[0]) and torch.equal(carry, ref[1]))
+        libs[name] = (L, h)
+    carry = torch.zeros(n, 5, 128, device=dev)
+    act = torch.empty(n, 20, device=dev)
+    lp = torch.empty(n, 20, device=dev)
+
+    def launch(name, step):
+        L, h = libs[name]
+        assert L.zb_policy_actor(h, obs.data_ptr(), 1, n, carry.data_ptr(), None, 0, 7, 0, step, act.data_ptr(),
+                                 lp.data_ptr(), None) == 0
+
+    # clocks up: ~2 s of back-to-back launches before anything is timed
+    for i in range(15000):
+        launch("base", i)
+    torch.cuda.synchronize()
+    times = {name: [] for name in VARIANTS}
+    outs = {}
+    for rnd in range(4):  # round-robin, so drift hits every variant alike
+        for name in VARIANTS:
+            carry.zero_()
+            ts = []
+            for rep in range(25):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                launch(name, rep)
+                b.record()
+                torch.cuda.synchronize()
+                ts.append(a.elapsed_time(b) * 1e3)
+            times[name] += ts[5:]
+            if rnd == 0:
+                outs[name] = (act.clone(), carry.clone())
+    for name in VARIANTS:
+        ts = sorted(times[name])
+        same = bool(torch.equal(outs[name][0], outs["base"][0]) and torch.equal(outs[name][1], outs["base"][1]))
         print(json.dumps(dict(variant=name, n=n, us=ts[len(ts) // 2], us_min=ts[0], bit_identical_to_base=same)),
               flush=True)
 
