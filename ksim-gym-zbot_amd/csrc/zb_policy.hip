@@ -97,6 +97,21 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   const int unit = 32 * w + c32;
   const float4* wp4 = reinterpret_cast<const float4*>(a.wpack);
 
+  constexpr int CPT = M * (H / 4) / NTHR;
+  float4 cr[CPT];
+  auto load_carry = [&](int l) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int i = tid + j * NTHR;
+      const int e = i / (H / 4), q = i - e * (H / 4);
+      const int ge = e0 + e;
+      cr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ge < a.n && !(a.reset && a.reset[ge]))
+        cr[j] = *reinterpret_cast<const float4*>(a.carry + ((size_t)ge * D + l) * H + 4 * q);
+    }
+  };
+  load_carry(0); /* layer 0's carry loads overlap the observation tile and input projection */
+
   /* 1. observation tile, zero-padded to KPAD (consecutive threads: consecutive k of an env) */
   for (int i = tid; i < M * KPAD; i += NTHR) {
     const int e = i / KPAD, k = i - e * KPAD;
@@ -118,20 +133,6 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   const size_t off_gru = (size_t)(H / 32) * GIN * 64;  /* float4 offset of layer 0's W_ih pack */
   constexpr size_t MAT = (size_t)12 * GH * 64;         /* one packed [3H][H] matrix, float4 */
   int cur = 0;
-  constexpr int CPT = M * (H / 4) / NTHR;
-  float4 cr[CPT];
-  auto load_carry = [&](int l) {
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      const int i = tid + j * NTHR;
-      const int e = i / (H / 4), q = i - e * (H / 4);
-      const int ge = e0 + e;
-      cr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ge < a.n && !(a.reset && a.reset[ge]))
-        cr[j] = *reinterpret_cast<const float4*>(a.carry + ((size_t)ge * D + l) * H + 4 * q);
-    }
-  };
-  load_carry(0);
   for (int l = 0; l < D; ++l) {
     /* carry of layer l (prefetched during layer l - 1) -> sh */
 #pragma unroll
