@@ -88,26 +88,20 @@ LOOP_OLD = """      const float* xp = xs + (8 * g + h2) * LDA + c32;
         const float ax = xp[2 * u * LDA], ah = hp[2 * u * LDA];"""
 GLOAD_END = "      const float4 n3 = whh[tr + gn], n4 = whh[tz + gn], n5 = whh[tn + gn];"
 
+def _sgb(nvalu):
+    return [("        epi_row(g);\n", "        epi_row(g);\n#pragma unroll\n        for (int k = 0; k < 12; ++k) {\n"
+             "          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);\n"
+             f"          __builtin_amdgcn_sched_group_barrier(0x002, {nvalu}, 0);\n        }}\n")]
+
+
 VARIANTS = {
     "base": [],
-    "nocarryload": [(CARRY_LOAD, NO_CARRY_LOAD)],
     "noepi": [(EPI, NO_EPI)],
     "nohead": [(HEAD, NO_HEAD)],
-    "prefetch": "prefetch",  # adopted into the product in r01_v17
-    # (r01_v17: "unroll1"/"unroll2" 150/143 us, "schedbar2" 111 us vs 119 -> adopted)
-    # A operands (LDS) of the next group read one group ahead, like the weights
-    "ldsahead": [("    for (int g = 0; g < GH; ++g) {\n      const size_t gn",
-                  "    float axs[4], ahs[4];\n#pragma unroll\n    for (int u = 0; u < 4; ++u) {\n"
-                  "      axs[u] = xs[(h2 + 2 * u) * LDA + c32];\n      ahs[u] = sh[(h2 + 2 * u) * LDA + c32];\n    }\n"
-                  "    for (int g = 0; g < GH; ++g) {\n      const size_t gn"),
-                 (GLOAD_END, GLOAD_END + "\n      const int gq = g + 1 < GH ? g + 1 : g;\n      float axn[4], ahn[4];\n"
-                  "#pragma unroll\n      for (int u = 0; u < 4; ++u) {\n"
-                  "        axn[u] = xs[(8 * gq + h2 + 2 * u) * LDA + c32];\n"
-                  "        ahn[u] = sh[(8 * gq + h2 + 2 * u) * LDA + c32];\n      }"),
-                 (LOOP_OLD, "#pragma unroll\n      for (int u = 0; u < 4; ++u) {\n        const float ax = axs[u], ah = ahs[u];"),
-                 ("      b0 = n0; b1 = n1; b2 = n2; b3 = n3; b4 = n4; b5 = n5;\n",
-                  "      b0 = n0; b1 = n1; b2 = n2; b3 = n3; b4 = n4; b5 = n5;\n#pragma unroll\n"
-                  "      for (int u = 0; u < 4; ++u) { axs[u] = axn[u]; ahs[u] = ahn[u]; }\n")],
+    # r01_v18 experiment: hh(l+1) MFMAs interleaved with layer l's epilogue (cross-layer
+    # software pipeline, 3 carry buffers). Bit-identical, 110.9 us vs 110.0 for the product:
+    # an f32 MFMA and the same wave's VALU do not overlap measurably (profiles/r01_v18_*).
+    "pipelined": "file:" + os.environ.get("ZB_POL_PIPELINED", os.path.join(OUT, "zb_policy_pipelined.hip")),
     "base2": [],
 }
 
@@ -119,6 +113,8 @@ def build():
     for name, patches in VARIANTS.items():
         if patches == "prefetch":
             s = _prefetch(src)
+        elif isinstance(patches, str) and patches.startswith("file:"):
+            s = open(patches[5:]).read()
         else:
             s = src
             for a, b in patches:
