@@ -205,7 +205,8 @@ def main() -> None:
     cfg = default_config(push=conf["push"], randomize=conf["randomize"])
     eng = HipEngine(cm, cfg, n, env_offset=rank * n, device=local_rank, seed=args.seed)
 
-    # synthetic policy outputs, generated before timing (policy is out of scope)
+    # synthetic actions for the headline env-step leg, generated before timing (the
+    # policy-in-the-loop leg below drives the same engine with the GRU actor instead)
     T = args.warmup + args.steps
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
