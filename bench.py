@@ -169,6 +169,54 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int) -> dict:
     }
 
 
+def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> dict:
+    """One PPO rollout per GPU end to end, everything before the PPO loss (SURVEY §8f f1 + f2):
+    T control steps of GRU-actor sampling -> zb_step with the critic observations recorded
+    (ksim rollout, sample_action train.py:1737-1763), the GRU critic over the T steps with the
+    carry reset on episode ends (get_ppo_variables, train.py:1683-1729), then GAE, value targets
+    and advantage normalization with the batch moments combined over RCCL (ksim
+    compute_ppo_inputs [U]). Value: env-steps of the whole job per second of wall time."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+    from zbot_amd import policy as P  # noqa: PLC0415
+    from zbot_amd.ppo import compute_ppo_inputs  # noqa: PLC0415
+
+    actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), device=dev.index)
+    critic = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=1), device=dev.index)
+    ro = P.PolicyRollout(eng, actor, seed=3)
+    ro.reset()
+    zeros = torch.zeros(1, n, dtype=torch.uint8, device=dev)
+
+    def once():
+        traj = ro.run(T, record_critic=True)
+        values = critic.critic(traj["obs_critic"], critic.initial_carry(n),
+                               reset=torch.cat([zeros, traj["done"][:-1]]))
+        return compute_ppo_inputs(values, traj["reward"], traj["done"])
+
+    once()  # first use of every kernel and of the moment collective, untimed
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = once()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    wall = float(wall.item())
+    assert bool(torch.isfinite(res.advantages_t).all())
+    return {
+        "workload": f"per GPU: {T}-step rollout of {n} envs with the GRU actor sampling every action, the GRU "
+                    "critic over the rollout, GAE + value targets + advantage normalization (moments over RCCL)",
+        "env_steps_per_s": world * n * T * reps / wall,
+        "ms_per_rollout": 1e3 * wall / reps,
+        "rollout_steps": T,
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,6 +229,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
     ap.add_argument("--no-policy", action="store_true", help="skip the policy-in-the-loop leg")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end rollout-pipeline leg")
     args = ap.parse_args()
 
     import torch  # noqa: PLC0415
@@ -273,6 +322,7 @@ def main() -> None:
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
     policy_leg = None if args.no_policy else bench_policy_in_loop(eng, n, 16, dev, rank)
+    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(eng, n, 32, 2, dev, world)
 
     if rank == 0:
         value = world * n * args.steps / elapsed
@@ -328,6 +378,8 @@ def main() -> None:
             out["ppo_inputs"] = ppo_leg
         if policy_leg is not None:
             out["policy_in_loop"] = policy_leg
+        if pipe_leg is not None:
+            out["rollout_pipeline"] = pipe_leg
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper())
         print(json.dumps(out), flush=True)
