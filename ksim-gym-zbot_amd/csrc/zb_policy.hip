@@ -112,12 +112,51 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   };
   load_carry(0); /* layer 0's carry loads overlap the observation tile and input projection */
 
-  /* 1. observation tile, zero-padded to KPAD (consecutive threads: consecutive k of an env) */
-  for (int i = tid; i < M * KPAD; i += NTHR) {
-    const int e = i / KPAD, k = i - e * KPAD;
-    float v = 0.f;
-    if (k < KIN && e0 + e < a.n) v = a.obs[(size_t)(e0 + e) * KIN + k];
-    su[k * LDA + e] = v;
+  /* 1. observation tile [k][env], zero-padded to KPAD. The block's 32 observation rows are one
+        contiguous chunk of M * KIN floats: stream it with 16-B loads, all issued before the
+        first LDS store (a load-then-store loop would wait out one HBM round trip per pass:
+        61 passes for the critic's 484 features). */
+  {
+    constexpr int FL = M * KIN, NV4 = (FL + 3) / 4, PASSES = (NV4 + NTHR - 1) / NTHR;
+    const int lim = (a.n - e0 < M ? a.n - e0 : M) * KIN; /* valid floats of this block */
+    const float* src = a.obs + (size_t)e0 * KIN;
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      float4 v[PASSES];
+#pragma unroll
+      for (int p = 0; p < PASSES; ++p) {
+        const int i4 = tid + p * NTHR;
+        v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (4 * i4 + 3 < lim) {
+          v[p] = reinterpret_cast<const float4*>(src)[i4];
+        } else if (4 * i4 < lim) {
+          v[p].x = src[4 * i4];
+          if (4 * i4 + 1 < lim) v[p].y = src[4 * i4 + 1];
+          if (4 * i4 + 2 < lim) v[p].z = src[4 * i4 + 2];
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < PASSES; ++p) {
+        const int i4 = tid + p * NTHR;
+        const float c4[4] = {v[p].x, v[p].y, v[p].z, v[p].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int f = 4 * i4 + c;
+          if (f < FL) {
+            const int e = f / KIN, k = f - e * KIN;
+            su[k * LDA + e] = c4[c]; /* zero past the last env */
+          }
+        }
+      }
+    } else {
+      for (int i = tid; i < FL; i += NTHR) {
+        const int e = i / KIN, k = i - e * KIN;
+        su[k * LDA + e] = i < lim ? src[i] : 0.f;
+      }
+    }
+    for (int i = tid; i < M * (KPAD - KIN); i += NTHR) { /* padding rows k = KIN .. KPAD - 1 */
+      const int k = KIN + i / M, e = i - (i / M) * M;
+      su[k * LDA + e] = 0.f;
+    }
   }
   __syncthreads();
 

@@ -96,12 +96,8 @@ def _sgb(nvalu):
 
 VARIANTS = {
     "base": [],
-    "noepi": [(EPI, NO_EPI)],
-    "nohead": [(HEAD, NO_HEAD)],
-    # r01_v18 experiment: hh(l+1) MFMAs interleaved with layer l's epilogue (cross-layer
-    # software pipeline, 3 carry buffers). Bit-identical, 110.9 us vs 110.0 for the product:
-    # an f32 MFMA and the same wave's VALU do not overlap measurably (profiles/r01_v18_*).
-    "pipelined": "file:" + os.environ.get("ZB_POL_PIPELINED", os.path.join(OUT, "zb_policy_pipelined.hip")),
+    # the product before the 16-B observation staging (r01_v18): ZB_POL_OLD or variants/zb_policy_v17.hip
+    "v17": "file:" + os.environ.get("ZB_POL_OLD", os.path.join(OUT, "zb_policy_v17.hip")),
     "base2": [],
 }
 
@@ -137,12 +133,13 @@ def run():
     import torch
 
     sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
-    from zbot_amd.policy import ACTOR, init_params
+    from zbot_amd.policy import ACTOR, CRITIC, init_params
 
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
     dev = torch.device("cuda", 0)
-    P = np.ascontiguousarray(init_params(ACTOR, 0), dtype=np.float32)
-    obs = torch.randn(n, 50, device=dev)
+    KIND = CRITIC if os.environ.get("ZB_POL_KIND") == "critic" else ACTOR
+    P = np.ascontiguousarray(init_params(KIND, 0), dtype=np.float32)
+    obs = torch.randn(n, 50 if KIND == ACTOR else 484, device=dev)
     libs = {}
     for name in VARIANTS:
         L = C.CDLL(os.path.join(OUT, f"libpol_{name}.so"))
@@ -150,8 +147,9 @@ def run():
         L.zb_policy_create.argtypes = [C.c_int, vp, C.c_size_t, C.c_int, C.POINTER(vp)]
         L.zb_policy_actor.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_uint64, C.c_int, C.c_uint32,
                                       vp, vp, vp]
+        L.zb_policy_critic.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, vp]
         h = vp()
-        assert L.zb_policy_create(ACTOR, P.ctypes.data, P.size, 0, C.byref(h)) == 0
+        assert L.zb_policy_create(KIND, P.ctypes.data, P.size, 0, C.byref(h)) == 0
         libs[name] = (L, h)
     carry = torch.zeros(n, 5, 128, device=dev)
     act = torch.empty(n, 20, device=dev)
@@ -159,8 +157,11 @@ def run():
 
     def launch(name, step):
         L, h = libs[name]
-        assert L.zb_policy_actor(h, obs.data_ptr(), 1, n, carry.data_ptr(), None, 0, 7, 0, step, act.data_ptr(),
-                                 lp.data_ptr(), None) == 0
+        if KIND == ACTOR:
+            assert L.zb_policy_actor(h, obs.data_ptr(), 1, n, carry.data_ptr(), None, 0, 7, 0, step,
+                                     act.data_ptr(), lp.data_ptr(), None) == 0
+        else:
+            assert L.zb_policy_critic(h, obs.data_ptr(), 1, n, carry.data_ptr(), None, act.data_ptr(), None) == 0
 
     # clocks up: ~2 s of back-to-back launches before anything is timed
     for i in range(15000):
@@ -185,7 +186,7 @@ def run():
     for name in VARIANTS:
         ts = sorted(times[name])
         same = bool(torch.equal(outs[name][0], outs["base"][0]) and torch.equal(outs[name][1], outs["base"][1]))
-        print(json.dumps(dict(variant=name, n=n, us=ts[len(ts) // 2], us_min=ts[0], bit_identical_to_base=same)),
+        print(json.dumps(dict(variant=name, kind="critic" if KIND == CRITIC else "actor", n=n, us=ts[len(ts) // 2], us_min=ts[0], bit_identical_to_base=same)),
               flush=True)
 
 
