@@ -342,9 +342,13 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
         for c in el:
             if c.tag == "geom":
                 ga = defaults.attrs(c, cls)
-                if ga.get("type", "sphere") != "box":
-                    continue
                 if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
+                    continue  # visual only
+                if ga.get("type", "sphere") != "box":
+                    # the engine collides box soles with the floor (plane-box); other colliding
+                    # geoms are listed so a caller can see what the model leaves out
+                    desc.setdefault("skipped_geoms", []).append(
+                        {"name": ga.get("name", ""), "body": name, "type": ga.get("type", "sphere")})
                     continue
                 gd = {"name": ga.get("name", f"{name}_geom{len(desc['geoms'])}"), "body": name, "type": "box",
                       "size": _floats(ga["size"], 3)}

@@ -386,3 +386,12 @@ def test_actuator_errors(what, err):
 
     with pytest.raises(ValueError, match=err):
         _actuated(mut)
+
+
+def test_non_box_colliders_are_reported():
+    b = load_mjcf("<mujoco><worldbody><body name='b'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
+                  "<geom name='shin' type='capsule' size='0.01 0.05'/>"
+                  "<geom name='vis' type='mesh' mesh='m' contype='0' conaffinity='0'/></body></worldbody></mujoco>")
+    assert b["skipped_geoms"] == [{"name": "shin", "body": "b", "type": "capsule"}]
+    assert b["geoms"] == []
+    assert "skipped_geoms" not in load_mjcf(to_mjcf(load_description()))
