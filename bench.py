@@ -321,7 +321,7 @@ def main() -> None:
             flop_per_env_step = tj.get("issued_fp32_flop_per_env_step")
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
-    policy_leg = None if args.no_policy else bench_policy_in_loop(eng, n, 16, dev, rank)
+    policy_leg = None if args.no_policy else bench_policy_in_loop(eng, n, 48, dev, rank)
     pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(eng, n, 32, 2, dev, world)
 
     if rank == 0:
