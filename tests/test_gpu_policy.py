@@ -132,3 +132,45 @@ def test_kinfer_step_matches_gpu_actor(pol):
     for e in range(n):
         np.testing.assert_allclose(a[e].cpu().numpy(), ref[e][0].numpy(), rtol=0, atol=2e-5)
         np.testing.assert_allclose(c[e].cpu().numpy(), ref[e][1].numpy(), rtol=0, atol=2e-5)
+
+
+def test_rollout_step_graph_capture(pol):
+    """zb_policy_actor -> zb_step captured in a HIP graph (torch.cuda.CUDAGraph) and replayed
+    gives the bits of the same launches run eagerly: neither entry point allocates, copies to the
+    host or synchronises (include/zbot.h, include/zbot_policy.h), so a rollout's launch-bound
+    inner loop can be a graph."""
+    from zbot_amd import compile_model, default_config
+    from zbot_amd.engine import HipEngine
+
+    n, T = 64, 3
+    cm = compile_model()
+    P = init_params(ACTOR, seed=2)
+    runs = []
+    for mode in ("eager", "graph"):
+        eng = HipEngine(cm, default_config(), n, seed=4)
+        eng.reset()
+        actor = pol.GruPolicy(ACTOR, P)
+        carry = actor.initial_carry(n)
+        acts = torch.empty(n, 20, device="cuda")
+
+        def body():
+            for t in range(T):
+                actor.actor(eng.obs_actor, carry, seed=5, step=t, actions=acts)
+                eng.step(acts, extras=False)
+
+        if mode == "eager":
+            body()
+        else:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    body()
+            torch.cuda.current_stream().wait_stream(s)
+            # capture records the launches without running them: the state is still the reset one
+            g.replay()
+        torch.cuda.synchronize()
+        runs.append((eng.get_state().cpu().clone(), carry.cpu().clone(), acts.cpu().clone()))
+    for a, b in zip(runs[0], runs[1]):
+        assert torch.equal(a, b)
