@@ -189,9 +189,12 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
 
     def once():
         traj = ro.run(T, record_critic=True)
-        values = critic.critic(traj["obs_critic"], critic.initial_carry(n),
-                               reset=torch.cat([zeros, traj["done"][:-1]]))
-        return compute_ppo_inputs(values, traj["reward"], traj["done"])
+        cc = critic.initial_carry(n)
+        # V(s_t) on the states acted in (carry reset where an episode starts), then the
+        # bootstrap V(s_T) with the carry the rollout ends with
+        values = critic.critic(traj["obs_critic"], cc, reset=torch.cat([zeros, traj["done"][:-1]]))
+        boot = critic.critic(traj["obs_critic_next"], cc, reset=traj["done"][-1])
+        return compute_ppo_inputs(values, traj["reward"], traj["done"], bootstrap=boot)
 
     once()  # first use of every kernel and of the moment collective, untimed
     torch.cuda.synchronize(dev)

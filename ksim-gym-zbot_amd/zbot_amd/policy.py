@@ -10,6 +10,7 @@ matrix cores (include/zbot_policy.h); there is no PyTorch or CPU fallback.
     actions, log_prob = actor.actor(obs_actor, carry, reset=done, log_prob=True)   # sample_action
     critic = GruPolicy(CRITIC, init_params(CRITIC, seed=1))
     values = critic.critic(obs_critic_t, critic.initial_carry(n), reset=resets_t)  # [T, n]
+    (obs_critic_t[t] is the observation of the state acted in at step t; PolicyRollout records it)
 
 `PolicyRollout` is ksim's rollout loop with the actor in it: per control step
 one actor launch then one zb_step launch, rows written straight into [T, n]
@@ -196,23 +197,34 @@ class PolicyRollout:
         self.carry = actor.initial_carry(engine.n)
         self.step_count = 0
         self.obs = None
+        self.obs_c = None  # critic observation of the current state (known after reset / recording)
         self.done = None
 
     def reset(self):
         out = self.eng.reset(extras=False)
         self.obs = out["obs_actor"].clone()
+        self.obs_c = out["obs_critic"].clone()
         self.carry.zero_()
         self.done = None
 
     def run(self, T: int, record_critic: bool = False) -> dict:
+        """T control steps. With record_critic, out["obs_critic"][t] is the critic observation of
+        the state the actor acted in at step t (what get_ppo_variables evaluates the critic on,
+        train.py:1683-1729) and out["obs_critic_next"] that of the state after step T-1 (the
+        bootstrap value's input)."""
         torch = self.actor.torch
         n, dev = self.eng.n, self.eng.device
         if self.obs is None:
             self.reset()
+        if record_critic and self.obs_c is None:
+            raise ZbError("the current state's critic observation is unknown (a run without "
+                          "record_critic came before): reset() first")
         f32 = dict(dtype=torch.float32, device=dev)
         obs = torch.empty(T + 1, n, ACTOR_IN, **f32)
         obs[0].copy_(self.obs)
-        crit = torch.empty(T, n, CRITIC_IN, **f32) if record_critic else None
+        crit = torch.empty(T + 1, n, CRITIC_IN, **f32) if record_critic else None
+        if record_critic:
+            crit[0].copy_(self.obs_c)
         acts = torch.empty(T, n, JOINTS, **f32)
         lp = torch.empty(T, n, JOINTS, **f32)
         rew = torch.empty(T, n, **f32)
@@ -224,12 +236,14 @@ class PolicyRollout:
                              seed=self.seed, env_offset=self.eng.env_offset, step=self.step_count, actions=acts[t],
                              log_prob=lp[t])
             _check(L.zb_step(self.eng.h, acts[t].data_ptr(), obs[t + 1].data_ptr(),
-                             crit[t].data_ptr() if record_critic else None, None, None, rew[t].data_ptr(),
+                             crit[t + 1].data_ptr() if record_critic else None, None, None, rew[t].data_ptr(),
                              done[t].data_ptr(), float(self.curriculum), stream))
             self.step_count += 1
         self.obs = obs[T].clone()
+        self.obs_c = crit[T].clone() if record_critic else None
         self.done = done[T - 1].clone()
         out = dict(obs_actor=obs, actions=acts, log_prob=lp, reward=rew, done=done)
         if record_critic:
-            out["obs_critic"] = crit
+            out["obs_critic"] = crit[:T]
+            out["obs_critic_next"] = crit[T]
         return out

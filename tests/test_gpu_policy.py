@@ -174,3 +174,26 @@ def test_rollout_step_graph_capture(pol):
         runs.append((eng.get_state().cpu().clone(), carry.cpu().clone(), acts.cpu().clone()))
     for a, b in zip(runs[0], runs[1]):
         assert torch.equal(a, b)
+
+
+def test_rollout_records_critic_obs_of_acted_states(pol, cmodel):
+    """obs_critic[t] is the state the actor acted in at step t (get_ppo_variables evaluates the
+    critic there, train.py:1683-1729): row 0 is the reset observation, and a second rollout starts
+    from the first one's obs_critic_next."""
+    from zbot_amd import default_config
+    from zbot_amd.engine import HipEngine, ZbError
+
+    eng = HipEngine(cmodel, default_config(), 32, seed=6)
+    ro = pol.PolicyRollout(eng, pol.GruPolicy(ACTOR, init_params(ACTOR, seed=1)), seed=2)
+    ro.reset()
+    reset_c = eng.obs_critic.clone()
+    a = ro.run(3, record_critic=True)
+    b = ro.run(2, record_critic=True)
+    torch.cuda.synchronize()
+    assert a["obs_critic"].shape == (3, 32, 484) and a["obs_critic_next"].shape == (32, 484)
+    assert torch.equal(a["obs_critic"][0], reset_c)
+    assert torch.equal(b["obs_critic"][0], a["obs_critic_next"])
+    assert not torch.equal(a["obs_critic"][1], a["obs_critic"][0])
+    ro.run(1)
+    with pytest.raises(ZbError):
+        ro.run(1, record_critic=True)
