@@ -1267,7 +1267,10 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
 }
 
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
-__device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float qacc, float qs, float fs, float Ma, float& grad) {
+/* returns this lane's cost share; the caller reduces it over the team (alone, or together with
+   the Newton loop's other per-iteration sums in one tsum_n) */
+__device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, float qacc, float qs, float fs,
+                                                       float Ma, float& grad) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float cost = 0.f;
@@ -1334,7 +1337,11 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
     if (r.hhi) qc -= r.fhi;
   }
   grad = Ma - fs - qc;
-  return tsum(cost);
+  return cost;
+}
+__device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float qacc, float qs, float fs, float Ma,
+                                                  float& grad) {
+  return tsum(update_constraint_lane(c, r, qacc, qs, fs, Ma, grad));
 }
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -1567,10 +1574,17 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     r.jhi -= alpha * search;
     float oldcost = cost;
     const int pa = r.act, pf = r.actf, plo = r.actlo, phi = r.acthi;
-    cost = update_constraint(c, r, x, qs, fs, Ma, grad);
+    /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
+       value, so the bits of separate tsum calls): cost, |grad|^2 and the active-set change */
+    float red[3];
+    red[0] = update_constraint_lane(c, r, x, qs, fs, Ma, grad);
+    red[1] = c.l < NV ? grad * grad : 0.f;
+    red[2] = (r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1.f : 0.f;
+    tsum_n<3>(red);
+    cost = red[0];
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
-    const bool changed = tmaxi((r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1 : 0) != 0;
+    const bool changed = red[2] > 0.f;
     STAMP(S_UPD);
     if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo, phi);
     STAMP(S_HESS);
@@ -1578,7 +1592,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     STAMP(S_SOLVE);
     it++;
     float improvement = scale * (oldcost - cost);
-    float gradient = scale * sqrtf(tsum(c.l < NV ? grad * grad : 0.f));
+    float gradient = scale * sqrtf(red[1]);
     if (improvement < cfg->tolerance || gradient < cfg->tolerance) break;
     search = -mg;
   }

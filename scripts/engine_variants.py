@@ -23,10 +23,8 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{ROOT}/inclu
 
 VARIANTS = {
     "base": [],
-    "maxilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-    "maxmemclause": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
-    "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
-    "nohighrp": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"],
+    # the engine before the Newton loop's combined reductions: ZB_ENG_OLD or evariants/zb_engine_r01v18.hip
+    "r01v18": "file:" + os.environ.get("ZB_ENG_OLD", os.path.join(OUT, "zb_engine_r01v18.hip")),
     "base2": [],
 }
 
@@ -36,8 +34,10 @@ def build():
     subprocess.run(["make", "-C", CSRC, "-s"], check=True)
     for name, extra in VARIANTS.items():
         obj = os.path.join(OUT, f"eng_{name}.o")
-        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *extra, "-c", "-o", obj, os.path.join(CSRC, "zb_engine.hip")],
-                       check=True)
+        src = os.path.join(CSRC, "zb_engine.hip")
+        if isinstance(extra, str) and extra.startswith("file:"):
+            src, extra = extra[5:], []
+        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *extra, "-c", "-o", obj, src], check=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                         os.path.join(OUT, f"libeng_{name}.so"), obj, os.path.join(CSRC, "build", "zb_capi.o"),
                         os.path.join(CSRC, "build", "zb_ppo.o"), os.path.join(CSRC, "build", "zb_policy.o")],
@@ -77,10 +77,20 @@ def run():
             b.record()
             torch.cuda.synchronize()
             times[name].append(a.elapsed_time(b) / 16)
+    # bit-identity of every variant with the first, from a fresh reset over 6 steps
+    finals = {}
+    for name in VARIANTS:
+        eng = E.HipEngine(cm, cfg, n, seed=9, lib_path=os.path.join(OUT, f"libeng_{name}.so"))
+        eng.reset()
+        for t in range(6):
+            eng.step(acts[t], extras=False)
+        finals[name] = eng.get_state()
+    first = next(iter(VARIANTS))
     for name in VARIANTS:
         ts = sorted(times[name])
         print(json.dumps(dict(variant=name, n=n, ms_per_step=ts[len(ts) // 2], ms_min=ts[0],
-                              env_steps_per_s=n / ts[0] * 1e3)), flush=True)
+                              env_steps_per_s=n / ts[0] * 1e3,
+                              bit_identical_to_first=bool(torch.equal(finals[name], finals[first])))), flush=True)
 
 
 if __name__ == "__main__":
