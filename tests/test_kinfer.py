@@ -139,3 +139,17 @@ def test_export_file_and_errors(params, tmp_path):
         K.export_kinfer(params[:-1])
     with pytest.raises(ValueError):
         K.metadata(["a", "b"])
+
+
+def test_command_line_export(tmp_path):
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "ksim-gym-zbot_amd"))
+    out = tmp_path / "r.kinfer"
+    subprocess.run([sys.executable, "-m", "zbot_amd.kinfer", "random", str(out)], check=True, env=env,
+                   capture_output=True, timeout=300)
+    init, step, meta = K.unpack(out.read_bytes())
+    assert meta["carry_size"] == [5, 128] and onnx_mini.Model(step).outputs[0] == ("action", [20])

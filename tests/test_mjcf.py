@@ -395,3 +395,18 @@ def test_non_box_colliders_are_reported():
     assert b["skipped_geoms"] == [{"name": "shin", "body": "b", "type": "capsule"}]
     assert b["geoms"] == []
     assert "skipped_geoms" not in load_mjcf(to_mjcf(load_description()))
+
+
+def test_command_line_round_trip(tmp_path):
+    import os
+    import subprocess
+    import sys
+
+    from zbot_amd.model import DEFAULT_ASSET
+
+    pkg_root = os.path.dirname(os.path.dirname(DEFAULT_ASSET))  # ksim-gym-zbot_amd/
+    env = dict(os.environ, PYTHONPATH=pkg_root)
+    xml, js = tmp_path / "z.xml", tmp_path / "z.json"
+    subprocess.run([sys.executable, "-m", "zbot_amd.mjcf", DEFAULT_ASSET, str(xml)], check=True, env=env)
+    subprocess.run([sys.executable, "-m", "zbot_amd.mjcf", str(xml), str(js)], check=True, env=env)
+    _assert_same_model(compile_model(_tree_order(load_description())), compile_model(str(js)))
