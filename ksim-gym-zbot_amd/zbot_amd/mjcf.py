@@ -215,7 +215,13 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
     template: descriptor supplying what MJCF does not hold (servo classes, the joint -> servo
     map, base clearance, constraint solref/solimp); default assets/zbot_like.json."""
     tmpl = template or load_description()
-    text = open(src).read() if os.path.exists(src) else src
+    if src.lstrip().startswith("<"):
+        text = src
+    elif os.path.exists(src):
+        with open(src) as f:
+            text = f.read()
+    else:
+        raise FileNotFoundError(f"MJCF file not found: {src}")
     root = ET.fromstring(text)
     if root.tag != "mujoco":
         raise ValueError("not an MJCF document (<mujoco> root expected)")

@@ -410,3 +410,8 @@ def test_command_line_round_trip(tmp_path):
     subprocess.run([sys.executable, "-m", "zbot_amd.mjcf", DEFAULT_ASSET, str(xml)], check=True, env=env)
     subprocess.run([sys.executable, "-m", "zbot_amd.mjcf", str(xml), str(js)], check=True, env=env)
     _assert_same_model(compile_model(_tree_order(load_description())), compile_model(str(js)))
+
+
+def test_missing_file_is_reported():
+    with pytest.raises(FileNotFoundError):
+        load_mjcf("/nonexistent/zbot.xml")
