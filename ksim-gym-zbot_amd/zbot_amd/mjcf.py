@@ -18,11 +18,17 @@ MJCF semantics (XML reference, MuJoCo 3.3.4 [U]):
     explicit attributes winning (joint: axis, range, armature, damping,
     frictionloss, pos; geom: type, size, pos, contype, conaffinity);
   * <body pos quat|euler|axisangle>, one <joint type="hinge"> or a
-    <freejoint/> per body, <inertial pos quat mass diaginertia>;
-  * box <geom>s with a nonzero contype/conaffinity as the foot-sole colliders,
-    the <geom type="plane"> of the worldbody as the floor (friction, solref,
+    <freejoint/> per body;
+  * <inertial pos quat mass diaginertia|fullinertia>, or, without one (or with
+    inertiafromgeom="true"), the mass and inertia of the body's box / sphere /
+    capsule / cylinder / ellipsoid geoms (density or mass, fromto,
+    inertiagrouprange), composed about their common centre of mass;
+  * box <geom>s with a nonzero contype/conaffinity as the foot-sole colliders
+    (other colliding geoms are listed in desc["skipped_geoms"]), the
+    <geom type="plane"> of the worldbody as the floor (friction, solref,
     solimp, margin);
-  * <site>s; <option timestep gravity>.
+  * <motor> / plain <general> actuators (gear, ctrlrange, ctrllimited), one per
+    hinge; <site>s and <touch> sensors; <option timestep gravity>.
 The servo model (FeetechParams, train.py:1121-1134) is not part of MJCF: it
 comes from `servo_classes` + `joint_servo` (joint -> class; by default the
 joint's MJCF class when it names a servo class, else the Z-Bot-like
@@ -178,7 +184,6 @@ def _compose(parts):
         inertia += R @ np.diag(diag) @ R.T + m * (float(d @ d) * np.eye(3) - np.outer(d, d))
     diag, iq = _principal(inertia)
     return float(M), [float(x) for x in com], diag, iq
-
 
 
 class _Defaults:
