@@ -23,8 +23,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{ROOT}/inclu
 
 VARIANTS = {
     "base": [],
-    # the engine before the Newton loop's combined reductions: ZB_ENG_OLD or evariants/zb_engine_r01v18.hip
-    "r01v18": "file:" + os.environ.get("ZB_ENG_OLD", os.path.join(OUT, "zb_engine_r01v18.hip")),
+    "waves1": ["-DZB_WAVES_PER_EU=1"],  # 512 registers, no spill, one wave per SIMD
     "base2": [],
 }
 
