@@ -25,9 +25,9 @@ sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
 METRIC = "env-steps/sec at N envs per GPU, 1/2/4/8 MI355X; % HBM roofline"
 
 CONFIGS = {
-    "c2": dict(envs=8192, push=False, randomize=False, name="C2: 8192 envs/GPU, flat-floor stand, 256-step rollout"),
-    "c3": dict(envs=32768, push=True, randomize=False, name="C3: 32768 envs/GPU, push-perturbation curriculum"),
-    "c5": dict(envs=16384, push=False, randomize=True, name="C5: 16384 envs/GPU, per-env domain randomization"),
+    "c2": dict(envs=8192, push=False, randomize=False, name="C2: {n} envs/GPU, flat-floor stand"),
+    "c3": dict(envs=32768, push=True, randomize=False, name="C3: {n} envs/GPU, push-perturbation curriculum"),
+    "c5": dict(envs=16384, push=False, randomize=True, name="C5: {n} envs/GPU, per-env domain randomization"),
 }
 
 
@@ -194,7 +194,7 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
         # bootstrap V(s_T) with the carry the rollout ends with
         values = critic.critic(traj["obs_critic"], cc, reset=torch.cat([zeros, traj["done"][:-1]]))
         boot = critic.critic(traj["obs_critic_next"], cc, reset=traj["done"][-1])
-        return compute_ppo_inputs(values, traj["reward"], traj["done"], bootstrap=boot)
+        return compute_ppo_inputs(values, traj["reward"], traj["done"], traj["success"], bootstrap=boot)
 
     once()  # first use of every kernel and of the moment collective, untimed
     torch.cuda.synchronize(dev)
@@ -343,7 +343,10 @@ def main() -> None:
             "dtype": "f32",
             "data": "synthetic: actions = JOINT_BIASES + 0.05*N(0,1) on the Z-Bot-like descriptor",
             "config": {
-                "workload": conf["name"],
+                # what the timed region ran: K back-to-back zb_step launches, each one control
+                # step (20 physics substeps) of every env, continuing one episode stream
+                "workload": conf["name"].format(n=n) + f", {args.steps} timed zb_step launches of one control step "
+                                                       f"each (after {args.warmup} warm-up steps)",
                 "envs_per_gpu": n,
                 "global_envs": world * n,
                 "substeps_per_step": cfg.n_substeps,

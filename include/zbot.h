@@ -95,20 +95,29 @@ int zb_reset(ZbHandle* h, const uint8_t* env_mask_dev, float* obs_actor,
  *   obs_extra    [n_envs, 96]  (nullable)
  *   reward_terms [n_envs, 12]  unscaled term values (nullable)
  *   reward       [n_envs]      sum_i scale_i * (curriculum if by_curr) * term_i
- *   done         [n_envs]      uint8 termination flag
+ *   done         [n_envs]      uint8 termination flag (failure or time limit)
+ *   success      [n_envs]      uint8 (nullable): the episode ended by the
+ *                              EpisodeLengthTermination time limit and not by a
+ *                              failure (train.py:1588-1593, ksim's successful
+ *                              termination [U]); ksim's compute_ppo_inputs
+ *                              bootstraps these steps with V(s_t)
+ *                              (include/zbot_ppo.h zb_gae `success`)
  *   curriculum_level           ksim curriculum scalar (one value for all envs)
+ * ABI version 2 added `success` (version 1 had no such argument).
  */
 int zb_step(ZbHandle* h, const float* action, float* obs_actor,
             float* obs_critic, float* obs_extra, float* reward_terms,
-            float* reward, uint8_t* done, float curriculum_level, void* stream);
+            float* reward, uint8_t* done, uint8_t* success,
+            float curriculum_level, void* stream);
 
 /* Run `n_steps` control steps back to back in ONE launch, with actions
  * action[t][n_envs][20]; outputs of the last step only (rollout benchmark /
  * fixed-policy rollouts). reward_sum [n_envs] (nullable) accumulates the
- * total reward of every step. */
+ * total reward of every step; done / success (nullable) are the last step's. */
 int zb_rollout(ZbHandle* h, const float* actions, int n_steps,
                float* obs_actor, float* obs_critic, float* reward_sum,
-               uint8_t* done, float curriculum_level, void* stream);
+               uint8_t* done, uint8_t* success, float curriculum_level,
+               void* stream);
 
 /* Persistent state access: [n_envs, ZB_STATE_STRIDE] fp32 words (device).
  * get copies out, set copies in (checkpoint / parity tests). */

@@ -17,7 +17,7 @@
 
 #include "zb_internal.h"
 
-#define ZB_ABI_VERSION 1
+#define ZB_ABI_VERSION 2
 
 struct ZbHandle {
   int device;
@@ -266,7 +266,8 @@ int zb_reset(ZbHandle* h, const uint8_t* env_mask_dev, float* obs_actor, float* 
 }
 
 int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_critic, float* obs_extra,
-            float* reward_terms, float* reward, uint8_t* done, float curriculum_level, void* stream) {
+            float* reward_terms, float* reward, uint8_t* done, uint8_t* success, float curriculum_level,
+            void* stream) {
   if (!h || !action) return fail(ZB_EARG, "zb_step: null handle or action");
   if (!(curriculum_level == curriculum_level)) return fail(ZB_EARG, "zb_step: curriculum is NaN");
   int rc = use_device(h);
@@ -279,6 +280,7 @@ int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_criti
   a.reward_terms = reward_terms;
   a.reward = reward;
   a.done = done;
+  a.success = success;
   a.curriculum = curriculum_level;
   hipError_t e = zb::launch_step(a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_step launch: %s", hipGetErrorString(e));
@@ -286,7 +288,7 @@ int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_criti
 }
 
 int zb_rollout(ZbHandle* h, const float* actions, int n_steps, float* obs_actor, float* obs_critic, float* reward_sum,
-               uint8_t* done, float curriculum_level, void* stream) {
+               uint8_t* done, uint8_t* success, float curriculum_level, void* stream) {
   if (!h || !actions || n_steps < 1) return fail(ZB_EARG, "zb_rollout: bad argument");
   int rc = use_device(h);
   if (rc) return rc;
@@ -297,6 +299,7 @@ int zb_rollout(ZbHandle* h, const float* actions, int n_steps, float* obs_actor,
   a.obs_critic = obs_critic;
   a.reward = reward_sum;
   a.done = done;
+  a.success = success;
   a.curriculum = curriculum_level;
   hipError_t e = zb::launch_step(a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_rollout launch: %s", hipGetErrorString(e));

@@ -2330,6 +2330,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   int iters = 0;
   float rsum = 0.f;
   bool done = false;
+  bool success = false; /* done by the time limit alone (ksim successful termination) */
   const int nsteps = a.nsteps;
   const bool rollout = nsteps > 1;
   for (int t = 0; t < nsteps; t++) {
@@ -2365,6 +2366,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
         bool fail;
         float* terms = (live && a.reward_terms && !rollout) ? a.reward_terms + (size_t)e * ZB_NUM_TERMS : nullptr;
         done = rewards(c, s, ls, B, a.curriculum, terms, total, fail);
+        success = done && !fail;
         rsum += total;
         if (live && a.stats && c.l == 0) {
           float* sp = a.stats + (size_t)e * ZB_NUM_STATS;
@@ -2399,6 +2401,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
     if (live && c.l == 0 && last_t) {
       if (a.reward) a.reward[e] = rollout ? rsum : total;
       if (a.done) a.done[e] = done ? 1 : 0;
+      if (a.success) a.success[e] = success ? 1 : 0;
     }
   }
   if (live && a.iters && c.l == 0) a.iters[e] = iters;

@@ -42,6 +42,7 @@ struct StepArgs {
   float* reward_terms;
   float* reward;            /* per step reward (nsteps==1) or reward sum (rollout) */
   uint8_t* done;
+  uint8_t* success;         /* [n] or null: time-limit end without failure */
   float curriculum;
   float* stats;             /* [n, ZB_NUM_STATS] */
   int32_t* iters;           /* [n] */

@@ -25,6 +25,7 @@ def default_config(
     ls_iterations: int = LS_ITERATIONS,
     dt: float = DT,
     ctrl_dt: float = CTRL_DT,
+    max_episode_sec: float = 80.0,
 ) -> cs.ZbEnvConfig:
     c = cs.ZbEnvConfig()
     c.struct_bytes = ctypes.sizeof(cs.ZbEnvConfig)
@@ -48,7 +49,7 @@ def default_config(
     c.imu_noise_std = math.radians(1)  # train.py:1497
     c.acc_noise_std = 0.5  # train.py:1503
     c.reset_qvel_scale = 0.01  # ksim RandomJointVelocityReset default scale [U]
-    c.max_episode_sec = 80.0  # train.py:1592
+    c.max_episode_sec = max_episode_sec  # train.py:1592 (80 s)
     c.lag_range[0], c.lag_range[1] = 0.0, 0.1  # train.py:1496
     c.bad_z[0], c.bad_z[1] = 0.05, 0.5  # train.py:1590
     c.max_tilt_rad = math.radians(60)  # train.py:1591

@@ -13,6 +13,7 @@ import os
 from . import cstructs as cs
 
 LIB_NAME = "libzbot_hip.so"
+ABI_VERSION = 2  # include/zbot.h: version 2 added zb_step / zb_rollout's `success` output
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 CSRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 
@@ -57,8 +58,8 @@ def load_library(path: str | None = None) -> C.CDLL:
                             C.POINTER(vp)]
     L.zb_destroy.argtypes = [vp]
     L.zb_reset.argtypes = [vp, vp, vp, vp, vp, vp]
-    L.zb_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp]
-    L.zb_rollout.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, C.c_float, vp]
+    L.zb_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_float, vp]
+    L.zb_rollout.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_float, vp]
     for f in ("zb_get_state", "zb_set_state", "zb_get_rand", "zb_set_rand", "zb_get_solver_iters"):
         getattr(L, f).argtypes = [vp, vp, vp]
     L.zb_get_stats.argtypes = [vp, vp, C.c_int, vp]
@@ -84,6 +85,8 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.zb_policy_critic.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, vp]
     for f in ("zb_policy_create", "zb_policy_destroy", "zb_policy_actor", "zb_policy_critic"):
         getattr(L, f).restype = C.c_int
+    if L.zb_abi_version() != ABI_VERSION:
+        raise ZbError(f"{lp}: ABI version {L.zb_abi_version()}, this binding speaks {ABI_VERSION}: rebuild it")
     if L.zb_model_struct_bytes() != C.sizeof(cs.ZbModel):
         raise ZbError("ZbModel layout mismatch between cstructs.py and the library")
     if L.zb_config_struct_bytes() != C.sizeof(cs.ZbEnvConfig):
@@ -133,6 +136,7 @@ class HipEngine:
         self.reward_terms = torch.zeros(n_envs, cs.NUM_TERMS, **f32)
         self.reward = torch.zeros(n_envs, **f32)
         self.done = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
+        self.success = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -148,7 +152,7 @@ class HipEngine:
 
     def outputs(self) -> dict:
         return dict(obs_actor=self.obs_actor, obs_critic=self.obs_critic, obs_extra=self.obs_extra,
-                    reward_terms=self.reward_terms, reward=self.reward, done=self.done)
+                    reward_terms=self.reward_terms, reward=self.reward, done=self.done, success=self.success)
 
     def reset(self, mask=None, extras: bool = True) -> dict:
         m = None
@@ -166,16 +170,25 @@ class HipEngine:
             raise ZbError(f"action must be [{self.n}, {cs.NJ}], got {tuple(a.shape)}")
         _check(self.L.zb_step(self.h, _ptr(a), _ptr(self.obs_actor), _ptr(self.obs_critic),
                               _ptr(self.obs_extra) if extras else None, _ptr(self.reward_terms) if terms else None,
-                              _ptr(self.reward), _ptr(self.done), float(curriculum), self._stream()))
+                              _ptr(self.reward), _ptr(self.done), _ptr(self.success), float(curriculum),
+                              self._stream()))
         return self.outputs()
+
+    def _check_out(self, t, name: str, shape: tuple, dtype) -> None:
+        """An output buffer the kernel writes through its raw pointer: exact shape, dtype, device, contiguity."""
+        if (tuple(t.shape) != shape or t.dtype != dtype or t.device != self.device or not t.is_contiguous()):
+            raise ZbError(f"{name} must be a contiguous {dtype} {list(shape)} tensor on {self.device}, got "
+                          f"{t.dtype} {list(t.shape)} on {t.device}")
 
     def rollout(self, actions, curriculum: float = 1.0, reward_sum=None) -> dict:
         a = actions.to(device=self.device, dtype=self.torch.float32).contiguous()
         T = a.shape[0]
-        if tuple(a.shape) != (T, self.n, cs.NJ):
-            raise ZbError("actions must be [T, n_envs, 20]")
+        if a.dim() != 3 or tuple(a.shape) != (T, self.n, cs.NJ) or T < 1:
+            raise ZbError("actions must be [T, n_envs, 20] with T >= 1")
+        if reward_sum is not None:
+            self._check_out(reward_sum, "reward_sum", (self.n,), self.torch.float32)
         _check(self.L.zb_rollout(self.h, _ptr(a), T, _ptr(self.obs_actor), _ptr(self.obs_critic), _ptr(reward_sum),
-                                 _ptr(self.done), float(curriculum), self._stream()))
+                                 _ptr(self.done), _ptr(self.success), float(curriculum), self._stream()))
         return self.outputs()
 
     def get_state(self):
@@ -197,6 +210,8 @@ class HipEngine:
 
     def set_rand(self, rand) -> None:
         r = rand.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if tuple(r.shape) != (self.n, cs.RAND_STRIDE):
+            raise ZbError(f"rand must be [n_envs, ZB_RAND_STRIDE] = [{self.n}, {cs.RAND_STRIDE}], got {tuple(r.shape)}")
         _check(self.L.zb_set_rand(self.h, _ptr(r), self._stream()))
         self.torch.cuda.current_stream(self.device).synchronize()
 

@@ -211,7 +211,8 @@ class PolicyRollout:
         """T control steps. With record_critic, out["obs_critic"][t] is the critic observation of
         the state the actor acted in at step t (what get_ppo_variables evaluates the critic on,
         train.py:1683-1729) and out["obs_critic_next"] that of the state after step T-1 (the
-        bootstrap value's input)."""
+        bootstrap value's input). out["success"][t] flags the steps whose episode ended at the
+        time limit without a failure (ksim's successes_t for compute_ppo_inputs)."""
         torch = self.actor.torch
         n, dev = self.eng.n, self.eng.device
         if self.obs is None:
@@ -229,6 +230,7 @@ class PolicyRollout:
         lp = torch.empty(T, n, JOINTS, **f32)
         rew = torch.empty(T, n, **f32)
         done = torch.zeros(T, n, dtype=torch.uint8, device=dev)
+        success = torch.zeros(T, n, dtype=torch.uint8, device=dev)
         L = self.eng.L
         stream = torch.cuda.current_stream(dev).cuda_stream
         for t in range(T):
@@ -237,12 +239,12 @@ class PolicyRollout:
                              log_prob=lp[t])
             _check(L.zb_step(self.eng.h, acts[t].data_ptr(), obs[t + 1].data_ptr(),
                              crit[t + 1].data_ptr() if record_critic else None, None, None, rew[t].data_ptr(),
-                             done[t].data_ptr(), float(self.curriculum), stream))
+                             done[t].data_ptr(), success[t].data_ptr(), float(self.curriculum), stream))
             self.step_count += 1
         self.obs = obs[T].clone()
         self.obs_c = crit[T].clone() if record_critic else None
         self.done = done[T - 1].clone()
-        out = dict(obs_actor=obs, actions=acts, log_prob=lp, reward=rew, done=done)
+        out = dict(obs_actor=obs, actions=acts, log_prob=lp, reward=rew, done=done, success=success)
         if record_critic:
             out["obs_critic"] = crit[:T]
             out["obs_critic_next"] = crit[T]

@@ -115,7 +115,8 @@ def combine_moments(moments, group=None):
     dist.all_gather(parts, moments, group=group)
     stacked = torch.stack(parts).contiguous()
     if stacked.device.type != "cuda":
-        return pairwise_tree_host(stacked)
+        # gloo on CPU tensors: the same tree on the host, handed back on the caller's device
+        return pairwise_tree_host(stacked).to(moments.device)
     out = torch.empty(2, dtype=torch.float64, device=stacked.device)
     _check(load_library().zb_moments_combine(stacked.data_ptr(), world, out.data_ptr(),
                                              _stream(torch, stacked.device)))
@@ -143,7 +144,17 @@ def normalize(gae_t, moments, total: float, eps: float = ADV_EPS, out=None):
     dev = gae_t.device
     if dev.type != "cuda":
         raise ZbError("ppo.normalize runs on the GPU (libzbot_hip.so)")
-    out = torch.empty_like(gae_t) if out is None else out
+    if (not isinstance(moments, torch.Tensor) or moments.dtype != torch.float64 or moments.numel() != 2
+            or moments.device != dev or not moments.is_contiguous()):
+        # the kernel dereferences moments[0..1] on the device: a host pointer would fault the GPU
+        raise ZbError(f"moments must be a contiguous float64 tensor of 2 elements on {dev}")
+    if gae_t.dtype != torch.float32 or not gae_t.is_contiguous():
+        raise ZbError("gae_t must be a contiguous float32 tensor")
+    if out is None:
+        out = torch.empty_like(gae_t)
+    elif (out.dtype != torch.float32 or out.device != dev or not out.is_contiguous()
+          or out.numel() != gae_t.numel()):
+        raise ZbError(f"out must be a contiguous float32 tensor of {gae_t.numel()} elements on {dev}")
     _check(load_library().zb_adv_normalize(gae_t.data_ptr(), out.data_ptr(), gae_t.numel(), moments.data_ptr(),
                                            float(total), C.c_float(eps), _stream(torch, dev)))
     return out

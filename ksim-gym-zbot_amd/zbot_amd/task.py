@@ -89,6 +89,7 @@ class StepResult:
     reward: object
     reward_terms: dict
     done: object
+    success: object = None  # time-limit ends without a failure (ksim successes_t)
 
 
 class ZbotWalkingEnv:
@@ -118,6 +119,7 @@ class ZbotWalkingEnv:
             reward=out["reward"] if with_reward else None,
             reward_terms=terms,
             done=out["done"] if with_reward else None,
+            success=out["success"] if with_reward else None,
         )
 
     def reset(self, mask=None) -> StepResult:

@@ -38,7 +38,7 @@ def lib(precision: str = "f32") -> C.CDLL:
     L.zbo_threefry2x32.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)]
     L.zbo_reset.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint64, fp, fp, u8p, fp, fp, fp]
     L.zbo_step.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint64, fp, fp, fp, fp, fp, fp, fp, fp,
-                           u8p, C.c_float, fp, i32p]
+                           u8p, u8p, C.c_float, fp, i32p]
     L.zbo_forward_debug.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp,
                                     C.POINTER(C.c_int), fp]
     L.zbo_simulate.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, C.c_int]
@@ -137,11 +137,14 @@ class OracleEnv:
         terms = np.zeros((self.n, cs.NUM_TERMS), dtype=np.float32)
         rew = np.zeros(self.n, dtype=np.float32)
         done = np.zeros(self.n, dtype=np.uint8)
+        success = np.zeros(self.n, dtype=np.uint8)
         rc = self.L.zbo_step(C.byref(self.model), C.byref(self.cfg), self.n, self.env_offset, self.seed,
                              _p(self.state), _p(self.rand), _p(action), _p(oa), _p(oc), _p(ox), _p(terms), _p(rew),
-                             _p(done, C.c_uint8), curriculum, _p(self.stats), _p(self.iters, C.c_int32))
+                             _p(done, C.c_uint8), _p(success, C.c_uint8), curriculum, _p(self.stats),
+                             _p(self.iters, C.c_int32))
         assert rc == 0
-        return dict(obs_actor=oa, obs_critic=oc, obs_extra=ox, reward_terms=terms, reward=rew, done=done)
+        return dict(obs_actor=oa, obs_critic=oc, obs_extra=ox, reward_terms=terms, reward=rew, done=done,
+                    success=success)
 
 
 def forward_debug(cmodel, cfg, qpos, qvel, ctrl=None, precision: str = "f32") -> dict:

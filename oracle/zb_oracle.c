@@ -1419,7 +1419,8 @@ int zbo_reset(const ZbModel* m, const ZbEnvConfig* cfg, int n, int env_offset, u
 
 int zbo_step(const ZbModel* m, const ZbEnvConfig* cfg, int n, int env_offset, uint64_t seed, float* state,
              float* rnd, const float* action, float* obs_actor, float* obs_critic, float* obs_extra,
-             float* reward_terms, float* reward, uint8_t* done, float curriculum, float* stats, int32_t* iters) {
+             float* reward_terms, float* reward, uint8_t* done, uint8_t* success, float curriculum, float* stats,
+             int32_t* iters) {
   if (!m || !cfg || !state || !action || n < 0) return -1;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int e = 0; e < n; e++) {
@@ -1444,6 +1445,7 @@ int zbo_step(const ZbModel* m, const ZbEnvConfig* cfg, int n, int env_offset, ui
                      &dflag, &sflag);
     if (reward) reward[e] = rew;
     if (done) done[e] = dn;
+    if (success) success[e] = (uint8_t)sflag;
     if (stats) {
       float* sp = stats + (size_t)e * ZB_NUM_STATS;
       sp[ZB_ST_REWARD] += rew;

@@ -100,7 +100,7 @@ def test_rollout_buffers_from_zb_step(ppo, oracle_mod, cmodel):
     for t in range(T):
         a = torch.from_numpy(O.synthetic_actions(cmodel.cmodel, 4, n, 0, t)).cuda()
         assert L.zb_step(eng.h, a.data_ptr(), eng.obs_actor.data_ptr(), eng.obs_critic.data_ptr(), None, None,
-                         rew[t].data_ptr(), done[t].data_ptr(), 1.0, eng._stream()) == 0
+                         rew[t].data_ptr(), done[t].data_ptr(), None, 1.0, eng._stream()) == 0
     vals = torch.linspace(-1, 1, T * n, device="cuda").reshape(T, n)
     out = ppo.compute_ppo_inputs(vals, rew, done)
     go, _, _ = oracle_mod.gae(rew.cpu().numpy(), vals.cpu().numpy(), done.cpu().numpy(), G, LAM)
