@@ -691,6 +691,44 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   tsync();
 }
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+/* Root Schur complement of the limb elimination on the matrix cores, for both
+ * envs of the wave: G[i][e] = sum_k D_k L(k,i) L(k,e), i,e < NROOT, k over the
+ * limb dofs NROOT..NV-1 (their eliminated rows are in LDS L[][] / Dk[]). Per
+ * env five v_mfma_f32_16x16x4_f32 (K = 4 limb dofs each; lane l supplies row
+ * NROOT + 4*chunk + l/16, entry l%16 < NROOT). Lane l ends with
+ * G[4*(l/16) + v][l%16]; the lower triangle (21 values, packed i(i+1)/2 + e) is
+ * left in the env's vec[V_TMP2], free during every factorization. Replaces 21
+ * team reductions (126 DPP/permlane VALU instructions per factor).
+ * Wave-uniform: call with every lane active (the MFMA reads all 64 lanes). */
+__device__ __forceinline__ void root_schur_mfma() {
+  static_assert(NV - NROOT == 20, "five K=4 chunks cover the 20 limb dofs");
+  const int l = threadIdx.x & 63;
+  const int i = l & 15, kk = l >> 4;
+  const int ic = i < RMAX ? i : 0;
+  v4f acc[NTEAM];
+#pragma unroll
+  for (int t = 0; t < NTEAM; t++) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ch = 0; ch < (NV - NROOT) / 4; ch++)
+#pragma unroll
+    for (int t = 0; t < NTEAM; t++) {
+      const int k = NROOT + 4 * ch + kk;
+      const float lv = g_lds[t].L[k][ic];
+      const float dv = g_lds[t].Dk[k];
+      const float a = i < RMAX ? dv * lv : 0.f, b = i < RMAX ? lv : 0.f;
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+    }
+#pragma unroll
+  for (int t = 0; t < NTEAM; t++)
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+      const int row = 4 * kk + v;
+      if (row < RMAX && i <= row) g_lds[t].vec[V_TMP2][row * (row + 1) / 2 + i] = acc[t][v];
+    }
+}
+
 /* ---------------------- sparse L'DL factor + solves ------------------------ */
 /* Sparse L'DL of depth-indexed rows (mj_factorM order: leaves first) for the
  * dof tree the engine accepts (zb_create): a root chain 0..nroot-1 and
@@ -701,6 +739,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
  * block is a set of team reductions; the root block is eliminated densely in
  * registers. On return the L rows are in LDS L[][] (L(k, anc_e(k))), pivots in
  * Dk[] (root: also 1/D in Di[]); returns 1/D_j. */
+template <bool MFMA_SCHUR>
 __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
@@ -719,14 +758,26 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
      the pivot row afterwards) and applies its Schur update. Position 0 has no
      receivers inside the chain. */
   const int cps = vopq(c.cps);
+  /* Alongside, each chain lane p builds row p of W = (I + Lt)^-1, the inverse of
+     its chain's unit triangular block (Lt(p, k) = L(k, p), k deeper in the chain),
+     by absolute chain position: W(p, k) = -sum_{m > p} L(m, p) W(m, k), W(m, m) = 1.
+     At level q the receiver already holds L(q, p) (sc) and pulls the pivot's
+     finished accumulators, so W costs no extra round trip here; solve_ldl then
+     applies each chain's triangular solve as one gather instead of a chain of
+     dependent ones. wacc[k] = -W(p, k) (zero for k <= p and past the chain). */
+  float wacc[NLIMBLV];
+#pragma unroll
+  for (int k = 0; k < NLIMBLV; k++) wacc[k] = 0.f;
 #pragma unroll
   for (int q = NLIMBLV - 1; q >= 1; q--) {
     const bool has = ischain && cps < q && q < c.cln;
     const int src = has ? c.chd + q : c.l;
-    float r[NROOT + NLIMBLV];
+    float r[NROOT + NLIMBLV], wq[NLIMBLV];
 #pragma unroll
     for (int e = 0; e < NROOT + q; e++) r[e] = tsh(X[e], src);
     const float dk = tsh(Xd, src);
+#pragma unroll
+    for (int k = q + 1; k < NLIMBLV; k++) wq[k] = tsh(wacc[k], src);
     /* A(k, j) = r[depth(j)], depth(j) = NROOT + cps, cps < q */
     float t = r[NROOT];
 #pragma unroll
@@ -737,15 +788,20 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
     for (int e = 0; e < NROOT; e++) X[e] -= sc * r[e];
 #pragma unroll
     for (int e = NROOT; e < NROOT + q - 1; e++) X[e] -= (e < ddep ? sc : 0.f) * r[e];
+    wacc[q] += sc;
+#pragma unroll
+    for (int k = q + 1; k < NLIMBLV; k++) wacc[k] -= sc * wq[k];
   }
   if (ischain) {
     const float Dkv = fmaxf(Xd, MINVAL);
     const float inv = 1.0f / Dkv;
 #pragma unroll
-    for (int e = 0; e < CAP; e++) X[e] = X[e] * inv;
+    for (int e = 0; e < NROOT; e++) X[e] = X[e] * inv;
+    /* stored row: L(j, root i) in slots 0..NROOT-1, W(p, k) in slots NROOT + k (the
+       chain-ancestor entries of L are not needed once W is known) */
+#pragma unroll
+    for (int k = 0; k < NLIMBLV; k++) X[NROOT + k] = -wacc[k];
     Xd = Dkv;
-  }
-  if (ischain) {
     st_row(&L->L[c.l][0], X);
     L->Dk[c.l] = Xd;
   }
@@ -756,7 +812,13 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
     tsync();
     constexpr int NG = RMAX * (RMAX + 1) / 2;
     float g[NG];
-    {
+    if constexpr (MFMA_SCHUR) {
+      /* wave-uniform call sites: the matrix cores sum over the limb rows in LDS */
+      root_schur_mfma();
+      tsync();
+#pragma unroll
+      for (int t = 0; t < NG; t++) g[t] = L->vec[V_TMP2][t];
+    } else {
       int t = 0;
 #pragma unroll
       for (int i = 0; i < RMAX; i++) {
@@ -764,8 +826,8 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
 #pragma unroll
         for (int j = 0; j <= i; j++) g[t++] = wi * X[j];
       }
+      tsum_n<NG>(g);
     }
-    tsum_n<NG>(g);
     float A[RMAX][RMAX], D[RMAX];
     {
       int t = 0;
@@ -820,25 +882,27 @@ __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
   return (c.l < NV) ? c.L->M[j][ddep] : 1.f;
 }
 
-/* x <- (L'DL)^-1 x, x held by dof lanes. Forward pass by level (a lane's
- * value is final once its level is reached; descendants' contributions come
- * through LDS two at a time), then the diagonal, then the root-to-leaf pass
- * over ancestors by depth. */
+/* x <- (L'DL)^-1 x, x held by dof lanes (mj_solveM order: L' pass from the
+ * leaves, diagonal, L pass from the root). Inside each limb chain both
+ * triangular passes are one gather with the chain's W = (I + Lt)^-1 from
+ * factor_ldl (slots NROOT.. of the stored rows): forward z_p = b_p +
+ * sum_{k > p} W(p, k) b_k, backward x_p = v_p + sum_{a < p} W(a, p) v_a. The
+ * root chain is dense and redundant in every lane. */
 __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
-  const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int nroot = NROOT;
   const bool ischain = c.chd >= 0;
-  /* forward pass along the limbs (leaves first): pull the pivot's final x */
-  const int nlv = NLIMBLV;
-  const int cps = vopq(c.cps);
+  const int cps = vopq(c.cps), cln = vopq(c.cln), chd = ischain ? c.chd : 0;
+  /* forward pass along the limbs: the chain's deeper right-hand sides, all in flight */
+  {
+    float w[CAP], bk[NLIMBLV];
+    ld_row(&L->L[c.l & 31][0], w);
 #pragma unroll
-  for (int q = NLIMBLV - 1; q >= 1; q--) {
-    const bool has = ischain && cps < q && q < c.cln;
-    const int src = has ? c.chd + q : c.l;
-    const float lk = L->L[src][ddep];
-    const float xk = tsh(x, src);
-    if (has) x -= lk * xk;
+    for (int k = 1; k < NLIMBLV; k++) bk[k] = tsh(x, (ischain && k < cln) ? chd + k : c.l);
+    float z = x;
+#pragma unroll
+    for (int k = 1; k < NLIMBLV; k++) z += (ischain && k > cps && k < cln) ? w[NROOT + k] * bk[k] : 0.f;
+    x = z;
   }
   /* root chain, dense and redundant in every lane */
   float xr[RMAX];
@@ -878,13 +942,19 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   } else {
     x *= Dinv;
   }
-  /* backward pass down the limbs: chain position s is final after step s */
-  for (int s = 0; s < nlv - 1; s++) {
-    const bool has = ischain && c.cps > s;
-    const int src = has ? c.chd + s : c.l;
-    const float la = L->L[c.l][has ? nroot + s : 0];
-    const float xa = tsh(x, src);
-    if (has) x -= la * xa;
+  /* backward pass down the limbs: the shallower chain values and W(a, p), all in flight */
+  {
+    float va[NLIMBLV - 1], wa[NLIMBLV - 1];
+#pragma unroll
+    for (int a = 0; a < NLIMBLV - 1; a++) {
+      const bool on = ischain && a < cps;
+      va[a] = tsh(x, on ? chd + a : c.l);
+      wa[a] = L->L[on ? chd + a : 0][NROOT + (cps < NLIMBLV ? cps : 0)];
+    }
+    float y = x;
+#pragma unroll
+    for (int a = 0; a < NLIMBLV - 1; a++) y += (ischain && a < cps) ? wa[a] * va[a] : 0.f;
+    x = y;
   }
   return x;
 }
@@ -1344,7 +1414,6 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
   return tsum(update_constraint_lane(c, r, qacc, qs, fs, Ma, grad));
 }
 
-typedef float v4f __attribute__((ext_vector_type(4)));
 /* G_f = sum_{r in foot f} D_r J_r J_r' (depth-indexed 12x12) for both feet of
  * both envs of the wave on the matrix cores: per (env, foot) four
  * v_mfma_f32_16x16x4_f32 over the foot's 16 contact rows (K = 4 rows each;
@@ -1458,7 +1527,9 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
   st_row(&L->Hs[c.l][0], H);
   L->Hs[c.l][CAP] = Hd;
   tsync();
-  return factor_ldl(c, H, Hd);
+  /* the full build runs with the whole wave (matrix-core Schur complement); a
+     refactor inside the Newton loop may run for one team only (team reductions) */
+  return full ? factor_ldl<true>(c, H, Hd) : factor_ldl<false>(c, H, Hd);
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
@@ -1582,18 +1653,21 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     red[2] = (r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1.f : 0.f;
     tsum_n<3>(red);
     cost = red[0];
+    STAMP(S_UPD);
+    it++;
+    /* mj_solNewton's termination test. MuJoCo runs it after the Hessian update and the new
+       search direction; both only feed the next iteration, so a terminating iteration skips
+       them here (qacc, forces and costs are the same bits either way). */
+    const float improvement = scale * (oldcost - cost);
+    const float gradient = scale * sqrtf(red[1]);
+    if (improvement < cfg->tolerance || gradient < cfg->tolerance || it >= cfg->iterations) break;
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = red[2] > 0.f;
-    STAMP(S_UPD);
     if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo, phi);
     STAMP(S_HESS);
-    float mg = solve_ldl(c, grad, Dinv);
+    const float mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
-    it++;
-    float improvement = scale * (oldcost - cost);
-    float gradient = scale * sqrtf(red[1]);
-    if (improvement < cfg->tolerance || gradient < cfg->tolerance) break;
     search = -mg;
   }
   iters += it;
@@ -1649,7 +1723,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   /* factor M (copy of rows) */
   float X[CAP];
   float Xd = load_mrow(c, X);
-  float DinvM = factor_ldl(c, X, Xd);
+  float DinvM = factor_ldl<true>(c, X, Xd);
   STAMP(S_FACM);
   /* velocities */
   if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < NV ? ls.v : 0.f;
@@ -2504,7 +2578,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   {
     float X[CAP];
     float Xd = load_mrow(c, X);
-    float Dinv = factor_ldl(c, X, Xd);
+    float Dinv = factor_ldl<true>(c, X, Xd);
     if (l < 32) L->vec[V_QVEL][l] = l < NV ? ls.v : 0.f;
     tsync();
     const float qv = l < NV ? ls.v : 0.f;
