@@ -239,6 +239,18 @@ __device__ __forceinline__ void quat2mat(float m[9], const float q[4]) {
   m[3] = 2 * (x * y + w * z); m[4] = 1 - 2 * (x * x + z * z); m[5] = 2 * (y * z - w * x);
   m[6] = 2 * (x * z - w * y); m[7] = 2 * (y * z + w * x); m[8] = 1 - 2 * (x * x + y * y);
 }
+/* r = q v q* for a unit quaternion q = (w, u): v + w t + u x t with t = 2 u x v
+   (21 VALU instead of quat2mat + mulmv3's 30) */
+__device__ __forceinline__ void quat_rotate(float r[3], const float q[4], const float v[3]) {
+  const float u[3] = {q[1], q[2], q[3]};
+  float t[3], c2[3];
+  cross3(t, u, v);
+  t[0] += t[0]; t[1] += t[1]; t[2] += t[2];
+  cross3(c2, u, t);
+  r[0] = v[0] + q[0] * t[0] + c2[0];
+  r[1] = v[1] + q[0] * t[1] + c2[1];
+  r[2] = v[2] + q[0] * t[2] + c2[2];
+}
 __device__ __forceinline__ void mulmv3(float r[3], const float m[9], const float v[3]) {
   float t0 = m[0] * v[0] + m[1] * v[1] + m[2] * v[2];
   float t1 = m[3] * v[0] + m[4] * v[1] + m[5] * v[2];
@@ -467,14 +479,12 @@ __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const La
       if (c.bjt == ZB_JNT_HINGE) {
         float jp[3] = {m->jnt_pos[b][0], m->jnt_pos[b][1], m->jnt_pos[b][2]};
         float ax[3] = {m->jnt_axis[b][0], m->jnt_axis[b][1], m->jnt_axis[b][2]};
-        float R[9], t1[3], t2[3], ql[4], qn[4];
-        quat2mat(R, q);
-        mulmv3(t1, R, jp);
+        float t1[3], t2[3], ql[4], qn[4];
+        quat_rotate(t1, q, jp);
         axis_angle_quat(ql, ax, ang);
         quat_mul(qn, q, ql);
         quat_normalize(qn);
-        quat2mat(R, qn);
-        mulmv3(t2, R, jp);
+        quat_rotate(t2, qn, jp);
 #pragma unroll
         for (int k = 0; k < 3; k++) p[k] += t1[k] - t2[k];
 #pragma unroll
@@ -491,9 +501,8 @@ __device__ __forceinline__ void kinematics(const Ctx& c, const EnvS& s, const La
     for (int k = 0; k < 4; k++) aq[k] = tsh(q[k], anc);
     const int aa = tshi(anc, anc);
     if (anc != 0) {
-      float R[9], t[3], qq[4];
-      quat2mat(R, aq);
-      mulmv3(t, R, p);
+      float t[3], qq[4];
+      quat_rotate(t, aq, p);
 #pragma unroll
       for (int k = 0; k < 3; k++) p[k] = ap[k] + t[k];
       quat_mul(qq, aq, q);
@@ -571,9 +580,9 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 #pragma unroll
     for (int k = 0; k < 3; k++) xipos[k] = B.xp[k] + t[k];
     float iq[4] = {m->body_iquat[isbody ? b : 0][0], m->body_iquat[isbody ? b : 0][1],
-                   m->body_iquat[isbody ? b : 0][2], m->body_iquat[isbody ? b : 0][3]}, iR[9];
-    quat2mat(iR, iq);
-    mulmm3(Ri, BR, iR);
+                   m->body_iquat[isbody ? b : 0][2], m->body_iquat[isbody ? b : 0][3]}, xi[4];
+    quat_mul(xi, B.xq, iq); /* ximat = frame of xquat * body_iquat (mj_local2Global) */
+    quat2mat(Ri, xi);
   }
   float ms[4] = {mass, mass * xipos[0], mass * xipos[1], mass * xipos[2]};
   tsum_n<4>(ms);
@@ -686,6 +695,11 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
         }
       }
       st_row(&L->M[j][0], mr);
+    } else {
+      float z[CAP];
+#pragma unroll
+      for (int e = 0; e < CAP; e++) z[e] = 0.f;
+      st_row(&L->M[j][0], z); /* non-dof lanes: zero rows, so M x needs no lane mask */
     }
   }
   tsync();
@@ -912,13 +926,15 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
     float own[RMAX];
 #pragma unroll
     for (int i = 0; i < RMAX; i++) own[i] = (ischain && i < nroot) ? L->L[c.l][i] : 0.f;
+    /* xr[k] = x_k - sum_{limb j} L(j, k) x_j: root lane k adds its own value into the
+       same team reduction (no separate broadcast of x_k) */
     float sr[RMAX];
 #pragma unroll
-    for (int k = 0; k < RMAX; k++) sr[k] = own[k] * (ischain ? x : 0.f);
+    for (int k = 0; k < RMAX; k++) sr[k] = c.l == k ? x : -own[k] * (ischain ? x : 0.f);
     tsum_n<RMAX>(sr);
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
-      if (k < nroot) xr[k] = team_lane(x, k) - sr[k];
+      if (k < nroot) xr[k] = sr[k];
 #pragma unroll
     for (int k = RMAX - 1; k >= 1; k--)
       if (k < nroot)
@@ -975,7 +991,7 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   for (int e = 0; e < CAP; e++) vv[e] = L->vec[slot][anc_lin(c.chd, e)];
   float y = 0.f;
 #pragma unroll
-  for (int e = 0; e < CAP; e++) y += (j < NV && e <= ddep) ? mrow[e] * vv[e] : 0.f;
+  for (int e = 0; e < CAP; e++) y += mrow[e] * vv[e]; /* rows are zero past the depth */
   if (j < NV) {
     /* limb lanes: transposed part M(k, j) x_k over the deeper dofs of the
        chain (consecutive dofs chd+cps+1 .. chd+cln-1), all loads in flight */
@@ -1021,7 +1037,8 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
   for (int e = 0; e < CAP; e++) vv[e] = c.L->vec[slot][anc_lin(r.chd, e)];
   float v = 0.f;
 #pragma unroll
-  for (int e = 0; e < CAP; e++) v += e <= kdep ? jr[e] * vv[e] : 0.f;
+  for (int e = 0; e < CAP; e++) v += jr[e] * vv[e]; /* zero past the row's depth */
+  (void)kdep;
   return v;
 }
 
@@ -1264,10 +1281,9 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   if (TEAM < 64) tb &= 0xffffffffu;
   r.nrow = __popc(tb);
   r.exmask = tb;
-  if (r.ex) {
-#pragma unroll
-    for (int e = 0; e < CAP; e++) L->u.J[l][e] = Jc[e];
-  }
+  /* every row is stored, zero where there is no contact (and past the row's
+     depth), so the row products below need no per-entry masks */
+  st_row(&L->u.J[l][0], Jc);
   /* ---- dof rows (lane j) ---- */
   r.hf = r.hlo = r.hhi = false;
   r.actf = r.actlo = r.acthi = 0;
@@ -1372,36 +1388,42 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, f
      share the foot's dof chain, so sum_r J_r[e] f_r (e = chain position) is
      a row reduction for all 12 positions at once (interleaved DPP, no LDS);
      a dof adds the sums of every foot whose chain holds it at its depth */
-  float q[CAP];
+  float q[16];
   {
     float jr[CAP];
     ld_row(&L->u.J[c.l][0], jr);
     const float fr = r.ex ? r.f : 0.f;
 #pragma unroll
-    for (int e = 0; e < CAP; e++) q[e] = r.ex ? jr[e] * fr : 0.f;
+    for (int e = 0; e < CAP; e++) q[e] = jr[e] * fr; /* J rows are zero where no contact */
+#pragma unroll
+    for (int e = CAP; e < 16; e++) q[e] = 0.f;
   }
+  /* transposing butterfly over the 16 rows of the foot (pairings: row mirror, half-row
+     mirror, quad xor 2, quad xor 1): at each stage a lane keeps the half of its column
+     sums on its side and adds its partner's copy of them, so lane 16f + e ends with
+     the foot-f sum of column e (45 instead of 108 VALU instructions) */
+  const int li = threadIdx.x & 15;
+  float u8[8], u4[4], u2[2];
+  {
+    const bool s1 = li >= 8;
 #pragma unroll
-  for (int e = 0; e < CAP; e++) q[e] += dppf<0xB1>(q[e]);
+    for (int k = 0; k < 8; k++) u8[k] = (s1 ? q[8 + k] : q[k]) + dppf<0x140>(s1 ? q[k] : q[8 + k]);
+    const bool s2 = (li & 4) != 0;
 #pragma unroll
-  for (int e = 0; e < CAP; e++) q[e] += dppf<0x4E>(q[e]);
+    for (int k = 0; k < 4; k++) u4[k] = (s2 ? u8[4 + k] : u8[k]) + dppf<0x141>(s2 ? u8[k] : u8[4 + k]);
+    const bool s3 = (li & 2) != 0;
 #pragma unroll
-  for (int e = 0; e < CAP; e++) q[e] += dppf<0x141>(q[e]);
-#pragma unroll
-  for (int e = 0; e < CAP; e++) q[e] += dppf<0x140>(q[e]);
-  float so = 0.f, sx = 0.f; /* this row's foot / the other foot, at depth(j) */
-#pragma unroll
-  for (int e = 0; e < CAP; e++) {
-    const float o = xor16f(q[e]);
-    so = e == ddep ? q[e] : so;
-    sx = e == ddep ? o : sx;
+    for (int k = 0; k < 2; k++) u2[k] = (s3 ? u4[2 + k] : u4[k]) + dppf<0x4E>(s3 ? u4[k] : u4[2 + k]);
   }
+  const bool s4 = (li & 1) != 0;
+  const float colsum = (s4 ? u2[1] : u2[0]) + dppf<0xB1>(s4 ? u2[0] : u2[1]);
+  /* a dof adds the column sum at its depth of every foot whose chain holds it */
+  const float so = tsh(colsum, ddep), sx = tsh(colsum, 16 + ddep);
   tsync();
   float qc = 0.f;
   if (c.l < NV) {
-    const int g = (c.l >> 4) & 1;
-    const bool own = (c.rowmask >> (16 * g)) & 0xFFFFu;
-    const bool oth = (c.rowmask >> (16 * (1 - g))) & 0xFFFFu;
-    qc = (own ? so : 0.f) + (oth ? sx : 0.f);
+    const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
+    qc = (f0 ? so : 0.f) + (f1 ? sx : 0.f);
     if (r.hf) qc += r.ff;
     if (r.hlo) qc += r.flo;
     if (r.hhi) qc -= r.fhi;
