@@ -631,31 +631,31 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 #pragma unroll
     for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], bj);
     if (j < NV) {
+      /* branch-free over the dof kinds (the task's dofs are the free joint's 6 and
+         hinges): the motion axis in the body frame is jnt_axis for a hinge and unit
+         axis k-3 for a free-joint rotation, anchored at jnt_pos / the body origin;
+         a free-joint translation k < 3 is the pure linear motion e_k */
+      const bool isfree = c.dfree;
+      const int k = c.dk0;
+      const bool trans = isfree && k < 3;
+      float ja[3], jp[3], t[3], ax[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        ja[i] = isfree ? (k - 3 == i ? 1.f : 0.f) : m->jnt_axis[bj][i];
+        jp[i] = isfree ? 0.f : m->jnt_pos[bj][i];
+      }
+      mulmv3(t, R, jp);
+      mulmv3(ax, R, ja);
+      float off[3] = {cm[0] - (xp[0] + t[0]), cm[1] - (xp[1] + t[1]), cm[2] - (xp[2] + t[2])}, cr[3];
+      cross3(cr, ax, off);
       float cd[6];
-      int jt = m->body_jnttype[bj];
-      if (jt == ZB_JNT_FREE) {
-        int k = j - m->body_dofadr[bj];
-        if (k < 3) {
-          cd[0] = cd[1] = cd[2] = 0.f;
-          cd[3] = k == 0 ? 1.f : 0.f; cd[4] = k == 1 ? 1.f : 0.f; cd[5] = k == 2 ? 1.f : 0.f;
-        } else {
-          float ax[3] = {R[k - 3], R[3 + k - 3], R[6 + k - 3]};
-          float off[3] = {cm[0] - xp[0], cm[1] - xp[1], cm[2] - xp[2]};
-          cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
-          cross3(cd + 3, ax, off);
-        }
-      } else {
-        float jp[3] = {m->jnt_pos[bj][0], m->jnt_pos[bj][1], m->jnt_pos[bj][2]};
-        float ja[3] = {m->jnt_axis[bj][0], m->jnt_axis[bj][1], m->jnt_axis[bj][2]};
-        float t[3], ax[3];
-        mulmv3(t, R, jp);
-        mulmv3(ax, R, ja);
-        float off[3] = {cm[0] - (xp[0] + t[0]), cm[1] - (xp[1] + t[1]), cm[2] - (xp[2] + t[2])};
-        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
-        cross3(cd + 3, ax, off);
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        cd[i] = trans ? 0.f : ax[i];
+        cd[3 + i] = trans ? (k == i ? 1.f : 0.f) : cr[i];
       }
 #pragma unroll
-      for (int k = 0; k < 6; k++) L->cdof[j][k] = cd[k];
+      for (int i = 0; i < 6; i++) L->cdof[j][i] = cd[i];
     }
   }
   /* crb = subtree sums of cinert */
@@ -689,12 +689,12 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const int e = e0 + i;
-          float v = dot6(ca[i], F);
-          if (e == ddep) v += arm;
-          mr[e] = e <= ddep ? v : 0.f;
+          mr[e] = e <= ddep ? dot6(ca[i], F) : 0.f;
         }
       }
       st_row(&L->M[j][0], mr);
+      /* the diagonal (ancestor slot ddep = the dof itself) with the armature */
+      L->M[j][ddep] = dot6(cd, F) + arm;
     } else {
       float z[CAP];
 #pragma unroll
@@ -1084,12 +1084,12 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B, float qv, float 
   const bool isfree = c.dfree;
   const int k0 = c.dk0;
   const int par = (isd && ddep > 0) ? anc_lin(c.chd, ddep - 1) : j;
+  const int src = (isfree && k0 >= 3) ? 2 : par; /* one pull per component */
   float before[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) {
-    const float pp = tsh(P[k], par);
-    const float p2 = team_lane(P[k], 2);
-    before[k] = (isfree && k0 >= 3) ? p2 : (ddep > 0 ? pp : 0.f);
+    const float pp = tsh(P[k], src);
+    before[k] = ddep > 0 ? pp : 0.f;
   }
 #pragma unroll
   for (int k = 0; k < 6; k++) cdd[k] = 0.f;
@@ -1204,22 +1204,21 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
   const bool gvalid = g < NGEOM;
   const int gg = gvalid ? g : 0;
   const int gb = gvalid ? m->geom_body[g] : 0;
-  float R[9], xp[3], xqs[4];
+  float xp[3], xqs[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) xqs[k] = tsh(B.xq[k], gb);
-  quat2mat(R, xqs);
 #pragma unroll
   for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
-  float gp[3] = {m->geom_pos[gg][0], m->geom_pos[gg][1], m->geom_pos[gg][2]}, t[3];
-  float gq[4] = {m->geom_quat[gg][0], m->geom_quat[gg][1], m->geom_quat[gg][2], m->geom_quat[gg][3]}, gR0[9], gR[9];
-  mulmv3(t, R, gp);
-  float gpos[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
-  quat2mat(gR0, gq);
-  mulmm3(gR, R, gR0);
+  /* corner in the body frame (geom_pos + geom_quat * local corner), then to the
+     world by the body's frame: two quaternion rotations */
+  float gq[4] = {m->geom_quat[gg][0], m->geom_quat[gg][1], m->geom_quat[gg][2], m->geom_quat[gg][3]}, t[3], gl[3];
   float loc[3] = {(corner & 1) ? m->geom_size[gg][0] : -m->geom_size[gg][0],
                   (corner & 2) ? m->geom_size[gg][1] : -m->geom_size[gg][1], -m->geom_size[gg][2]};
-  mulmv3(t, gR, loc);
-  float p[3] = {gpos[0] + t[0], gpos[1] + t[1], gpos[2] + t[2]};
+  quat_rotate(t, gq, loc);
+#pragma unroll
+  for (int k = 0; k < 3; k++) gl[k] = m->geom_pos[gg][k] + t[k];
+  quat_rotate(t, xqs, gl);
+  float p[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
   float dist = p[2];
   pos[0] = p[0]; pos[1] = p[1]; pos[2] = p[2] - 0.5f * dist;
   mu = m->floor_friction[0] * s.floor_mu;
@@ -1301,21 +1300,34 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
     const float floss = c.L->par[P_FLOSS][c.l];
     const bool lim = m->dof_limited[l] != 0;
     const float dlo = ls.q - m->dof_range[l][0], dhi = m->dof_range[l][1] - ls.q;
-    float D0, R0, a0, D1, R1, a1, D2, R2, a2;
-    row_params(m->dof_solref, m->dof_solimp, 0.f, dA, v, cfg->dt, D0, R0, a0);
-    row_params(m->dof_solref, m->dof_solimp, dlo, dA, v, cfg->dt, D1, R1, a1);
-    row_params(m->dof_solref, m->dof_solimp, dhi, dA, -v, cfg->dt, D2, R2, a2);
+    /* frictionloss row: pos = 0, so the impedance is solimp's dmin (dmax when the
+       width is zero) and aref = -b v (mj_makeImpedance at distance 0) */
+    float D0, R0, a0;
+    {
+      const auto si = m->dof_solimp;
+      const float tc = fmaxf(m->dof_solref[0], 2.f * cfg->dt), dmax = si[1];
+      const float imp = fminf(fmaxf(si[2] <= MINVAL ? dmax : si[0], MINIMP), MAXIMP);
+      R0 = fmaxf((1.f - imp) / imp * dA, MINVAL);
+      D0 = 1.f / R0;
+      a0 = -(2.f / (dmax * tc)) * v;
+    }
     r.hf = floss > 0.f;
     r.fl = r.hf ? floss : 0.f;
     r.Df = r.hf ? D0 : 0.f;
     r.Rf = r.hf ? R0 : 0.f;
     r.af = r.hf ? a0 : 0.f;
     r.hlo = lim && dlo < 0.f;
-    r.Dlo = r.hlo ? D1 : 0.f;
-    r.alo = r.hlo ? a1 : 0.f;
     r.hhi = lim && dhi < 0.f;
-    r.Dhi = r.hhi ? D2 : 0.f;
-    r.ahi = r.hhi ? a2 : 0.f;
+    /* joint-limit rows exist only past a limit (at most one side per dof): one row
+       evaluation, and none at all when no dof of the wave is past a limit */
+    if (__ballot(r.hlo || r.hhi) != 0ull) {
+      float D1, R1, a1;
+      row_params(m->dof_solref, m->dof_solimp, r.hlo ? dlo : dhi, dA, r.hlo ? v : -v, cfg->dt, D1, R1, a1);
+      r.Dlo = r.hlo ? D1 : 0.f;
+      r.alo = r.hlo ? a1 : 0.f;
+      r.Dhi = r.hhi ? D1 : 0.f;
+      r.ahi = r.hhi ? a1 : 0.f;
+    }
   }
   tsync();
 }
