@@ -169,6 +169,39 @@ __device__ __forceinline__ void tsum_n(float v[N]) {
     v[i] = a + b;
   }
 }
+/* 21 team sums (the root Schur complement), written to out[0..20] in LDS: a
+ * transposing butterfly instead of 21 all-lane reductions. Rows 0/1 of the team
+ * first exchange halves with v_permlane16_swap (value i stays in row 0, value
+ * 11 + i in row 1), then four DPP stages inside each 16-lane row each keep the
+ * half of the slots on the lane's side and add the partner's copy of them, so
+ * lane 16r + c ends with the full sum of value 11r + c (67 VALU instructions
+ * instead of 126). The caller syncs before reading out[]. */
+__device__ __forceinline__ void reduce21_to(const float v[21], float* out) {
+  float w[16];
+#pragma unroll
+  for (int i = 0; i < 11; i++) {
+    const float hi = i + 11 < 21 ? v[i + 11] : 0.f;
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(hi), false, false);
+    w[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 11; i < 16; i++) w[i] = 0.f;
+  const int li = threadIdx.x & 15;
+  float u8[8], u4[4], u2[2];
+  const bool s1 = li >= 8;
+#pragma unroll
+  for (int k = 0; k < 8; k++) u8[k] = (s1 ? w[8 + k] : w[k]) + dppf<0x140>(s1 ? w[k] : w[8 + k]);
+  const bool s2 = (li & 4) != 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) u4[k] = (s2 ? u8[4 + k] : u8[k]) + dppf<0x141>(s2 ? u8[k] : u8[4 + k]);
+  const bool s3 = (li & 2) != 0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) u2[k] = (s3 ? u4[2 + k] : u4[k]) + dppf<0x4E>(s3 ? u4[k] : u4[2 + k]);
+  const bool s4 = (li & 1) != 0;
+  const float sum = (s4 ? u2[1] : u2[0]) + dppf<0xB1>(s4 ? u2[0] : u2[1]);
+  const int idx = ((threadIdx.x & 16) ? 11 : 0) + li;
+  if (li < 11 && idx < 21) out[idx] = sum;
+}
 __device__ __forceinline__ float tmaxf(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
@@ -800,8 +833,10 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
     Xd -= sc * t;
 #pragma unroll
     for (int e = 0; e < NROOT; e++) X[e] -= sc * r[e];
+    /* entries at chain positions >= the lane's own are never read (a pivot at
+       level p only hands out positions < p), so no mask */
 #pragma unroll
-    for (int e = NROOT; e < NROOT + q - 1; e++) X[e] -= (e < ddep ? sc : 0.f) * r[e];
+    for (int e = NROOT; e < NROOT + q - 1; e++) X[e] -= sc * r[e];
     wacc[q] += sc;
 #pragma unroll
     for (int k = q + 1; k < NLIMBLV; k++) wacc[k] -= sc * wq[k];
@@ -833,6 +868,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
 #pragma unroll
       for (int t = 0; t < NG; t++) g[t] = L->vec[V_TMP2][t];
     } else {
+      static_assert(NG == 21, "reduce21_to");
       int t = 0;
 #pragma unroll
       for (int i = 0; i < RMAX; i++) {
@@ -840,7 +876,10 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
 #pragma unroll
         for (int j = 0; j <= i; j++) g[t++] = wi * X[j];
       }
-      tsum_n<NG>(g);
+      reduce21_to(g, &L->vec[V_TMP2][0]);
+      tsync();
+#pragma unroll
+      for (int t2 = 0; t2 < NG; t2++) g[t2] = L->vec[V_TMP2][t2];
     }
     float A[RMAX][RMAX], D[RMAX];
     {
@@ -862,11 +901,15 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
         const float Dkv = fmaxf(D[k], MINVAL);
         const float inv = 1.0f / Dkv;
         D[k] = Dkv;
-#pragma unroll
-        for (int i = 0; i < k; i++) A[k][i] = A[k][i] * inv;
+        float tk[RMAX]; /* the unscaled row: the update multiplier A(k,i) = L(k,i) D_k */
 #pragma unroll
         for (int i = 0; i < k; i++) {
-          const float t = A[k][i] * Dkv;
+          tk[i] = A[k][i];
+          A[k][i] = A[k][i] * inv;
+        }
+#pragma unroll
+        for (int i = 0; i < k; i++) {
+          const float t = tk[i];
           D[i] -= t * A[k][i];
 #pragma unroll
           for (int e = 0; e < i; e++) A[i][e] -= t * A[k][e];

@@ -49,6 +49,8 @@ PROBES = {
             f"  {{ {B} float ca2[6]; for (int k = 0; k < 6; k++) ca2[k] = opqf(ca[k]); float d_ = rne_project(c, B, ca2, zero6); SINK(d_); }}\n"),
     "solve_sm": ("  float qs = solve_ldl(c, fs, DinvM);",
                  f"  {{ {B} float d_ = solve_ldl(c, opqf(fs), DinvM); SINK(d_); }}\n"),
+    "ls": ("    float alpha = line_search(c, r, search, Ma, fs, Mv);",
+           f"    {{ {B} Rows r2 = r; float mv2; float a2 = line_search(c, r2, opqf(search), Ma, fs, mv2); SINK(a2); SINK(mv2); }}\n"),
     "comvel": ("  com_vel(c, B, qv, cdd);\n  float ca[6], zero6",
                f"  {{ {B} BodyK B2 = B; float c2[6]; com_vel(c, B2, opqf(qv), c2); SINK(c2[0]); SINK(B2.cv[0]); }}\n"),
 }
