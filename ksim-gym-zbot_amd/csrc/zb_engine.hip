@@ -728,12 +728,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
       st_row(&L->M[j][0], mr);
       /* the diagonal (ancestor slot ddep = the dof itself) with the armature */
       L->M[j][ddep] = dot6(cd, F) + arm;
-    } else {
-      float z[CAP];
-#pragma unroll
-      for (int e = 0; e < CAP; e++) z[e] = 0.f;
-      st_row(&L->M[j][0], z); /* non-dof lanes: zero rows, so M x needs no lane mask */
-    }
+    } /* non-dof lanes keep the zero rows make_ctx stored, so M x needs no lane mask */
   }
   tsync();
 }
@@ -952,13 +947,14 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   const int cps = vopq(c.cps), cln = vopq(c.cln), chd = ischain ? c.chd : 0;
   /* forward pass along the limbs: the chain's deeper right-hand sides, all in flight */
   {
+    /* W(p, k) is zero for k <= p and past the chain, so only non-chain lanes mask it */
     float w[CAP], bk[NLIMBLV];
     ld_row(&L->L[c.l & 31][0], w);
 #pragma unroll
-    for (int k = 1; k < NLIMBLV; k++) bk[k] = tsh(x, (ischain && k < cln) ? chd + k : c.l);
+    for (int k = 1; k < NLIMBLV; k++) bk[k] = tsh(x, chd + k);
     float z = x;
 #pragma unroll
-    for (int k = 1; k < NLIMBLV; k++) z += (ischain && k > cps && k < cln) ? w[NROOT + k] * bk[k] : 0.f;
+    for (int k = 1; k < NLIMBLV; k++) z += (ischain ? w[NROOT + k] : 0.f) * bk[k];
     x = z;
   }
   /* root chain, dense and redundant in every lane */
@@ -1006,13 +1002,13 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
     float va[NLIMBLV - 1], wa[NLIMBLV - 1];
 #pragma unroll
     for (int a = 0; a < NLIMBLV - 1; a++) {
-      const bool on = ischain && a < cps;
-      va[a] = tsh(x, on ? chd + a : c.l);
-      wa[a] = L->L[on ? chd + a : 0][NROOT + (cps < NLIMBLV ? cps : 0)];
+      va[a] = tsh(x, chd + a);
+      /* W(a, p) of a shallower chain position; row 31 (zero) otherwise */
+      wa[a] = L->L[(ischain && a < cps) ? chd + a : 31][NROOT + cps];
     }
     float y = x;
 #pragma unroll
-    for (int a = 0; a < NLIMBLV - 1; a++) y += (ischain && a < cps) ? wa[a] * va[a] : 0.f;
+    for (int a = 0; a < NLIMBLV - 1; a++) y += wa[a] * va[a];
     x = y;
   }
   return x;
@@ -1041,11 +1037,12 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
     float a[NLIMBLV - 1];
 #pragma unroll
     for (int q = 1; q < NLIMBLV; q++) {
-      const int k = ischain ? min(c.chd + c.cps + q, NV - 1) : j;
+      /* past the chain: row 31, a zero row of a non-dof lane */
+      const int k = (ischain && c.cps + q < c.cln) ? c.chd + c.cps + q : 31;
       a[q - 1] = L->M[k][ddep] * L->vec[slot][k];
     }
 #pragma unroll
-    for (int q = 1; q < NLIMBLV; q++) y += (ischain && c.cps + q < c.cln) ? a[q - 1] : 0.f;
+    for (int q = 1; q < NLIMBLV; q++) y += a[q - 1];
   }
   if (nroot > 0) {
     /* root lanes: limb dofs by one team reduction per root dof (their
@@ -1062,8 +1059,8 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
     float yr = 0.f;
 #pragma unroll
     for (int k = 1; k < RMAX; k++) {
-      const float mk = L->M[k][jr] * L->vec[slot][k];
-      yr += (k < nroot && k > j) ? mk : 0.f;
+      const int kk = (k < nroot && k > j) ? k : 31; /* row 31 is zero */
+      yr += L->M[kk][jr] * L->vec[slot][kk];
     }
     if (j < nroot) y += yr + sr;
   }
@@ -1610,51 +1607,59 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
-__device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float& Mv) {
+__device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float grad,
+                                             float& Mv) {
   CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
   r.Jv = r.ex ? row_dot(c, r, V_TMP) : 0.f;
   tsync();
-  float cc[2] = {c.l < NV ? search * (Ma - fs) : 0.f, c.l < NV ? search * Mv : 0.f};
-  tsum_n<2>(cc);
+  /* the quadratic's coefficients and the slope/curvature at alpha = 0 in one reduction:
+     d1(0) = search . grad (the gradient update_constraint left for the current active
+     set), d2(0) = c2 + sum of D (J search)^2 over the rows active now */
+  const bool isd = c.l < NV;
+  const float jv0 = isd ? search : 0.f;
+  float g20 = (r.ex && r.act) ? r.D * r.Jv * r.Jv : 0.f;
+  g20 += (r.hf && r.actf) ? r.Df * jv0 * jv0 : 0.f;
+  g20 += (r.hlo && r.actlo) ? r.Dlo * jv0 * jv0 : 0.f;
+  g20 += (r.hhi && r.acthi) ? r.Dhi * jv0 * jv0 : 0.f;
+  float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
+  tsum_n<4>(cc);
   const float c1 = cc[0], c2 = cc[1];
+  /* per-row constants of the piecewise quadratic along the search direction (the
+     two joint-limit rows of a dof are folded into one: at most one side exists) */
+  const float DJ = r.D * r.Jv, DJ2 = DJ * r.Jv;
+  const float Rf = r.Rf * r.fl, FJ = r.fl * jv0, DfJ = r.Df * jv0, DfJ2 = DfJ * jv0;
+  const bool hl = r.hlo || r.hhi;
+  const float sv = r.hlo ? jv0 : -jv0, jl0 = r.hlo ? r.jlo : r.jhi;
+  const float DlJ = (r.hlo ? r.Dlo : r.Dhi) * sv, DlJ2 = DlJ * sv;
   auto eval = [&](float alpha, float& d1, float& d2) {
-    /* piecewise-quadratic row terms, branch-free (rows with a zero
-       direction contribute exact zeros, as the branchy form skips them) */
-    float g1 = 0.f, g2 = 0.f;
+    /* branch-free; rows that do not exist or are inactive add exact zeros */
+    float g1, g2;
     {
       const float x = r.jar + alpha * r.Jv;
       const bool on = r.ex && x < 0.f;
-      g1 += on ? r.D * x * r.Jv : 0.f;
-      g2 += on ? r.D * r.Jv * r.Jv : 0.f;
+      g1 = on ? DJ * x : 0.f;
+      g2 = on ? DJ2 : 0.f;
     }
-    const float jv = c.l < NV ? search : 0.f;
     {
-      const float x = r.jf + alpha * jv, Rf = r.Rf * r.fl;
+      const float x = r.jf + alpha * jv0;
       const bool lo = x <= -Rf, hi = x >= Rf;
-      g1 += r.hf ? (lo ? -(r.fl * jv) : (hi ? r.fl * jv : r.Df * x * jv)) : 0.f;
-      g2 += (r.hf && !lo && !hi) ? r.Df * jv * jv : 0.f;
+      g1 += r.hf ? (lo ? -FJ : (hi ? FJ : DfJ * x)) : 0.f;
+      g2 += (r.hf && !lo && !hi) ? DfJ2 : 0.f;
     }
     {
-      const float x = r.jlo + alpha * jv;
-      const bool on = r.hlo && x < 0.f;
-      g1 += on ? r.Dlo * x * jv : 0.f;
-      g2 += on ? r.Dlo * jv * jv : 0.f;
-    }
-    {
-      const float x = r.jhi - alpha * jv;
-      const bool on = r.hhi && x < 0.f;
-      g1 += on ? r.Dhi * x * (-jv) : 0.f;
-      g2 += on ? r.Dhi * jv * jv : 0.f;
+      const float x = jl0 + alpha * sv;
+      const bool on = hl && x < 0.f;
+      g1 += on ? DlJ * x : 0.f;
+      g2 += on ? DlJ2 : 0.f;
     }
     float gg[2] = {g1, g2};
     tsum_n<2>(gg);
     d1 = c1 + alpha * c2 + gg[0];
     d2 = c2 + gg[1];
   };
-  float d1, d2;
-  eval(0.f, d1, d2);
+  float d1 = cc[2], d2 = c2 + cc[3];
   if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
   float gtol = cfg->ls_tolerance * (-d1);
   float lo = 0.f, hi = -1.f;
@@ -1711,7 +1716,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   while (live && it < cfg->iterations) {
     float Mv;
     STAMP(S_CHECK);
-    float alpha = line_search(c, r, search, Ma, fs, Mv);
+    float alpha = line_search(c, r, search, Ma, fs, grad, Mv);
     STAMP(S_LS);
     if (alpha == 0.f) break;
     x += alpha * search;
@@ -2426,6 +2431,15 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
     if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm |= 0xFFFFu << (16 * g);
   }
   c.rowmask = rm;
+  if (!isd) {
+    /* non-dof lanes: zero factor and mass rows (row 31 is the zero row that masked
+       gathers point at; kernels never write these rows afterwards) */
+    float z[CAP];
+#pragma unroll
+    for (int e = 0; e < CAP; e++) z[e] = 0.f;
+    st_row(&L->L[l][0], z);
+    st_row(&L->M[l][0], z);
+  }
   c.dk0 = isd ? l - m->body_dofadr[c.dbody] : 0;
   c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
   {
