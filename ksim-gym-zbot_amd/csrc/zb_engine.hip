@@ -458,10 +458,11 @@ struct Rows {
   float aref, D, jar, Jv, f;
   int act;
   /* dof rows: frictionloss, lower, upper limit */
-  bool hf, hlo, hhi;
+  bool hf, hl;
   float af, Df, Rf, fl, jf, ff; int actf;
-  float alo, Dlo, jlo, flo; int actlo;
-  float ahi, Dhi, jhi, fhi; int acthi;
+  /* the joint-limit row (exists only past a limit, at most one side per dof):
+     Jacobian sl * e_dof (sl = +1 lower, -1 upper), jl = sl * qacc - al */
+  float sl, al, Dl, jl, flim; int actl;
   int nrow;
   uint32_t exmask; /* team-uniform: existing contact rows */
 };
@@ -1324,12 +1325,13 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
      depth), so the row products below need no per-entry masks */
   st_row(&L->u.J[l][0], Jc);
   /* ---- dof rows (lane j) ---- */
-  r.hf = r.hlo = r.hhi = false;
-  r.actf = r.actlo = r.acthi = 0;
-  r.ff = r.flo = r.fhi = 0.f;
-  r.jf = r.jlo = r.jhi = 0.f;
-  r.Df = r.Dlo = r.Dhi = 0.f;
-  r.af = r.alo = r.ahi = 0.f;
+  r.hf = r.hl = false;
+  r.actf = r.actl = 0;
+  r.ff = r.flim = 0.f;
+  r.jf = r.jl = 0.f;
+  r.Df = r.Dl = 0.f;
+  r.af = r.al = 0.f;
+  r.sl = 1.f;
   r.Rf = 0.f;
   r.fl = 0.f;
   if (l < NV) {
@@ -1356,17 +1358,16 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
     r.Df = r.hf ? D0 : 0.f;
     r.Rf = r.hf ? R0 : 0.f;
     r.af = r.hf ? a0 : 0.f;
-    r.hlo = lim && dlo < 0.f;
-    r.hhi = lim && dhi < 0.f;
+    const bool hlo = lim && dlo < 0.f, hhi = lim && dhi < 0.f;
+    r.hl = hlo || hhi;
+    r.sl = hhi ? -1.f : 1.f;
     /* joint-limit rows exist only past a limit (at most one side per dof): one row
        evaluation, and none at all when no dof of the wave is past a limit */
-    if (__ballot(r.hlo || r.hhi) != 0ull) {
+    if (__ballot(r.hl) != 0ull) {
       float D1, R1, a1;
-      row_params(m->dof_solref, m->dof_solimp, r.hlo ? dlo : dhi, dA, r.hlo ? v : -v, cfg->dt, D1, R1, a1);
-      r.Dlo = r.hlo ? D1 : 0.f;
-      r.alo = r.hlo ? a1 : 0.f;
-      r.Dhi = r.hhi ? D1 : 0.f;
-      r.ahi = r.hhi ? a1 : 0.f;
+      row_params(m->dof_solref, m->dof_solimp, hlo ? dlo : dhi, dA, r.sl * v, cfg->dt, D1, R1, a1);
+      r.Dl = r.hl ? D1 : 0.f;
+      r.al = r.hl ? a1 : 0.f;
     }
   }
   tsync();
@@ -1389,18 +1390,16 @@ __device__ __forceinline__ float eval_one(float jar, float D, float& force, int&
 }
 
 /* row costs at given jar values (no state change) */
-__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jlo_, float jhi_) {
+__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jl_) {
   float f;
   int a;
   const float k0 = eval_one(jc, r.D, f, a);
   const float k1 = eval_fric(jf_, r.Df, r.Rf, r.fl, f, a);
-  const float k2 = eval_one(jlo_, r.Dlo, f, a);
-  const float k3 = eval_one(jhi_, r.Dhi, f, a);
+  const float k2 = eval_one(jl_, r.Dl, f, a);
   float cost = 0.f;
   cost += r.ex ? k0 : 0.f;
   cost += r.hf ? k1 : 0.f;
-  cost += r.hlo ? k2 : 0.f;
-  cost += r.hhi ? k3 : 0.f;
+  cost += r.hl ? k2 : 0.f;
   return cost;
 }
 
@@ -1419,20 +1418,16 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, f
     int a0, a1, a2, a3;
     const float k0 = eval_one(r.jar, r.D, f0, a0);
     const float k1 = eval_fric(r.jf, r.Df, r.Rf, r.fl, f1, a1);
-    const float k2 = eval_one(r.jlo, r.Dlo, f2, a2);
-    const float k3 = eval_one(r.jhi, r.Dhi, f3, a3);
+    const float k2 = eval_one(r.jl, r.Dl, f2, a2);
     cost += r.ex ? k0 : 0.f;
     cost += r.hf ? k1 : 0.f;
-    cost += r.hlo ? k2 : 0.f;
-    cost += r.hhi ? k3 : 0.f;
+    cost += r.hl ? k2 : 0.f;
     r.f = r.ex ? f0 : r.f;
     r.act = r.ex ? a0 : r.act;
     r.ff = r.hf ? f1 : r.ff;
     r.actf = r.hf ? a1 : r.actf;
-    r.flo = r.hlo ? f2 : r.flo;
-    r.actlo = r.hlo ? a2 : r.actlo;
-    r.fhi = r.hhi ? f3 : r.fhi;
-    r.acthi = r.hhi ? a3 : r.acthi;
+    r.flim = r.hl ? f2 : r.flim;
+    r.actl = r.hl ? a2 : r.actl;
   }
   if (r.ex) L->rowF[c.l] = r.f;
   L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
@@ -1477,8 +1472,7 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, f
     const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
     qc = (f0 ? so : 0.f) + (f1 ? sx : 0.f);
     if (r.hf) qc += r.ff;
-    if (r.hlo) qc += r.flo;
-    if (r.hhi) qc -= r.fhi;
+    if (r.hl) qc += r.sl * r.flim;
   }
   grad = Ma - fs - qc;
   return cost;
@@ -1510,11 +1504,11 @@ __device__ __forceinline__ void jdj_mfma() {
 #pragma unroll
       for (int f = 0; f < NGEOM; f++) {
         const int r = 16 * f + 4 * ch + k;
+        /* no masks: rowDA is zero for absent / inactive rows, and output rows or
+           columns e >= CAP (lanes reading entry CAP-1) are never stored */
         const float jv = g_lds[t].u.J[r][ec];
         const float dv = g_lds[t].rowDA[r];
-        const bool on = dv != 0.f && e < CAP;
-        const float a = on ? dv * jv : 0.f, b = on ? jv : 0.f;
-        acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t][f], 0, 0, 0);
+        acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv * jv, jv, acc[t][f], 0, 0, 0);
       }
   /* lane l holds G[4*(l/16) + v][l%16] */
 #pragma unroll
@@ -1534,8 +1528,7 @@ __device__ __forceinline__ void jdj_mfma() {
  * H of the previous build is updated with the rows whose activity changed
  * (+-D_r J_r J_r') -- MuJoCo's Newton also only re-assembles on a change of
  * the active set, and the change is usually a handful of rows. */
-__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo,
-                                                int phi) {
+__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float H[CAP], Hd;
@@ -1553,7 +1546,9 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
       ld_row(G + CAP * CAP, g1);
       const float d0 = G[ddep], d1 = G[CAP * CAP + ddep];
 #pragma unroll
-      for (int e = 0; e < CAP; e++) H[e] += e < ddep ? (f0 ? g0[e] : 0.f) + (f1 ? g1[e] : 0.f) : 0.f;
+      /* entries at or past the lane's depth are never read by the factorization,
+         so they need no mask */
+      for (int e = 0; e < CAP; e++) H[e] += (f0 ? g0[e] : 0.f) + (f1 ? g1[e] : 0.f);
       Hd += (f0 ? d0 : 0.f) + (f1 ? d1 : 0.f);
     }
   } else {
@@ -1582,19 +1577,17 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
       Hd += jj1 * jd1;
 #pragma unroll
       for (int e = 0; e < CAP; e++) {
-        H[e] += (e < ddep ? jj0 : 0.f) * j0[e];
-        H[e] += (e < ddep ? jj1 : 0.f) * j1[e];
+        H[e] += jj0 * j0[e]; /* entries at or past the depth are never read */
+        H[e] += jj1 * j1[e];
       }
     }
     float dd = 0.f;
     if (full) {
       if (r.hf && r.actf) dd += r.Df;
-      if (r.hlo && r.actlo) dd += r.Dlo;
-      if (r.hhi && r.acthi) dd += r.Dhi;
+      if (r.hl && r.actl) dd += r.Dl;
     } else {
       if (r.hf) dd += (float)(r.actf - pf) * r.Df;
-      if (r.hlo) dd += (float)(r.actlo - plo) * r.Dlo;
-      if (r.hhi) dd += (float)(r.acthi - phi) * r.Dhi;
+      if (r.hl) dd += (float)(r.actl - plo) * r.Dl;
     }
     Hd += dd;
   }
@@ -1621,8 +1614,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   const float jv0 = isd ? search : 0.f;
   float g20 = (r.ex && r.act) ? r.D * r.Jv * r.Jv : 0.f;
   g20 += (r.hf && r.actf) ? r.Df * jv0 * jv0 : 0.f;
-  g20 += (r.hlo && r.actlo) ? r.Dlo * jv0 * jv0 : 0.f;
-  g20 += (r.hhi && r.acthi) ? r.Dhi * jv0 * jv0 : 0.f;
+  g20 += (r.hl && r.actl) ? r.Dl * jv0 * jv0 : 0.f;
   float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
   tsum_n<4>(cc);
   const float c1 = cc[0], c2 = cc[1];
@@ -1630,9 +1622,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
      two joint-limit rows of a dof are folded into one: at most one side exists) */
   const float DJ = r.D * r.Jv, DJ2 = DJ * r.Jv;
   const float Rf = r.Rf * r.fl, FJ = r.fl * jv0, DfJ = r.Df * jv0, DfJ2 = DfJ * jv0;
-  const bool hl = r.hlo || r.hhi;
-  const float sv = r.hlo ? jv0 : -jv0, jl0 = r.hlo ? r.jlo : r.jhi;
-  const float DlJ = (r.hlo ? r.Dlo : r.Dhi) * sv, DlJ2 = DlJ * sv;
+  const bool hl = r.hl;
+  const float sv = r.sl * jv0, jl0 = r.jl;
+  const float DlJ = r.Dl * sv, DlJ2 = DlJ * sv;
   auto eval = [&](float alpha, float& d1, float& d2) {
     /* branch-free; rows that do not exist or are inactive add exact zeros */
     float g1, g2;
@@ -1689,8 +1681,8 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float jw = r.ex ? row_dot(c, r, V_TMP) - r.aref : 0.f;
   float js = r.ex ? row_dot(c, r, V_TMP2) - r.aref : 0.f;
   tsync();
-  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, x - r.alo, -x - r.ahi),
-                  rows_cost(c, r, js, qs - r.af, qs - r.alo, -qs - r.ahi)};
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, r.sl * x - r.al),
+                  rows_cost(c, r, js, qs - r.af, r.sl * qs - r.al)};
   tsum_n<2>(cws);
   const float cw = cws[0], cs = cws[1];
   if (cw > cs) {
@@ -1702,13 +1694,12 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   }
   STAMP(S_WARM);
   r.jf = x - r.af;
-  r.jlo = x - r.alo;
-  r.jhi = -x - r.ahi;
+  r.jl = r.sl * x - r.al;
   float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
   float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
-  float Dinv = hessian_factor(c, r, true, 0, 0, 0, 0);
+  float Dinv = hessian_factor(c, r, true, 0, 0, 0);
   STAMP(S_HESS0);
   float search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
@@ -1723,16 +1714,15 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
     r.jf += alpha * search;
-    r.jlo += alpha * search;
-    r.jhi -= alpha * search;
+    r.jl += alpha * (r.sl * search);
     float oldcost = cost;
-    const int pa = r.act, pf = r.actf, plo = r.actlo, phi = r.acthi;
+    const int pa = r.act, pf = r.actf, plo = r.actl;
     /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
        value, so the bits of separate tsum calls): cost, |grad|^2 and the active-set change */
     float red[3];
     red[0] = update_constraint_lane(c, r, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
-    red[2] = (r.act != pa || r.actf != pf || r.actlo != plo || r.acthi != phi) ? 1.f : 0.f;
+    red[2] = (r.act != pa || r.actf != pf || r.actl != plo) ? 1.f : 0.f;
     tsum_n<3>(red);
     cost = red[0];
     STAMP(S_UPD);
@@ -1746,7 +1736,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = red[2] > 0.f;
-    if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo, phi);
+    if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo);
     STAMP(S_HESS);
     const float mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
@@ -1832,7 +1822,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   /* constraints */
   make_constraints(c, s, ls, B, cm, r);
   STAMP(S_CON);
-  int nrows = tmaxi(r.nrow + (r.hf || r.hlo || r.hhi ? 1 : 0));
+  int nrows = tmaxi(r.nrow + (r.hf || r.hl ? 1 : 0));
   float qacc;
   /* entered by the whole wave when either env has rows (the full Hessian
      build runs on the matrix cores and needs every lane); an env without
@@ -2655,7 +2645,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = c.L->ci[l][k];
     for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
   }
-  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (r.hf ? 1 : 0) + (r.hlo ? 1 : 0) + (r.hhi ? 1 : 0)));
+  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (r.hf ? 1 : 0) + (r.hl ? 1 : 0)));
   if (l == 0) {
     d[ZB_DBG_MISC + 0] = (float)nefc;
     d[ZB_DBG_MISC + 1] = (float)(r.nrow / 4);

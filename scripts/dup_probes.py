@@ -25,10 +25,8 @@ PROBES = {
     # (anchor, code inserted BEFORE the anchor)
     "mulm_ls": ("  Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */",
                 f"  {{ {B} float d_ = mul_m(c, opqf(search), V_TMP); SINK(d_); }}\n"),
-    "rowdot_ls": ("  tsync();\n  float cc[2] = {",
+    "rowdot_ls": ("  tsync();\n  /* the quadratic's coefficients",
                   f"  {{ {B} float d_ = r.ex ? row_dot(c, r, V_TMP) : 0.f; SINK(d_); }}\n"),
-    "eval0": ("  if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;",
-              f"  {{ {B} float e1_, e2_; eval(opqf(0.f), e1_, e2_); SINK(e1_); SINK(e2_); }}\n"),
     "update": ("    red[0] = update_constraint_lane(c, r, x, qs, fs, Ma, grad);",
                f"    {{ {B} Rows r2 = r; float g2_; float d_ = update_constraint_lane(c, r2, opqf(x), qs, fs, Ma, g2_); SINK(d_); SINK(g2_); }}\n"),
     "solve_nw": ("    const float mg = solve_ldl(c, grad, Dinv);",
@@ -49,8 +47,14 @@ PROBES = {
             f"  {{ {B} float ca2[6]; for (int k = 0; k < 6; k++) ca2[k] = opqf(ca[k]); float d_ = rne_project(c, B, ca2, zero6); SINK(d_); }}\n"),
     "solve_sm": ("  float qs = solve_ldl(c, fs, DinvM);",
                  f"  {{ {B} float d_ = solve_ldl(c, opqf(fs), DinvM); SINK(d_); }}\n"),
-    "ls": ("    float alpha = line_search(c, r, search, Ma, fs, Mv);",
-           f"    {{ {B} Rows r2 = r; float mv2; float a2 = line_search(c, r2, opqf(search), Ma, fs, mv2); SINK(a2); SINK(mv2); }}\n"),
+    "ls": ("    float alpha = line_search(c, r, search, Ma, fs, grad, Mv);",
+           f"    {{ {B} Rows r2 = r; float mv2; float a2 = line_search(c, r2, opqf(search), Ma, fs, grad, mv2); SINK(a2); SINK(mv2); }}\n"),
+    "hess_full": ("  float Dinv = hessian_factor(c, r, true, 0, 0, 0);",
+                  f"  {{ {B} float d_ = hessian_factor(c, r, true, 0, 0, 0); SINK(d_); }}\n"),
+    "warm": ("  STAMP(S_WARM);",
+             f"  {{ {B} float Ma2 = mul_m(c, opqf(x), V_TMP); SINK(Ma2); }}\n"),
+    "jdj": ("    jdj_mfma();",
+            f"    {{ {B} jdj_mfma(); }}\n"),
     "comvel": ("  com_vel(c, B, qv, cdd);\n  float ca[6], zero6",
                f"  {{ {B} BodyK B2 = B; float c2[6]; com_vel(c, B2, opqf(qv), c2); SINK(c2[0]); SINK(B2.cv[0]); }}\n"),
 }
