@@ -42,6 +42,9 @@ def lib(precision: str = "f32") -> C.CDLL:
     L.zbo_forward_debug.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp,
                                     C.POINTER(C.c_int), fp]
     L.zbo_simulate.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, C.c_int]
+    L.zbo_constraint_debug.argtypes = [C.c_void_p, C.c_void_p, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp,
+                                       C.POINTER(C.c_int)]
+    L.zbo_constraint_debug.restype = C.c_int
     L.zbo_trapezoidal_step.argtypes = [fp, fp, fp, C.c_float, fp, fp, C.c_int, fp, fp]
     L.zbo_rotate_quat_by_quat.argtypes = [fp, fp, C.c_int, fp]
     L.zbo_feetech.argtypes = [C.c_void_p, C.c_float, fp, fp, fp, fp, fp, fp, fp, fp]
@@ -163,6 +166,28 @@ def forward_debug(cmodel, cfg, qpos, qvel, ctrl=None, precision: str = "f32") ->
                                      _p(out["cinert"]), _p(out["cvel"]), nn, _p(out["touch"]))
     out["nefc"], out["ncon"] = nn[0], nn[1]
     return out
+
+
+def constraint_problem(cmodel, cfg, qpos, qvel, ctrl=None, qaccw=None, precision: str = "f32") -> dict:
+    """The constrained-acceleration problem of one forward pass and the oracle's Newton solution:
+    qM [nv, nv], qacc_smooth, qacc, and the rows J [nefc, nv], D, R, aref, floss, type
+    (0 frictionloss, 1 joint limit, 2 contact pyramid edge)."""
+    nv = cmodel.nv
+    maxefc = 2 * 32 + 4 * 32
+    qpos = np.ascontiguousarray(qpos, dtype=np.float32)
+    qvel = np.ascontiguousarray(qvel, dtype=np.float32)
+    ctrl = None if ctrl is None else np.ascontiguousarray(ctrl, dtype=np.float32)
+    qaccw = None if qaccw is None else np.ascontiguousarray(qaccw, dtype=np.float32)
+    qM = np.zeros((nv, nv), np.float32)
+    qs, qa = np.zeros(nv, np.float32), np.zeros(nv, np.float32)
+    J = np.zeros((maxefc, nv), np.float32)
+    D, R, aref, floss = (np.zeros(maxefc, np.float32) for _ in range(4))
+    typ = np.zeros(maxefc, np.int32)
+    ne = lib(precision).zbo_constraint_debug(C.byref(cmodel), C.byref(cfg), _p(qpos), _p(qvel), _p(ctrl), _p(qaccw),
+                                             _p(qM), _p(qs), _p(qa), _p(J), _p(D), _p(R), _p(aref), _p(floss),
+                                             typ.ctypes.data_as(C.POINTER(C.c_int)))
+    return dict(qM=qM, qacc_smooth=qs, qacc=qa, J=J[:ne], D=D[:ne], R=R[:ne], aref=aref[:ne], floss=floss[:ne],
+                type=typ[:ne])
 
 
 def simulate(cmodel, cfg, qpos, qvel, nsteps: int, ctrl=None, qaccw=None, precision: str = "f32"):

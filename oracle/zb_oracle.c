@@ -1511,6 +1511,51 @@ int zbo_forward_debug(const ZbModel* m, const ZbEnvConfig* cfg, const float* qpo
   return 0;
 }
 
+/*
+ * The constrained-acceleration problem of one forward pass, for the solver
+ * optimality tests (tests/test_solver_optimality.py): qacc_smooth, the dense
+ * mass matrix and the constraint rows (J [nefc][nv], D, R, aref, frictionloss,
+ * type: 0 frictionloss, 1 limit, 2 contact edge), plus the Newton solution
+ * qacc. Returns nefc.
+ */
+int zbo_constraint_debug(const ZbModel* m, const ZbEnvConfig* cfg, const float* qpos, const float* qvel,
+                         const float* ctrl, const float* qacc_warm, float* qM, float* qacc_smooth, float* qacc,
+                         float* J, float* D, float* R, float* aref, float* floss, int* type) {
+  ZbData* d = (ZbData*)calloc(1, sizeof(ZbData));
+  EnvCtx c = {m, cfg, 0, 0};
+  load_params(&c, d, NULL);
+  for (int q = 0; q < m->nq; q++) d->qpos[q] = qpos[q];
+  for (int j = 0; j < m->nv; j++) {
+    d->qvel[j] = qvel[j];
+    d->qacc_warm[j] = qacc_warm ? qacc_warm[j] : 0;
+  }
+  for (int a = 0; a < m->nu; a++) d->ctrl[a] = ctrl ? ctrl[a] : 0;
+  forward(m, d, cfg->dt, cfg);
+  const int nv = m->nv, ne = d->nefc;
+  for (int i = 0; i < nv; i++) {
+    qacc_smooth[i] = (float)d->qacc_smooth[i];
+    qacc[i] = (float)d->qacc[i];
+    for (int j = 0; j < nv; j++) qM[i * nv + j] = 0;
+  }
+  for (int i = 0; i < nv; i++) {
+    qM[i * nv + i] = (float)d->qM[i][i];
+    for (int j = m->dof_parent[i]; j >= 0; j = m->dof_parent[j]) {
+      qM[i * nv + j] = (float)d->qM[i][j];
+      qM[j * nv + i] = (float)d->qM[i][j];
+    }
+  }
+  for (int r = 0; r < ne; r++) {
+    for (int j = 0; j < nv; j++) J[r * nv + j] = (float)d->efc_J[r][j];
+    D[r] = (float)d->efc_D[r];
+    R[r] = (float)d->efc_R[r];
+    aref[r] = (float)d->efc_aref[r];
+    floss[r] = (float)d->efc_floss[r];
+    type[r] = d->efc_type[r];
+  }
+  free(d);
+  return ne;
+}
+
 /* advance (qpos, qvel, qacc_warmstart) by n physics steps at fixed ctrl */
 int zbo_simulate(const ZbModel* m, const ZbEnvConfig* cfg, float* qpos, float* qvel, float* qaccw, const float* ctrl,
                  int nsteps) {
