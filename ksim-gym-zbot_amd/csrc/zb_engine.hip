@@ -717,13 +717,18 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const int a = anc_lin(c.chd, e0 + i);
+          if (e0 + i >= 3) {
 #pragma unroll
-          for (int k = 0; k < 6; k++) ca[i][k] = L->cdof[a][k];
+            for (int k = 0; k < 6; k++) ca[i][k] = L->cdof[a][k];
+          }
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const int e = e0 + i;
-          mr[e] = e <= ddep ? dot6(ca[i], F) : 0.f;
+          /* ancestors 0..2 are the free joint's world-frame translations, cdof = (0, e_k):
+             their products are components of F (body 1 carries the free joint, zb_create) */
+          const float v = e < 3 ? F[3 + e] : dot6(ca[i], F);
+          mr[e] = e <= ddep ? v : 0.f;
         }
       }
       st_row(&L->M[j][0], mr);
@@ -929,9 +934,9 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
 __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
   const int ddep = vopq(c.ddep);
   const int j = c.l & 31;
+  /* no mask: entries at or past the depth (the diagonal, zero padding) are never read
+     as off-diagonals by the factorization, and non-dof rows are zero */
   ld_row(&c.L->M[j][0], X);
-#pragma unroll
-  for (int e = 0; e < CAP; e++) X[e] = (e < ddep && c.l < NV) ? X[e] : 0.f;
   return (c.l < NV) ? c.L->M[j][ddep] : 1.f;
 }
 
@@ -1305,8 +1310,10 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
     for (int e = 0; e < CAP; e++) {
       if (e <= r.kdep) {
         int a = anc_lin(r.chd, e);
-        float v = sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
-                  dir[0] * L->cdof[a][3] + dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
+        /* free-joint translations (ancestors 0..2): cdof = (0, e_k), J = dir_k */
+        float v = e < 3 ? dir[e]
+                        : sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
+                              dir[0] * L->cdof[a][3] + dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
         Jc[e] = v;
         vel += v * L->vec[V_QVEL][a];
       }
@@ -1675,9 +1682,8 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   EnvL* L = c.L;
   /* warmstart selection */
   float x = w;
+  if (c.l < 32) L->vec[V_TMP2][c.l] = qs; /* mul_m's barrier publishes it with x in vec[V_TMP] */
   float Ma = mul_m(c, x, V_TMP);
-  if (c.l < 32) { L->vec[V_TMP][c.l] = x; L->vec[V_TMP2][c.l] = qs; }
-  tsync();
   float jw = r.ex ? row_dot(c, r, V_TMP) - r.aref : 0.f;
   float js = r.ex ? row_dot(c, r, V_TMP2) - r.aref : 0.f;
   tsync();
