@@ -233,6 +233,9 @@ def main() -> None:
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
     ap.add_argument("--no-policy", action="store_true", help="skip the policy-in-the-loop leg")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end rollout-pipeline leg")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo rehearses the "
+                         "multi-rank path on a one-GPU box, ranks sharing device local_rank %% device_count)")
     args = ap.parse_args()
 
     import torch  # noqa: PLC0415
@@ -246,16 +249,19 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     conf = CONFIGS[args.config]
     n = args.envs or conf["envs"]
     cm = compile_model()
     cfg = default_config(push=conf["push"], randomize=conf["randomize"])
-    eng = HipEngine(cm, cfg, n, env_offset=rank * n, device=local_rank, seed=args.seed)
+    eng = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
 
     # synthetic actions for the headline env-step leg, generated before timing (the
     # policy-in-the-loop leg below drives the same engine with the GRU actor instead)
@@ -351,7 +357,8 @@ def main() -> None:
                 "global_envs": world * n,
                 "substeps_per_step": cfg.n_substeps,
                 "solver": f"newton, {cfg.iterations} iters / {cfg.ls_iterations} ls iters",
-                "parallelism": f"env-shard x{world} (one process per GPU)",
+                "parallelism": f"env-shard x{world} (one process per GPU)" + (
+                    "" if world == 1 or args.dist_backend == "nccl" else f", {args.dist_backend} rehearsal"),
                 "avg_solver_iters_per_env_step": iters,
             },
             "roofline": {
