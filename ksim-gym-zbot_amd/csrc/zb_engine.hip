@@ -81,7 +81,10 @@ struct __align__(16) EnvL {
   } u;
   union {
     float sub[32][10];      /* subtree sums (smooth phase, sensors) */
-    float Hs[32][CAP + 1];  /* unfactored Newton Hessian rows (+ diagonal) */
+    struct {
+      float Hs[32][CAP]; /* unfactored Newton Hessian rows (16-byte aligned for ld_row) */
+      float Hsd[32];     /* and their diagonals */
+    };
   };
   float vec[NVEC][32];
   float rowDA[32];
@@ -302,9 +305,32 @@ __device__ __forceinline__ void mulmm3(float r[9], const float a[9], const float
 #pragma unroll
     for (int j = 0; j < 3; j++) r[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
 }
+/* sin / cos for |x| <= pi/2 by their Taylor series through x^11 / x^12 (truncation below
+   6e-8, the fp32 epsilon; ~14 VALU instead of sincosf's range reduction); larger arguments
+   (a joint more than pi from its reference) take sincosf */
+__device__ __forceinline__ void sincos_small(float x, float* s, float* c) {
+  if (fabsf(x) <= 1.5707964f) {
+    const float x2 = x * x;
+    float ps = -2.5052108e-8f;                  /* -1/11! */
+    ps = fmaf(ps, x2, 2.7557319e-6f);           /* 1/9! */
+    ps = fmaf(ps, x2, -1.9841270e-4f);          /* -1/7! */
+    ps = fmaf(ps, x2, 8.3333333e-3f);           /* 1/5! */
+    ps = fmaf(ps, x2, -1.6666667e-1f);          /* -1/3! */
+    *s = fmaf(ps * x2, x, x);
+    float pc = 2.0876757e-9f;                   /* 1/12! */
+    pc = fmaf(pc, x2, -2.7557319e-7f);          /* -1/10! */
+    pc = fmaf(pc, x2, 2.4801587e-5f);           /* 1/8! */
+    pc = fmaf(pc, x2, -1.3888889e-3f);          /* -1/6! */
+    pc = fmaf(pc, x2, 4.1666667e-2f);           /* 1/4! */
+    pc = fmaf(pc, x2, -0.5f);
+    *c = fmaf(pc, x2, 1.f);
+  } else {
+    sincosf(x, s, c);
+  }
+}
 __device__ __forceinline__ void axis_angle_quat(float q[4], const float ax[3], float angle) {
   float s, c;
-  sincosf(0.5f * angle, &s, &c);
+  sincos_small(0.5f * angle, &s, &c);
   q[0] = c; q[1] = ax[0] * s; q[2] = ax[1] * s; q[3] = ax[2] * s;
 }
 __device__ __forceinline__ void cross_motion(float r[6], const float v[6], const float u[6]) {
@@ -788,7 +814,7 @@ __device__ __forceinline__ void root_schur_mfma() {
  * registers. On return the L rows are in LDS L[][] (L(k, anc_e(k))), pivots in
  * Dk[] (root: also 1/D in Di[]); returns 1/D_j. */
 template <bool MFMA_SCHUR>
-__device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd) {
+__device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd, const float (*S)[CAP]) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int nroot = NROOT;
@@ -820,9 +846,10 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
   for (int q = NLIMBLV - 1; q >= 1; q--) {
     const bool has = ischain && cps < q && q < c.cln;
     const int src = has ? c.chd + q : c.l;
+    /* only the chain entries travel: the root columns follow from W below */
     float r[NROOT + NLIMBLV], wq[NLIMBLV];
 #pragma unroll
-    for (int e = 0; e < NROOT + q; e++) r[e] = tsh(X[e], src);
+    for (int e = NROOT; e < NROOT + q; e++) r[e] = tsh(X[e], src);
     const float dk = tsh(Xd, src);
 #pragma unroll
     for (int k = q + 1; k < NLIMBLV; k++) wq[k] = tsh(wacc[k], src);
@@ -832,8 +859,6 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
     for (int p = 1; p < q; p++) t = cps == p ? r[NROOT + p] : t;
     const float sc = has ? t / fmaxf(dk, MINVAL) : 0.f;
     Xd -= sc * t;
-#pragma unroll
-    for (int e = 0; e < NROOT; e++) X[e] -= sc * r[e];
     /* entries at chain positions >= the lane's own are never read (a pivot at
        level p only hands out positions < p), so no mask */
 #pragma unroll
@@ -843,6 +868,18 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
     for (int k = q + 1; k < NLIMBLV; k++) wacc[k] -= sc * wq[k];
   }
   if (ischain) {
+    /* root columns of the eliminated chain row: the level updates on them compose to
+       B(p, :) + sum_{k > p} W(p, k) B(k, :), B the chain rows' root entries as passed
+       in (rows S[] in LDS; wacc[k] = -W(p, k) is zero for k <= p and past the chain) */
+    const int chd = c.chd;
+#pragma unroll
+    for (int k = 1; k < NLIMBLV; k++) {
+      float b[NROOT];
+#pragma unroll
+      for (int e = 0; e < NROOT; e++) b[e] = S[chd + k][e];
+#pragma unroll
+      for (int e = 0; e < NROOT; e++) X[e] -= wacc[k] * b[e];
+    }
     const float Dkv = fmaxf(Xd, MINVAL);
     const float inv = 1.0f / Dkv;
 #pragma unroll
@@ -1517,16 +1554,15 @@ __device__ __forceinline__ void jdj_mfma() {
         const float dv = g_lds[t].rowDA[r];
         acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv * jv, jv, acc[t][f], 0, 0, 0);
       }
-  /* lane l holds G[4*(l/16) + v][l%16] */
+  /* lane l holds G[4*(l/16) + v][l%16], v = 0..3: G is symmetric (to rounding), so the
+     four go to row l%16, columns 4*(l/16) + v, as one 16-byte store */
+  static_assert(CAP % 4 == 0, "16-byte G rows");
+  if (k < CAP / 4 && e < CAP)
 #pragma unroll
-  for (int t = 0; t < NTEAM; t++)
+    for (int t = 0; t < NTEAM; t++)
 #pragma unroll
-    for (int f = 0; f < NGEOM; f++)
-#pragma unroll
-      for (int v = 0; v < 4; v++) {
-        const int i = 4 * k + v;
-        if (i < CAP && e < CAP) (&g_lds[t].L[0][0])[f * CAP * CAP + i * CAP + e] = acc[t][f][v];
-      }
+      for (int f = 0; f < NGEOM; f++)
+        *reinterpret_cast<v4f*>(&g_lds[t].L[0][0] + f * CAP * CAP + e * CAP + 4 * k) = acc[t][f];
 }
 
 /* H = M + J' D_active J rows (depth-indexed), then factor -> Dinv */
@@ -1560,7 +1596,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     }
   } else {
     ld_row(&L->Hs[c.l][0], H);
-    Hd = L->Hs[c.l][CAP];
+    Hd = L->Hsd[c.l];
     const float dl = r.ex ? ((r.act ? r.D : 0.f) - (pa ? r.D : 0.f)) : 0.f;
     L->rowF[c.l] = dl; /* rowF is free until the next update_constraint */
     tb = team_ballot(dl != 0.f) & c.rowmask;
@@ -1599,11 +1635,11 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     Hd += dd;
   }
   st_row(&L->Hs[c.l][0], H);
-  L->Hs[c.l][CAP] = Hd;
+  L->Hsd[c.l] = Hd;
   tsync();
   /* the full build runs with the whole wave (matrix-core Schur complement); a
      refactor inside the Newton loop may run for one team only (team reductions) */
-  return full ? factor_ldl<true>(c, H, Hd) : factor_ldl<false>(c, H, Hd);
+  return full ? factor_ldl<true>(c, H, Hd, L->Hs) : factor_ldl<false>(c, H, Hd, L->Hs);
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
@@ -1801,7 +1837,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   /* factor M (copy of rows) */
   float X[CAP];
   float Xd = load_mrow(c, X);
-  float DinvM = factor_ldl<true>(c, X, Xd);
+  float DinvM = factor_ldl<true>(c, X, Xd, L->M);
   STAMP(S_FACM);
   /* velocities */
   if (c.l < 32) L->vec[V_QVEL][c.l] = c.l < NV ? ls.v : 0.f;
@@ -2665,7 +2701,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   {
     float X[CAP];
     float Xd = load_mrow(c, X);
-    float Dinv = factor_ldl<true>(c, X, Xd);
+    float Dinv = factor_ldl<true>(c, X, Xd, L->M);
     if (l < 32) L->vec[V_QVEL][l] = l < NV ? ls.v : 0.f;
     tsync();
     const float qv = l < NV ? ls.v : 0.f;

@@ -2,7 +2,8 @@
 # Per-variant instruction counts of the step kernel (run on the GPU box; diagnostic only):
 #   scripts/pmc_variants.sh evariants/libeng_a.so evariants/libeng_b.so ...
 # One rocprofv3 --pmc pass per library over scripts/variant_driver.py; prints per-launch
-# SQ_INSTS_VALU / SALU / LDS per wave (median over the step launches).
+# SQ_INSTS_VALU / SALU / LDS per wave (median over the step launches). PMC="<counters>" overrides
+# the list (at most 8 SQ counters, one of them SQ_WAVES: values are printed per wave).
 set -e -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -10,7 +11,7 @@ mkdir -p gpurun_out
 for lib in "$@"; do
   name=$(basename "$lib" .so)
   rm -rf "gpurun_out/pmcv_$name"
-  timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 \
+  timeout -k 10 120 rocprofv3 --pmc ${PMC:-SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32} \
     --output-format csv -d "gpurun_out/pmcv_$name" -o run -- python3 scripts/variant_driver.py "$lib" > "gpurun_out/pmcv_$name.log" 2>&1
   python3 - "$name" <<'PY'
 import csv, glob, statistics, sys
