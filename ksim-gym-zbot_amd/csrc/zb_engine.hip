@@ -222,6 +222,22 @@ __device__ __forceinline__ int tmaxi(int v) {
   return rows2max(v);
 }
 __device__ __forceinline__ void tsync() { __syncthreads(); }
+/* a loaded value pinned in place: `t = keepf(load); p ? t : k` stays a load and a select. Without
+   it the compiler sinks the load into a branch of its own, with a full LDS round trip
+   (s_waitcnt lgkmcnt(0)) per element instead of all loads in flight. */
+__device__ __forceinline__ float keepf(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+/* an LDS pointer whose whole address sits in one register: loads at small constant
+   offsets from it pair into ds_read2 (the 8-bit dword offsets of ds_read2_b32 cannot
+   hold a field offset inside EnvL, so the compiler would not pair them otherwise) */
+typedef const __attribute__((address_space(3))) float* LdsF;
+__device__ __forceinline__ LdsF lds_opq(const float* p) {
+  uint32_t v = (uint32_t)(uintptr_t)(LdsF)p;
+  asm volatile("" : "+v"(v));
+  return (LdsF)(uintptr_t)v;
+}
 /* bitmask over the team's lanes of predicate p */
 __device__ __forceinline__ uint32_t team_ballot(bool p) { return (uint32_t)(__ballot(p) >> (threadIdx.x & 32)); }
 /* An opaque copy of a per-lane constant: stops the compiler from hoisting
@@ -630,7 +646,10 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   EnvL* L = c.L;
   const int b = c.l;
   const bool isbody = b >= 1 && b < NB;
-  float mass = isbody ? m->body_mass[b][0] * c.L->par[P_MSCALE][c.l] : 0.f;
+  const int bb = isbody ? b : 0;
+  const float mscale = keepf(c.L->par[P_MSCALE][c.l]);
+  const float bmass = keepf(m->body_mass[bb][0]);
+  float mass = isbody ? bmass * mscale : 0.f;
   float xipos[3], Ri[9];
   {
     float ip[3] = {m->body_ipos[isbody ? b : 0][0], m->body_ipos[isbody ? b : 0][1], m->body_ipos[isbody ? b : 0][2]}, t[3];
@@ -652,11 +671,11 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   /* cinert: inertia about cm in world orientation (mju_inertCom) */
   float ci[10];
   {
-    float in[3] = {0.f, 0.f, 0.f};
-    if (isbody) {
-      in[0] = m->body_inertia[b][0] * c.L->par[P_MSCALE][c.l];
-      in[1] = m->body_inertia[b][1] * c.L->par[P_MSCALE][c.l];
-      in[2] = m->body_inertia[b][2] * c.L->par[P_MSCALE][c.l];
+    float in[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float bi = keepf(m->body_inertia[bb][k]);
+      in[k] = isbody ? bi * mscale : 0.f;
     }
     float dif[3] = {xipos[0] - cm[0], xipos[1] - cm[1], xipos[2] - cm[2]};
     float I[9];
@@ -690,6 +709,14 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
     quat2mat(R, xqs);
 #pragma unroll
     for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], bj);
+    /* the joint's axis and anchor, fetched by every lane (a load under the branch below
+       would wait for each element in turn) */
+    float jax[3], jpos[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      jax[i] = keepf(m->jnt_axis[bj][i]);
+      jpos[i] = keepf(m->jnt_pos[bj][i]);
+    }
     if (j < NV) {
       /* branch-free over the dof kinds (the task's dofs are the free joint's 6 and
          hinges): the motion axis in the body frame is jnt_axis for a hinge and unit
@@ -701,8 +728,8 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
       float ja[3], jp[3], t[3], ax[3];
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        ja[i] = isfree ? (k - 3 == i ? 1.f : 0.f) : m->jnt_axis[bj][i];
-        jp[i] = isfree ? 0.f : m->jnt_pos[bj][i];
+        ja[i] = isfree ? (k - 3 == i ? 1.f : 0.f) : jax[i];
+        jp[i] = isfree ? 0.f : jpos[i];
       }
       mulmv3(t, R, jp);
       mulmv3(ax, R, ja);
@@ -961,7 +988,8 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
       }
     }
     tsync();
-    if (isroot) return L->Di[c.l];
+    const float di = keepf(L->Di[c.l & 31]);
+    if (isroot) return di;
   }
   tsync();
   return 1.0f / fmaxf(Xd, MINVAL);
@@ -974,7 +1002,8 @@ __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
   /* no mask: entries at or past the depth (the diagonal, zero padding) are never read
      as off-diagonals by the factorization, and non-dof rows are zero */
   ld_row(&c.L->M[j][0], X);
-  return (c.l < NV) ? c.L->M[j][ddep] : 1.f;
+  const float d = keepf(c.L->M[j][ddep]);
+  return (c.l < NV) ? d : 1.f;
 }
 
 /* x <- (L'DL)^-1 x, x held by dof lanes (mj_solveM order: L' pass from the
@@ -988,11 +1017,13 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   const int nroot = NROOT;
   const bool ischain = c.chd >= 0;
   const int cps = vopq(c.cps), cln = vopq(c.cln), chd = ischain ? c.chd : 0;
+  /* the lane's stored row: W(p, k) in slots NROOT + k (chain lanes), L(j, root i) in 0..NROOT-1 */
+  float w[CAP];
+  ld_row(&L->L[c.l & 31][0], w);
   /* forward pass along the limbs: the chain's deeper right-hand sides, all in flight */
   {
     /* W(p, k) is zero for k <= p and past the chain, so only non-chain lanes mask it */
-    float w[CAP], bk[NLIMBLV];
-    ld_row(&L->L[c.l & 31][0], w);
+    float bk[NLIMBLV];
 #pragma unroll
     for (int k = 1; k < NLIMBLV; k++) bk[k] = tsh(x, chd + k);
     float z = x;
@@ -1007,7 +1038,7 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   if (nroot > 0) {
     float own[RMAX];
 #pragma unroll
-    for (int i = 0; i < RMAX; i++) own[i] = (ischain && i < nroot) ? L->L[c.l][i] : 0.f;
+    for (int i = 0; i < RMAX; i++) own[i] = (ischain && i < nroot) ? w[i] : 0.f;
     /* xr[k] = x_k - sum_{limb j} L(j, k) x_j: root lane k adds its own value into the
        same team reduction (no separate broadcast of x_k) */
     float sr[RMAX];
@@ -1043,12 +1074,16 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   /* backward pass down the limbs: the shallower chain values and W(a, p), all in flight */
   {
     float va[NLIMBLV - 1], wa[NLIMBLV - 1];
+    const LdsF wcol = lds_opq(&L->L[chd][NROOT + cps]);
+    const int npre = vopq(ischain ? c.cps : 0); /* shallower chain positions */
 #pragma unroll
     for (int a = 0; a < NLIMBLV - 1; a++) {
-      va[a] = tsh(x, chd + a);
-      /* W(a, p) of a shallower chain position; row 31 (zero) otherwise */
-      wa[a] = L->L[(ischain && a < cps) ? chd + a : 31][NROOT + cps];
+      /* W(a, p) of a shallower chain position (consecutive rows: paired loads), masked */
+      /* a multiply, not a select: a select would let the compiler sink the load into a branch */
+      wa[a] = wcol[a * CAP] * (a < npre ? 1.f : 0.f);
     }
+#pragma unroll
+    for (int a = 0; a < NLIMBLV - 1; a++) va[a] = tsh(x, chd + a);
     float y = x;
 #pragma unroll
     for (int a = 0; a < NLIMBLV - 1; a++) y += wa[a] * va[a];
@@ -1078,11 +1113,15 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
     /* limb lanes: transposed part M(k, j) x_k over the deeper dofs of the
        chain (consecutive dofs chd+cps+1 .. chd+cln-1), all loads in flight */
     float a[NLIMBLV - 1];
+    const int kb = ischain ? c.chd + c.cps : 0;
+    /* deeper dofs of the chain, opaque so that the five masks are compares here rather
+       than SGPR pairs hoisted out of the substep loop */
+    const int nd = vopq(ischain ? c.cln - c.cps - 1 : 0);
 #pragma unroll
     for (int q = 1; q < NLIMBLV; q++) {
-      /* past the chain: row 31, a zero row of a non-dof lane */
-      const int k = (ischain && c.cps + q < c.cln) ? c.chd + c.cps + q : 31;
-      a[q - 1] = L->M[k][ddep] * L->vec[slot][k];
+      /* consecutive rows (paired loads), masked past the chain */
+      const float mk = L->M[kb + q][ddep], vk = L->vec[slot][kb + q];
+      a[q - 1] = q <= nd ? mk * vk : 0.f;
     }
 #pragma unroll
     for (int q = 1; q < NLIMBLV; q++) y += a[q - 1];
@@ -1097,13 +1136,14 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
     float sr = 0.f;
 #pragma unroll
     for (int i = 0; i < RMAX; i++) sr = j == i ? si[i] : sr;
-    /* deeper root dofs: all loads in flight, masked */
+    /* deeper root dofs: fixed rows (paired loads), masked */
     const int jr = j < nroot ? j : 0;
+    const int jo = vopq(j); /* as nd above */
     float yr = 0.f;
 #pragma unroll
     for (int k = 1; k < RMAX; k++) {
-      const int kk = (k < nroot && k > j) ? k : 31; /* row 31 is zero */
-      yr += L->M[kk][jr] * L->vec[slot][kk];
+      const float mk = L->M[k][jr], vk = L->vec[slot][k];
+      yr += (k < nroot && k > jo) ? mk * vk : 0.f;
     }
     if (j < nroot) y += yr + sr;
   }
@@ -1157,7 +1197,10 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B, float qv, float 
   const bool isd = j < NV;
   float cd[6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) cd[k] = isd ? L->cdof[j][k] : 0.f;
+  for (int k = 0; k < 6; k++) {
+    const float t = keepf(L->cdof[j][k]);
+    cd[k] = isd ? t : 0.f;
+  }
   float P[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) P[k] = isd ? cd[k] * qv : 0.f;
@@ -1198,7 +1241,10 @@ __device__ __forceinline__ void com_acc(const Ctx& c, const float cdd[6], float 
   for (int k = 0; k < 6; k++) P[k] = isd ? cdd[k] * qv : 0.f;
   if (with_acc) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) P[k] += isd ? L->cdof[j][k] * qa : 0.f;
+    for (int k = 0; k < 6; k++) {
+      const float t = keepf(L->cdof[j][k]);
+      P[k] += isd ? t * qa : 0.f;
+    }
   }
   dof_prefix6(c, P);
   const float g[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
@@ -1345,15 +1391,16 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
     float vel = 0.f;
 #pragma unroll
     for (int e = 0; e < CAP; e++) {
-      if (e <= r.kdep) {
-        int a = anc_lin(r.chd, e);
-        /* free-joint translations (ancestors 0..2): cdof = (0, e_k), J = dir_k */
-        float v = e < 3 ? dir[e]
-                        : sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
-                              dir[0] * L->cdof[a][3] + dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
-        Jc[e] = v;
-        vel += v * L->vec[V_QVEL][a];
-      }
+      /* every entry computed (anc_lin past the depth is a valid dummy dof), kept up to the
+         row's depth: all loads in flight */
+      const int a = anc_lin(r.chd, e);
+      /* free-joint translations (ancestors 0..2): cdof = (0, e_k), J = dir_k */
+      float v = e < 3 ? dir[e]
+                      : sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] +
+                            dir[0] * L->cdof[a][3] + dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
+      v = e <= r.kdep ? v : 0.f;
+      Jc[e] = v;
+      vel += v * keepf(L->vec[V_QVEL][a]);
     }
     float dA = m->body_invweight0[gb][0] * (1.f + mu * mu);
     float Rr;
@@ -1615,7 +1662,8 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
       ld_row(&L->u.J[k1][0], j1);
       const float jd0 = L->u.J[k0][ddep], jd1 = L->u.J[k1][ddep];
       const float jj0 = da[k0] * jd0;
-      const float jj1 = h1 ? da[k1] * jd1 : 0.f;
+      const float da1 = keepf(da[k1]);
+      const float jj1 = h1 ? da1 * jd1 : 0.f;
       Hd += jj0 * jd0;
       Hd += jj1 * jd1;
 #pragma unroll
@@ -1857,7 +1905,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   } else {
     ls.actforce = 0.f;
   }
-  float fs = (c.l < NV) ? (-c.L->par[P_DAMP][c.l] * ls.v - bias + act) : 0.f;
+  const float damp = keepf(c.L->par[P_DAMP][c.l & 31]);
+  float fs = (c.l < NV) ? (-damp * ls.v - bias + act) : 0.f;
   STAMP(S_RNE);
   float qs = solve_ldl(c, fs, DinvM);
   STAMP(S_SOLVES);
@@ -2455,7 +2504,8 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   uint32_t desc = 0;
   for (int k = 0; k < NV; k++) {
     int dk = m->dof_depth[k];
-    if (isd && k != l && dk > c.ddep && m->dof_anc[k][c.ddep] == l) desc |= 1u << k;
+    const int anc = vopq(m->dof_anc[k][c.ddep]);
+    if (isd && k != l && dk > c.ddep && anc == l) desc |= 1u << k;
   }
   uint32_t rm = 0;
   for (int g = 0; g < NGEOM; g++) {
