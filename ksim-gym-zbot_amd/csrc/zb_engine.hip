@@ -205,6 +205,30 @@ __device__ __forceinline__ void reduce21_to(const float v[21], float* out) {
   const int idx = ((threadIdx.x & 16) ? 11 : 0) + li;
   if (li < 11 && idx < 21) out[idx] = sum;
 }
+/* six team sums, lane i (< 6) receiving sum i: a transposing butterfly (plain pair add
+ * with the row mirror, then three stages that each keep the half of the slots selected by
+ * one lane bit: slot = lane & 7), then the two 16-lane rows added. 29 VALU instructions
+ * instead of tsum_n<6>'s 42. */
+__device__ __forceinline__ float reduce6_lane(const float v[6]) {
+  const int li = threadIdx.x & 15;
+  float q[8];
+#pragma unroll
+  for (int k = 0; k < 6; k++) q[k] = v[k] + dppf<0x140>(v[k]);
+  q[6] = q[7] = 0.f;
+  const bool s2 = (li & 4) != 0;
+  float u4[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) u4[k] = (s2 ? q[4 + k] : q[k]) + dppf<0x141>(s2 ? q[k] : q[4 + k]);
+  const bool s1 = (li & 2) != 0;
+  float u2[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) u2[k] = (s1 ? u4[2 + k] : u4[k]) + dppf<0x4E>(s1 ? u4[k] : u4[2 + k]);
+  const bool s0 = (li & 1) != 0;
+  const float r = (s0 ? u2[1] : u2[0]) + dppf<0xB1>(s0 ? u2[0] : u2[1]);
+  float a, b;
+  rows2(r, a, b);
+  return a + b;
+}
 __device__ __forceinline__ float tmaxf(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
@@ -1129,13 +1153,11 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   if (nroot > 0) {
     /* root lanes: limb dofs by one team reduction per root dof (their
        M(k, root i) = mrow[i]), deeper root dofs from LDS */
+    static_assert(RMAX == 6, "reduce6_lane");
     float si[RMAX];
 #pragma unroll
     for (int i = 0; i < RMAX; i++) si[i] = (ischain && i < nroot) ? mrow[i] * x : 0.f;
-    tsum_n<RMAX>(si);
-    float sr = 0.f;
-#pragma unroll
-    for (int i = 0; i < RMAX; i++) sr = j == i ? si[i] : sr;
+    const float sr = reduce6_lane(si); /* root lane j: sum j */
     /* deeper root dofs: fixed rows (paired loads), masked */
     const int jr = j < nroot ? j : 0;
     const int jo = vopq(j); /* as nd above */
@@ -1696,7 +1718,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
-  r.Jv = r.ex ? row_dot(c, r, V_TMP) : 0.f;
+  r.Jv = row_dot(c, r, V_TMP); /* J rows are zero where no contact: no branch around the loads */
   tsync();
   /* the quadratic's coefficients and the slope/curvature at alpha = 0 in one reduction:
      d1(0) = search . grad (the gradient update_constraint left for the current active
@@ -1768,8 +1790,9 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float x = w;
   if (c.l < 32) L->vec[V_TMP2][c.l] = qs; /* mul_m's barrier publishes it with x in vec[V_TMP] */
   float Ma = mul_m(c, x, V_TMP);
-  float jw = r.ex ? row_dot(c, r, V_TMP) - r.aref : 0.f;
-  float js = r.ex ? row_dot(c, r, V_TMP2) - r.aref : 0.f;
+  const float rw = keepf(row_dot(c, r, V_TMP)), rs = keepf(row_dot(c, r, V_TMP2));
+  float jw = r.ex ? rw - r.aref : 0.f;
+  float js = r.ex ? rs - r.aref : 0.f;
   tsync();
   float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, r.sl * x - r.al),
                   rows_cost(c, r, js, qs - r.af, r.sl * qs - r.al)};
