@@ -814,6 +814,30 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
     } /* non-dof lanes keep the zero rows make_ctx stored, so M x needs no lane mask */
   }
   tsync();
+  /* The transposed entries in the row padding: slot ddep + q of row j holds M(j + q, j) for
+   * the q-th deeper dof of j's chain (the root chain for a root dof), zero past it. The
+   * ancestor gather of mul_m reads slot e > ddep at dof anc_lin(chd, e) = j + (e - ddep), so
+   * one 12-entry row product gives M(j, anc) x_anc + M(j, j) x_j + sum_q M(j + q, j) x_{j+q}.
+   * Nothing else reads past the diagonal (the factorizations take off-diagonals below it). */
+  {
+    const int j = c.l;
+    const bool isd = j < NV;
+    const int nd = vopq(isd ? (j < NROOT ? NROOT - 1 - j : c.cln - c.cps - 1) : 0);
+    const int jb = isd ? j : 0;
+    float t[NLIMBLV - 1];
+#pragma unroll
+    for (int q = 1; q < NLIMBLV; q++) {
+      const float v = L->M[jb + q][ddep];
+      t[q - 1] = q <= nd ? v : 0.f;
+    }
+#pragma unroll
+    for (int q = 1; q < NLIMBLV; q++) {
+      /* past the chain the (zero) value goes to row 31, which stays the zero row */
+      float* dst = q <= nd ? &L->M[j][ddep + q] : &L->M[31][0];
+      *dst = t[q - 1];
+    }
+  }
+  tsync();
 }
 
 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -1023,7 +1047,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
 __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
   const int ddep = vopq(c.ddep);
   const int j = c.l & 31;
-  /* no mask: entries at or past the depth (the diagonal, zero padding) are never read
+  /* no mask: entries at or past the depth (the diagonal, the transposed entries) are never read
      as off-diagonals by the factorization, and non-dof rows are zero */
   ld_row(&c.L->M[j][0], X);
   const float d = keepf(c.L->M[j][ddep]);
@@ -1118,56 +1142,30 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
 
 /* y = M x (M rows in LDS), x in dof lanes; uses vec[slot] */
 __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
-  const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   const int j = c.l;
   const bool ischain = c.chd >= 0;
   const int nroot = NROOT;
   if (j < 32) L->vec[slot][j] = x;
   tsync();
-  /* lower part M(j, anc) x_anc: one row load + all ancestor values in flight */
+  /* M(j, anc) x_anc, the diagonal and the deeper dofs of j's chain (their entries sit in
+     the row padding, com_crb_m): one row load + all ancestor values in flight */
   float mrow[CAP], vv[CAP];
   ld_row(&L->M[j & 31][0], mrow);
 #pragma unroll
   for (int e = 0; e < CAP; e++) vv[e] = L->vec[slot][anc_lin(c.chd, e)];
   float y = 0.f;
 #pragma unroll
-  for (int e = 0; e < CAP; e++) y += mrow[e] * vv[e]; /* rows are zero past the depth */
-  if (j < NV) {
-    /* limb lanes: transposed part M(k, j) x_k over the deeper dofs of the
-       chain (consecutive dofs chd+cps+1 .. chd+cln-1), all loads in flight */
-    float a[NLIMBLV - 1];
-    const int kb = ischain ? c.chd + c.cps : 0;
-    /* deeper dofs of the chain, opaque so that the five masks are compares here rather
-       than SGPR pairs hoisted out of the substep loop */
-    const int nd = vopq(ischain ? c.cln - c.cps - 1 : 0);
-#pragma unroll
-    for (int q = 1; q < NLIMBLV; q++) {
-      /* consecutive rows (paired loads), masked past the chain */
-      const float mk = L->M[kb + q][ddep], vk = L->vec[slot][kb + q];
-      a[q - 1] = q <= nd ? mk * vk : 0.f;
-    }
-#pragma unroll
-    for (int q = 1; q < NLIMBLV; q++) y += a[q - 1];
-  }
+  for (int e = 0; e < CAP; e++) y += mrow[e] * vv[e]; /* zero past the chain */
   if (nroot > 0) {
-    /* root lanes: limb dofs by one team reduction per root dof (their
-       M(k, root i) = mrow[i]), deeper root dofs from LDS */
+    /* root lanes: the limb dofs' M(k, root i) = mrow[i], one transposing reduction
+       (the deeper root dofs come with the row product, from the row padding) */
     static_assert(RMAX == 6, "reduce6_lane");
     float si[RMAX];
 #pragma unroll
     for (int i = 0; i < RMAX; i++) si[i] = (ischain && i < nroot) ? mrow[i] * x : 0.f;
     const float sr = reduce6_lane(si); /* root lane j: sum j */
-    /* deeper root dofs: fixed rows (paired loads), masked */
-    const int jr = j < nroot ? j : 0;
-    const int jo = vopq(j); /* as nd above */
-    float yr = 0.f;
-#pragma unroll
-    for (int k = 1; k < RMAX; k++) {
-      const float mk = L->M[k][jr], vk = L->vec[slot][k];
-      yr += (k < nroot && k > jo) ? mk * vk : 0.f;
-    }
-    if (j < nroot) y += yr + sr;
+    if (j < nroot) y += sr;
   }
   tsync();
   return y;

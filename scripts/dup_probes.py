@@ -31,12 +31,12 @@ PROBES = {
                f"    {{ {B} Rows r2 = r; float g2_; float d_ = update_constraint_lane(c, r2, opqf(x), qs, fs, Ma, g2_); SINK(d_); SINK(g2_); }}\n"),
     "solve_nw": ("    const float mg = solve_ldl(c, grad, Dinv);",
                  f"    {{ {B} float d_ = solve_ldl(c, opqf(grad), Dinv); SINK(d_); }}\n"),
-    "factor_h": ("  return full ? factor_ldl<true>(c, H, Hd) : factor_ldl<false>(c, H, Hd);",
+    "factor_h": ("  return full ? factor_ldl<true>(c, H, Hd, L->Hs) : factor_ldl<false>(c, H, Hd, L->Hs);",
                  f"  {{ {B} float H2[CAP]; for (int e = 0; e < CAP; e++) H2[e] = opqf(H[e]);\n"
-                 "    float d_ = full ? factor_ldl<true>(c, H2, opqf(Hd)) : factor_ldl<false>(c, H2, opqf(Hd)); SINK(d_); }\n"),
-    "factor_m": ("  float DinvM = factor_ldl<true>(c, X, Xd);",
+                 "    float d_ = full ? factor_ldl<true>(c, H2, opqf(Hd), L->Hs) : factor_ldl<false>(c, H2, opqf(Hd), L->Hs); SINK(d_); }\n"),
+    "factor_m": ("  float DinvM = factor_ldl<true>(c, X, Xd, L->M);",
                  f"  {{ {B} float X2[CAP]; for (int e = 0; e < CAP; e++) X2[e] = opqf(X[e]);\n"
-                 "    float d_ = factor_ldl<true>(c, X2, opqf(Xd)); SINK(d_); }\n"),
+                 "    float d_ = factor_ldl<true>(c, X2, opqf(Xd), L->M); SINK(d_); }\n"),
     "kin": ("  kinematics(c, s, ls, B);",
             f"  {{ {B} LaneS l2 = ls; l2.q = opqf(ls.q); BodyK B2; kinematics(c, s, l2, B2); SINK(B2.xp[0]); SINK(B2.xq[0]); }}\n"),
     "crb": ("  com_crb_m(c, s, ls, B, cm);",
