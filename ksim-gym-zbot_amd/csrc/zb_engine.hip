@@ -1084,14 +1084,13 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
 #pragma unroll
   for (int k = 0; k < RMAX; k++) xr[k] = 0.f;
   if (nroot > 0) {
-    float own[RMAX];
-#pragma unroll
-    for (int i = 0; i < RMAX; i++) own[i] = (ischain && i < nroot) ? w[i] : 0.f;
     /* xr[k] = x_k - sum_{limb j} L(j, k) x_j: root lane k adds its own value into the
-       same team reduction (no separate broadcast of x_k) */
+       same team reduction (no separate broadcast of x_k); w[] of a root or non-dof lane
+       meets a zero (xs), and non-dof rows are zero */
+    const float xs = ischain ? x : 0.f;
     float sr[RMAX];
 #pragma unroll
-    for (int k = 0; k < RMAX; k++) sr[k] = c.l == k ? x : -own[k] * (ischain ? x : 0.f);
+    for (int k = 0; k < RMAX; k++) sr[k] = c.l == k ? x : -w[k] * xs;
     tsum_n<RMAX>(sr);
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
@@ -1110,9 +1109,10 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
 #pragma unroll
         for (int a = 0; a < k; a++) xr[k] -= L->L[k][a] * xr[a];
     x *= Dinv;
+    /* limb lanes; a root lane's x is replaced below, a non-dof row is zero */
 #pragma unroll
     for (int e = 0; e < RMAX; e++)
-      if (e < nroot) x -= own[e] * xr[e];
+      if (e < nroot) x -= w[e] * xr[e];
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
       if (c.l == k && k < nroot) x = xr[k];
@@ -1731,31 +1731,32 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   const float c1 = cc[0], c2 = cc[1];
   /* per-row constants of the piecewise quadratic along the search direction (the
      two joint-limit rows of a dof are folded into one: at most one side exists) */
-  const float DJ = r.D * r.Jv, DJ2 = DJ * r.Jv;
-  const float Rf = r.Rf * r.fl, FJ = r.fl * jv0, DfJ = r.Df * jv0, DfJ2 = DfJ * jv0;
-  const bool hl = r.hl;
+  /* row existence folded into the constants (zero for a row that does not exist) */
+  const float DJ = r.ex ? r.D * r.Jv : 0.f, DJ2 = DJ * r.Jv;
+  const float Rf = r.Rf * r.fl, DfJ = r.hf ? r.Df * jv0 : 0.f, DfJ2 = DfJ * jv0;
   const float sv = r.sl * jv0, jl0 = r.jl;
-  const float DlJ = r.Dl * sv, DlJ2 = DlJ * sv;
+  const float DlJ = r.hl ? r.Dl * sv : 0.f, DlJ2 = DlJ * sv;
   auto eval = [&](float alpha, float& d1, float& d2) {
     /* branch-free; rows that do not exist or are inactive add exact zeros */
     float g1, g2;
     {
+      /* contact: active below zero */
       const float x = r.jar + alpha * r.Jv;
-      const bool on = r.ex && x < 0.f;
-      g1 = on ? DJ * x : 0.f;
-      g2 = on ? DJ2 : 0.f;
+      g1 = DJ * fminf(x, 0.f);
+      g2 = x < 0.f ? DJ2 : 0.f;
     }
     {
+      /* frictionloss: linear zone |x| < R fl, saturated at -+fl outside (the force
+         D x clamped to the saturation: D x = fl at x = R fl) */
       const float x = r.jf + alpha * jv0;
-      const bool lo = x <= -Rf, hi = x >= Rf;
-      g1 += r.hf ? (lo ? -FJ : (hi ? FJ : DfJ * x)) : 0.f;
-      g2 += (r.hf && !lo && !hi) ? DfJ2 : 0.f;
+      g1 += DfJ * __builtin_amdgcn_fmed3f(x, -Rf, Rf);
+      g2 += fabsf(x) < Rf ? DfJ2 : 0.f;
     }
     {
+      /* joint limit: active below zero */
       const float x = jl0 + alpha * sv;
-      const bool on = hl && x < 0.f;
-      g1 += on ? DlJ * x : 0.f;
-      g2 += on ? DlJ2 : 0.f;
+      g1 += DlJ * fminf(x, 0.f);
+      g2 += x < 0.f ? DlJ2 : 0.f;
     }
     float gg[2] = {g1, g2};
     tsum_n<2>(gg);
