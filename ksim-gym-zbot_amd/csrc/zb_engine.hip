@@ -229,6 +229,61 @@ __device__ __forceinline__ float reduce6_lane(const float v[6]) {
   rows2(r, a, b);
   return a + b;
 }
+/* K team sums written to out[0..K-1] in LDS by a transposing butterfly (the K <= 16
+ * generalisation of reduce21_to): the two 16-lane rows exchange halves (value i stays in
+ * row 0, value H + i goes to row 1), then the four DPP pairings inside a row either add
+ * (while there are fewer slots than lanes to spread them over) or keep the half of the
+ * slots selected by one lane bit, so that lane 16r + s ends with value rH + s. The caller
+ * syncs before reading out[]. */
+template <int K>
+__device__ __forceinline__ void reduce_to_lds(const float v[K], float* out) {
+  constexpr int H = (K + 1) / 2;
+  constexpr int S = H <= 2 ? 2 : (H <= 4 ? 4 : (H <= 8 ? 8 : 16));
+  static_assert(K <= 32 && H <= 16, "two rows of 16 slots");
+  float w[16];
+#pragma unroll
+  for (int i = 0; i < H; i++) {
+    const float hi = i + H < K ? v[i + H] : 0.f;
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(hi), false, false);
+    w[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = H; i < 16; i++) w[i] = 0.f;
+  const int li = threadIdx.x & 15;
+  /* stage 1: row mirror (lane ^ 15); selects on bit 3 when there are 16 slots */
+  if constexpr (S == 16) {
+    const bool s3 = li >= 8;
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = (s3 ? w[8 + k] : w[k]) + dppf<0x140>(s3 ? w[k] : w[8 + k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < H; k++) w[k] += dppf<0x140>(w[k]);
+  }
+  /* stage 2: half-row mirror (lane ^ 7); bit 2 when there are 8 or more slots */
+  if constexpr (S >= 8) {
+    const bool s2 = (li & 4) != 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = (s2 ? w[4 + k] : w[k]) + dppf<0x141>(s2 ? w[k] : w[4 + k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < (H < 4 ? H : 4); k++) w[k] += dppf<0x141>(w[k]);
+  }
+  /* stage 3: lane ^ 2, bit 1 (S >= 4) */
+  if constexpr (S >= 4) {
+    const bool s1 = (li & 2) != 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) w[k] = (s1 ? w[2 + k] : w[k]) + dppf<0x4E>(s1 ? w[k] : w[2 + k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 2; k++) w[k] += dppf<0x4E>(w[k]);
+  }
+  /* stage 4: lane ^ 1, bit 0 */
+  const bool s0 = (li & 1) != 0;
+  const float sum = (s0 ? w[1] : w[0]) + dppf<0xB1>(s0 ? w[0] : w[1]);
+  const int slot = li & (S - 1);
+  const int idx = ((threadIdx.x & 16) ? H : 0) + slot;
+  if (li < S && slot < H && idx < K) out[idx] = sum;
+}
 __device__ __forceinline__ float tmaxf(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
@@ -644,21 +699,19 @@ __device__ __forceinline__ void subtree_sum(const Ctx& c, float v[K]) {
       live = nl;
     }
   }
-  /* the base (the one branching body) adds its children's chain sums: one
-     batched team reduction instead of a gather loop */
-  {
-    const bool bchild = c.l >= 2 && c.l < NB && c.bpar == 1;
-    float w[K];
-#pragma unroll
-    for (int i = 0; i < K; i++) w[i] = bchild ? v[i] : 0.f;
-    tsum_n<K>(w);
-    if (c.l == 1) {
-#pragma unroll
-      for (int i = 0; i < K; i++) v[i] += w[i];
-    }
-  }
 #pragma unroll
   for (int i = 0; i < K; i++) L->sub[c.l][i] = v[i];
+  /* the base (the one branching body): its own value plus its children's chain sums,
+     one transposing team reduction straight into its row sub[1] (written after the
+     plain stores above, in program order). Callers read the sums from sub[]. */
+  {
+    const bool bchild = c.l >= 2 && c.l < NB && c.bpar == 1;
+    const bool take = bchild || c.l == 1;
+    float w[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) w[i] = take ? v[i] : 0.f;
+    reduce_to_lds<K>(w, &L->sub[1][0]);
+  }
   tsync();
 }
 
