@@ -730,9 +730,7 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
   float xipos[3], Ri[9];
   {
     float ip[3] = {m->body_ipos[isbody ? b : 0][0], m->body_ipos[isbody ? b : 0][1], m->body_ipos[isbody ? b : 0][2]}, t[3];
-    float BR[9];
-    quat2mat(BR, B.xq);
-    mulmv3(t, BR, ip);
+    quat_rotate(t, B.xq, ip); /* xmat * ipos */
 #pragma unroll
     for (int k = 0; k < 3; k++) xipos[k] = B.xp[k] + t[k];
     float iq[4] = {m->body_iquat[isbody ? b : 0][0], m->body_iquat[isbody ? b : 0][1],
@@ -919,8 +917,8 @@ __device__ __forceinline__ void root_schur_mfma() {
       const int k = NROOT + 4 * ch + kk;
       const float lv = g_lds[t].L[k][ic];
       const float dv = g_lds[t].Dk[k];
-      const float a = i < RMAX ? dv * lv : 0.f, b = i < RMAX ? lv : 0.f;
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+      /* no masks: lanes i >= RMAX feed rows / columns of G that are never stored */
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv * lv, lv, acc[t], 0, 0, 0);
     }
 #pragma unroll
   for (int t = 0; t < NTEAM; t++)
@@ -960,6 +958,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
      the pivot row afterwards) and applies its Schur update. Position 0 has no
      receivers inside the chain. */
   const int cps = vopq(c.cps);
+  const int chdv = ischain ? c.chd : 0;
   /* Alongside, each chain lane p builds row p of W = (I + Lt)^-1, the inverse of
      its chain's unit triangular block (Lt(p, k) = L(k, p), k deeper in the chain),
      by absolute chain position: W(p, k) = -sum_{m > p} L(m, p) W(m, k), W(m, m) = 1.
@@ -973,7 +972,9 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
 #pragma unroll
   for (int q = NLIMBLV - 1; q >= 1; q--) {
     const bool has = ischain && cps < q && q < c.cln;
-    const int src = has ? c.chd + q : c.l;
+    /* lanes without a pivot at this level pull from any lane of a valid index and
+       discard it (sc = 0 below; every pulled value is finite) */
+    const int src = chdv + q;
     /* only the chain entries travel: the root columns follow from W below */
     float r[NROOT + NLIMBLV], wq[NLIMBLV];
 #pragma unroll
@@ -1702,17 +1703,22 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     jdj_mfma();
     tsync();
     if (c.l < NV) {
+      /* the G row of each foot whose chain holds the dof, else the zero row 31 of L
+         (G occupies rows 0..23): no per-entry selects */
       const float* G = &L->L[0][0] + ddep * CAP;
       const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
+      static_assert(NGEOM * CAP * CAP <= 31 * CAP, "G staged below the zero row 31");
+      const float* G0 = f0 ? G : &L->L[31][0];
+      const float* G1 = f1 ? G + CAP * CAP : &L->L[31][0];
       float g0[CAP], g1[CAP];
-      ld_row(G, g0);
-      ld_row(G + CAP * CAP, g1);
-      const float d0 = G[ddep], d1 = G[CAP * CAP + ddep];
+      ld_row(G0, g0);
+      ld_row(G1, g1);
+      const float d0 = G0[f0 ? ddep : 0], d1 = G1[f1 ? ddep : 0];
 #pragma unroll
       /* entries at or past the lane's depth are never read by the factorization,
          so they need no mask */
-      for (int e = 0; e < CAP; e++) H[e] += (f0 ? g0[e] : 0.f) + (f1 ? g1[e] : 0.f);
-      Hd += (f0 ? d0 : 0.f) + (f1 ? d1 : 0.f);
+      for (int e = 0; e < CAP; e++) H[e] += g0[e] + g1[e];
+      Hd += d0 + d1;
     }
   } else {
     ld_row(&L->Hs[c.l][0], H);
