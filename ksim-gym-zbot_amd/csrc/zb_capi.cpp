@@ -28,6 +28,7 @@ struct ZbHandle {
   ZbEnvConfig cfg;
   ZbModel* dmodel;
   ZbEnvConfig* dcfg;
+  int32_t* dtopo; /* [TP_NF][32] per-lane topology */
   float* state;
   float* rnd;
   float* stats;
@@ -174,6 +175,79 @@ static int check_cfg(const ZbEnvConfig* c) {
   return ZB_OK;
 }
 
+/* The per-lane roles of a 32-lane team (body lane, dof lane, limb-chain position, contact
+   rows holding the dof, actuator), computed once here instead of by every wave at the top
+   of every launch. Field-major [TP_NF][32]; the checks of check_model hold. */
+static void build_topology(const ZbModel* m, int32_t t[zb::TP_NF][zb::TOPO_LANES]) {
+  using namespace zb;
+  const int NB = ZB_NBODY_TASK, NV = 6 + ZB_NJ;
+  memset(t, 0, sizeof(int32_t) * TP_NF * TOPO_LANES);
+  int nch_of[TOPO_LANES], bdep_of[TOPO_LANES];
+  for (int l = 0; l < TOPO_LANES; l++) {
+    const bool isb = l < NB;
+    t[TP_BPAR][l] = isb ? m->body_parent[l] : 0;
+    t[TP_BDEP][l] = bdep_of[l] = isb ? m->body_depth[l] : 1000;
+    t[TP_BJT][l] = isb ? m->body_jnttype[l] : ZB_JNT_NONE;
+    t[TP_BDOFADR][l] = isb ? m->body_dofadr[l] : -1;
+    t[TP_BLAST][l] = isb ? m->body_lastdof[l] : -1;
+    int nch = 0;
+    uint32_t ch0 = 0, ch1 = 0;
+    for (int b = 1; b < NB; b++)
+      if (isb && m->body_parent[b] == l && nch < 8) {
+        if (nch < 4) ch0 |= (uint32_t)b << (8 * nch);
+        else ch1 |= (uint32_t)b << (8 * (nch - 4));
+        nch++;
+      }
+    t[TP_NCH][l] = nch_of[l] = nch;
+    t[TP_CH0][l] = (int32_t)ch0;
+    t[TP_CH1][l] = (int32_t)ch1;
+  }
+  /* per body depth: the largest child count among the bodies at that depth (4 bits each) */
+  uint64_t lv = 0;
+  for (int d = 0; d <= TOPO_MAXBD && d < 16; d++) {
+    int mx = 0;
+    for (int l = 0; l < TOPO_LANES; l++)
+      if (bdep_of[l] == d && nch_of[l] > mx) mx = nch_of[l];
+    lv |= (uint64_t)(mx & 0xf) << (4 * d);
+  }
+  for (int l = 0; l < TOPO_LANES; l++) {
+    t[TP_LVL_LO][l] = (int32_t)(uint32_t)lv;
+    t[TP_LVL_HI][l] = (int32_t)(uint32_t)(lv >> 32);
+    const bool isd = l < NV;
+    const int ddep = isd ? m->dof_depth[l] : 0;
+    const int dbody = isd ? m->dof_body[l] : 0;
+    t[TP_DDEP][l] = ddep;
+    t[TP_DBODY][l] = dbody;
+    t[TP_QADR][l] = isd ? m->dof_qposadr[l] : -1;
+    int act = -1;
+    for (int a = 0; a < m->nu; a++)
+      if (isd && m->act_dof[a] == l) act = a;
+    t[TP_ACT][l] = act;
+    uint32_t desc = 0;
+    for (int k = 0; k < NV; k++)
+      if (isd && k != l && m->dof_depth[k] > ddep && m->dof_anc[k][ddep] == l) desc |= 1u << k;
+    uint32_t rm = 0;
+    for (int g = 0; g < TOPO_NGEOM; g++) {
+      const int kd = m->body_lastdof[m->geom_body[g]];
+      if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm |= 0xFFFFu << (16 * g);
+    }
+    t[TP_ROWMASK][l] = (int32_t)rm;
+    t[TP_DK0][l] = isd ? l - m->body_dofadr[dbody] : 0;
+    t[TP_DFREE][l] = (isd && m->body_jnttype[dbody] == ZB_JNT_FREE) ? 1 : 0;
+    int hd = -1, ln = 0;
+    if (isd && l >= TOPO_NROOT) {
+      hd = l;
+      while (m->dof_parent[hd] >= TOPO_NROOT) hd = m->dof_parent[hd];
+      int k = hd;
+      while (k + 1 < NV && m->dof_parent[k + 1] == k) k++;
+      ln = k - hd + 1;
+    }
+    t[TP_CHD][l] = hd;
+    t[TP_CPS][l] = hd >= 0 ? l - hd : 0;
+    t[TP_CLN][l] = ln;
+  }
+}
+
 int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_offset, int device, uint64_t seed,
               ZbHandle** out) {
   if (!model || !cfg || !out || n_envs < 0 || env_offset < 0) return fail(ZB_EARG, "zb_create: bad argument");
@@ -202,6 +276,12 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMalloc(&h->stats, n * ZB_NUM_STATS * sizeof(float));
   if (e == hipSuccess) e = hipMalloc(&h->iters, n * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemcpy(h->dmodel, model, sizeof(ZbModel), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    int32_t topo[zb::TP_NF][zb::TOPO_LANES];
+    build_topology(model, topo);
+    e = hipMalloc(&h->dtopo, sizeof topo);
+    if (e == hipSuccess) e = hipMemcpy(h->dtopo, topo, sizeof topo, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMemset(h->state, 0, n * ZB_STATE_STRIDE * sizeof(float));
   if (e == hipSuccess) e = hipMemset(h->rnd, 0, n * ZB_RAND_STRIDE * sizeof(float));
   if (e == hipSuccess) e = hipMemset(h->stats, 0, n * ZB_NUM_STATS * sizeof(float));
@@ -223,6 +303,7 @@ int zb_destroy(ZbHandle* h) {
   (void)hipSetDevice(h->device);
   if (h->dmodel) (void)hipFree(h->dmodel);
   if (h->dcfg) (void)hipFree(h->dcfg);
+  if (h->dtopo) (void)hipFree(h->dtopo);
   if (h->state) (void)hipFree(h->state);
   if (h->rnd) (void)hipFree(h->rnd);
   if (h->stats) (void)hipFree(h->stats);
@@ -236,6 +317,7 @@ static zb::StepArgs base_args(ZbHandle* h) {
   zb::StepArgs a;
   memset(&a, 0, sizeof a);
   a.model = h->dmodel;
+  a.topo = h->dtopo;
   a.cfg = h->dcfg;
   a.n_envs = h->n;
   a.env_offset = h->env_offset;

@@ -2538,8 +2538,10 @@ __device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, flo
 }
 
 /* ---------------------------- per-team context ------------------------------ */
-__device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvConfig* cfg, EnvL* L,
-                                         uint64_t seed, uint32_t env) {
+__device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvConfig* cfg, const int32_t* topo,
+                                         EnvL* L, uint64_t seed, uint32_t env) {
+  static_assert(TOPO_NROOT == NROOT && TOPO_NGEOM == NGEOM && TOPO_MAXBD == MAXBD && TOPO_LANES == TEAM,
+                "topology table built for this kernel's constants");
   c.m = (MP)m;
   c.cfg = (CP)cfg;
   c.L = L;
@@ -2548,53 +2550,28 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   const int l = threadIdx.x & (TEAM - 1);
   c.l = l;
   c.nu = m->nu;
-  /* body role */
-  const bool isb = l < NB;
-  c.bpar = isb ? m->body_parent[l] : 0;
-  c.bdep = isb ? m->body_depth[l] : 1000;
-  c.bjt = isb ? m->body_jnttype[l] : ZB_JNT_NONE;
-  c.bdofadr = isb ? m->body_dofadr[l] : -1;
-  c.blast = isb ? m->body_lastdof[l] : -1;
-  
-  int nch = 0;
-  uint32_t ch0 = 0, ch1 = 0;
-  for (int b = 1; b < NB; b++) {
-    if (isb && m->body_parent[b] == l && nch < 8) {
-      if (nch < 4) ch0 |= (uint32_t)b << (8 * nch);
-      else ch1 |= (uint32_t)b << (8 * (nch - 4));
-      nch++;
-    }
-  }
-  c.nch = nch;
-  c.ch0 = ch0;
-  c.ch1 = ch1;
-  uint64_t lv = 0;
-  for (int d = 0; d <= MAXBD && d < 16; d++) {
-    int mx = tmaxi(c.bdep == d ? nch : 0);
-    lv |= (uint64_t)(mx & 0xf) << (4 * d);
-  }
-  c.lvlch = lv;
-  /* dof role */
-  const bool isd = l < NV;
-  c.ddep = isd ? m->dof_depth[l] : 0;
-  c.dbody = isd ? m->dof_body[l] : 0;
-  c.qadr = isd ? m->dof_qposadr[l] : -1;
-  c.act = -1;
-  for (int a = 0; a < c.nu; a++)
-    if (isd && m->act_dof[a] == l) c.act = a;
-  uint32_t desc = 0;
-  for (int k = 0; k < NV; k++) {
-    int dk = m->dof_depth[k];
-    const int anc = vopq(m->dof_anc[k][c.ddep]);
-    if (isd && k != l && dk > c.ddep && anc == l) desc |= 1u << k;
-  }
-  uint32_t rm = 0;
-  for (int g = 0; g < NGEOM; g++) {
-    int kd = m->body_lastdof[m->geom_body[g]];
-    if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm |= 0xFFFFu << (16 * g);
-  }
-  c.rowmask = rm;
-  if (!isd) {
+  /* the lane's roles, from the table zb_create built (all loads in flight) */
+  const int32_t* t = topo + l;
+  c.bpar = t[TP_BPAR * TEAM];
+  c.bdep = t[TP_BDEP * TEAM];
+  c.bjt = t[TP_BJT * TEAM];
+  c.bdofadr = t[TP_BDOFADR * TEAM];
+  c.blast = t[TP_BLAST * TEAM];
+  c.nch = t[TP_NCH * TEAM];
+  c.ch0 = (uint32_t)t[TP_CH0 * TEAM];
+  c.ch1 = (uint32_t)t[TP_CH1 * TEAM];
+  c.lvlch = (uint64_t)(uint32_t)t[TP_LVL_LO * TEAM] | ((uint64_t)(uint32_t)t[TP_LVL_HI * TEAM] << 32);
+  c.ddep = t[TP_DDEP * TEAM];
+  c.dbody = t[TP_DBODY * TEAM];
+  c.qadr = t[TP_QADR * TEAM];
+  c.act = t[TP_ACT * TEAM];
+  c.rowmask = (uint32_t)t[TP_ROWMASK * TEAM];
+  c.dk0 = t[TP_DK0 * TEAM];
+  c.dfree = t[TP_DFREE * TEAM];
+  c.chd = t[TP_CHD * TEAM];
+  c.cps = t[TP_CPS * TEAM];
+  c.cln = t[TP_CLN * TEAM];
+  if (l >= NV) {
     /* non-dof lanes: zero factor and mass rows (row 31 is the zero row that masked
        gathers point at; kernels never write these rows afterwards) */
     float z[CAP];
@@ -2602,22 +2579,6 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
     for (int e = 0; e < CAP; e++) z[e] = 0.f;
     st_row(&L->L[l][0], z);
     st_row(&L->M[l][0], z);
-  }
-  c.dk0 = isd ? l - m->body_dofadr[c.dbody] : 0;
-  c.dfree = isd && m->body_jnttype[c.dbody] == ZB_JNT_FREE;
-  {
-    const int nr = NROOT;
-    int hd = -1, ln = 0;
-    if (isd && l >= nr) {
-      hd = l;
-      while (m->dof_parent[hd] >= nr) hd = m->dof_parent[hd];
-      int k = hd;
-      while (k + 1 < NV && m->dof_parent[k + 1] == k) k++;
-      ln = k - hd + 1;
-    }
-    c.chd = hd;
-    c.cps = hd >= 0 ? l - hd : 0;
-    c.cln = ln;
   }
 }
 
@@ -2640,7 +2601,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
   float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   float* rnd = live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)ee * ZB_RAND_STRIDE : nullptr;
 #ifdef ZB_STAMPS
@@ -2753,7 +2714,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
   float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   float* rnd = live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)ee * ZB_RAND_STRIDE : nullptr;
   EnvS& s = c.L->s;
@@ -2782,7 +2743,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
-  make_ctx(c, m, cfg, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
   float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   EnvS& s = c.L->s;
   LaneS ls;

@@ -26,8 +26,21 @@
 
 namespace zb {
 
+/* per-lane topology of a team (32 lanes), built once by zb_create from the model
+   (zb_capi.cpp build_topology) and read by the kernels' make_ctx: field-major
+   [TP_NF][32] int32 */
+enum {
+  TP_BPAR, TP_BDEP, TP_BJT, TP_BDOFADR, TP_BLAST, TP_NCH, TP_CH0, TP_CH1, TP_LVL_LO, TP_LVL_HI,
+  TP_DDEP, TP_DBODY, TP_QADR, TP_ACT, TP_ROWMASK, TP_DK0, TP_DFREE, TP_CHD, TP_CPS, TP_CLN, TP_NF
+};
+constexpr int TOPO_LANES = 32;
+constexpr int TOPO_NROOT = 6;  /* root dof chain (the free joint), zb_engine.hip NROOT */
+constexpr int TOPO_NGEOM = 2;  /* foot geoms, zb_engine.hip NGEOM */
+constexpr int TOPO_MAXBD = 8;  /* deepest body, zb_engine.hip MAXBD */
+
 struct StepArgs {
   const ZbModel* model;     /* device copy */
+  const int32_t* topo;      /* [TP_NF][32] per-lane topology (device) */
   const ZbEnvConfig* cfg;   /* device copy */
   int n_envs;
   int env_offset;
