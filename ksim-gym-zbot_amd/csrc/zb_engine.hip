@@ -982,16 +982,18 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
     const float dk = tsh(Xd, src);
 #pragma unroll
     for (int k = q + 1; k < NLIMBLV; k++) wq[k] = tsh(wacc[k], src);
-    /* A(k, j) = r[depth(j)], depth(j) = NROOT + cps, cps < q */
-    float t = r[NROOT];
-#pragma unroll
-    for (int p = 1; p < q; p++) t = cps == p ? r[NROOT + p] : t;
+    /* A(q, p) from the lane's own row: slot NROOT + pos holds A(p, pos) for every chain
+       position, ancestors below the diagonal and deeper dofs in the padding (the rows
+       carry their transposed entries there, com_crb_m / hessian_factor), and the update
+       below keeps the padding current, so the entry sits at a fixed slot */
+    const float t = X[NROOT + q];
     const float sc = has ? t / fmaxf(dk, MINVAL) : 0.f;
     Xd -= sc * t;
-    /* entries at chain positions >= the lane's own are never read (a pivot at
-       level p only hands out positions < p), so no mask */
+    /* every position below the pivot: the ancestors (read by later pivots' receivers)
+       and the padding up to q - 1 (the next levels' t); the slot of the lane's own
+       position is junk, never read (Xd is the diagonal) */
 #pragma unroll
-    for (int e = NROOT; e < NROOT + q - 1; e++) X[e] -= sc * r[e];
+    for (int e = NROOT; e < NROOT + q; e++) X[e] -= sc * r[e];
     wacc[q] += sc;
 #pragma unroll
     for (int k = q + 1; k < NLIMBLV; k++) wacc[k] -= sc * wq[k];
