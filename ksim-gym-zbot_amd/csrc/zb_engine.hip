@@ -300,7 +300,15 @@ __device__ __forceinline__ int tmaxi(int v) {
   v = max(v, dppi<0x140>(v));
   return rows2max(v);
 }
-__device__ __forceinline__ void tsync() { __syncthreads(); }
+/* The team exchange point. A workgroup is one wave, and the LDS unit executes one wave's
+   DS instructions in issue order, so a lane's ds_write is seen by any later ds_read or
+   ds_bpermute of the wave: no s_barrier and no lgkmcnt drain are needed, only a point the
+   compiler cannot move LDS accesses across. */
+__device__ __forceinline__ void tsync() {
+  static_assert(NTEAM * TEAM == 64, "one wave per workgroup");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 /* a loaded value pinned in place: `t = keepf(load); p ? t : k` stays a load and a select. Without
    it the compiler sinks the load into a branch of its own, with a full LDS round trip
    (s_waitcnt lgkmcnt(0)) per element instead of all loads in flight. */
