@@ -792,15 +792,8 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
     quat2mat(R, xqs);
 #pragma unroll
     for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], bj);
-    /* the joint's axis and anchor, fetched by every lane (a load under the branch below
-       would wait for each element in turn) */
-    float jax[3], jpos[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      jax[i] = keepf(m->jnt_axis[bj][i]);
-      jpos[i] = keepf(m->jnt_pos[bj][i]);
-    }
-    if (j < NV) {
+    /* every lane, the non-dof ones storing zero rows (read as zero by com_vel / com_acc) */
+    {
       /* branch-free over the dof kinds (the task's dofs are the free joint's 6 and
          hinges): the motion axis in the body frame is jnt_axis for a hinge and unit
          axis k-3 for a free-joint rotation, anchored at jnt_pos / the body origin;
@@ -811,8 +804,8 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
       float ja[3], jp[3], t[3], ax[3];
 #pragma unroll
       for (int i = 0; i < 3; i++) {
-        ja[i] = isfree ? (k - 3 == i ? 1.f : 0.f) : jax[i];
-        jp[i] = isfree ? 0.f : jpos[i];
+        ja[i] = isfree ? (k - 3 == i ? 1.f : 0.f) : m->jnt_axis[bj][i];
+        jp[i] = isfree ? 0.f : m->jnt_pos[bj][i];
       }
       mulmv3(t, R, jp);
       mulmv3(ax, R, ja);
@@ -824,8 +817,9 @@ __device__ __forceinline__ void com_crb_m(const Ctx& c, const EnvS& s, const Lan
         cd[i] = trans ? 0.f : ax[i];
         cd[3 + i] = trans ? (k == i ? 1.f : 0.f) : cr[i];
       }
+      const bool isd = j < NV;
 #pragma unroll
-      for (int i = 0; i < 6; i++) L->cdof[j][i] = cd[i];
+      for (int i = 0; i < 6; i++) L->cdof[j][i] = isd ? cd[i] : 0.f;
     }
   }
   /* crb = subtree sums of cinert */
@@ -1114,8 +1108,8 @@ __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
   /* no mask: entries at or past the depth (the diagonal, the transposed entries) are never read
      as off-diagonals by the factorization, and non-dof rows are zero */
   ld_row(&c.L->M[j][0], X);
-  const float d = keepf(c.L->M[j][ddep]);
-  return (c.l < NV) ? d : 1.f;
+  /* non-dof rows are zero: their diagonal becomes 1 without a select around the load */
+  return c.L->M[j][ddep] + (c.l < NV ? 0.f : 1.f);
 }
 
 /* x <- (L'DL)^-1 x, x held by dof lanes (mj_solveM order: L' pass from the
@@ -1279,15 +1273,13 @@ __device__ __forceinline__ void com_vel(const Ctx& c, BodyK& B, float qv, float 
   EnvL* L = c.L;
   const int j = c.l;
   const bool isd = j < NV;
+  /* non-dof rows of cdof are zero (com_crb_m) and so is their qv */
   float cd[6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const float t = keepf(L->cdof[j][k]);
-    cd[k] = isd ? t : 0.f;
-  }
+  for (int k = 0; k < 6; k++) cd[k] = L->cdof[j][k];
   float P[6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) P[k] = isd ? cd[k] * qv : 0.f;
+  for (int k = 0; k < 6; k++) P[k] = cd[k] * qv;
   dof_prefix6(c, P);
   /* velocity before this dof's own contribution: the parent's prefix for a
      hinge, the translational part (dof 2) for the free joint's rotations */
@@ -1325,10 +1317,7 @@ __device__ __forceinline__ void com_acc(const Ctx& c, const float cdd[6], float 
   for (int k = 0; k < 6; k++) P[k] = isd ? cdd[k] * qv : 0.f;
   if (with_acc) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const float t = keepf(L->cdof[j][k]);
-      P[k] += isd ? t * qa : 0.f;
-    }
+    for (int k = 0; k < 6; k++) P[k] += L->cdof[j][k] * qa; /* zero rows past the dofs */
   }
   dof_prefix6(c, P);
   const float g[6] = {0.f, 0.f, 0.f, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
@@ -1484,7 +1473,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
                             dir[0] * L->cdof[a][3] + dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
       v = e <= r.kdep ? v : 0.f;
       Jc[e] = v;
-      vel += v * keepf(L->vec[V_QVEL][a]);
+      vel += v * L->vec[V_QVEL][a];
     }
     float dA = m->body_invweight0[gb][0] * (1.f + mu * mu);
     float Rr;
@@ -1751,8 +1740,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
       ld_row(&L->u.J[k1][0], j1);
       const float jd0 = L->u.J[k0][ddep], jd1 = L->u.J[k1][ddep];
       const float jj0 = da[k0] * jd0;
-      const float da1 = keepf(da[k1]);
-      const float jj1 = h1 ? da1 * jd1 : 0.f;
+      const float jj1 = (da[k1] * jd1) * (h1 ? 1.f : 0.f); /* a weight, not a select (loads) */
       Hd += jj0 * jd0;
       Hd += jj1 * jd1;
 #pragma unroll
@@ -1858,9 +1846,9 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float x = w;
   if (c.l < 32) L->vec[V_TMP2][c.l] = qs; /* mul_m's barrier publishes it with x in vec[V_TMP] */
   float Ma = mul_m(c, x, V_TMP);
-  const float rw = keepf(row_dot(c, r, V_TMP)), rs = keepf(row_dot(c, r, V_TMP2));
-  float jw = r.ex ? rw - r.aref : 0.f;
-  float js = r.ex ? rs - r.aref : 0.f;
+  /* rows that do not exist have zero J and zero aref: no mask */
+  float jw = row_dot(c, r, V_TMP) - r.aref;
+  float js = row_dot(c, r, V_TMP2) - r.aref;
   tsync();
   float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, r.sl * x - r.al),
                   rows_cost(c, r, js, qs - r.af, r.sl * qs - r.al)};
