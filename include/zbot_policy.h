@@ -48,7 +48,7 @@ extern "C" {
 #define ZB_POL_ACTOR_IN 50     /* NUM_ACTOR_INPUTS train.py:51 */
 #define ZB_POL_CRITIC_IN 484   /* NUM_CRITIC_INPUTS train.py:52 */
 #define ZB_POL_ACTOR_OUT 300   /* NUM_JOINTS * 3 * num_mixtures train.py:934-938 */
-#define ZB_POL_ENVS_PER_BLOCK 32
+#define ZB_POL_ENVS_PER_BLOCK 32   /* envs per workgroup (two 16-row matrix-core tiles) */
 
 #define ZB_POL_ACTOR 0
 #define ZB_POL_CRITIC 1

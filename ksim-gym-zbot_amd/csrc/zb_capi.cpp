@@ -514,16 +514,16 @@ size_t zb_policy_param_count(int kind) {
   return H * I + H + D * (6 * H * H + 4 * H) + O * H + O + (kind == ZB_POL_ACTOR ? ZB_POL_JOINTS : 0);
 }
 
-/* W [N][K] (natural layout) -> matrix-core B fragments [ceil(N/32)][ceil(K/8)][64][4]:
-   element u of lane l in k-group g of tile t is W[32t + (l & 31)][8g + 2u + (l >> 5)]
+/* W [N][K] (natural layout) -> B fragments of v_mfma_f32_16x16x4_f32 [ceil(N/16)][ceil(K/16)][64][4]:
+   element u of lane l in k-group g of tile t is W[16t + (l & 15)][16g + 4u + (l >> 4)]
    (zero outside W), so a lane reads 4 consecutive MFMA k-steps with one 16-B load */
 static void pack_b(const float* W, int N, int K, std::vector<float>& out) {
-  const int NT = (N + 31) / 32, G = (K + 7) / 8;
+  const int NT = (N + 15) / 16, G = (K + 15) / 16;
   for (int t = 0; t < NT; t++)
     for (int g = 0; g < G; g++)
       for (int l = 0; l < 64; l++)
         for (int u = 0; u < 4; u++) {
-          const int row = 32 * t + (l & 31), k = 8 * g + 2 * u + (l >> 5);
+          const int row = 16 * t + (l & 15), k = 16 * g + 4 * u + (l >> 4);
           out.push_back(row < N && k < K ? W[(size_t)row * K + k] : 0.f);
         }
 }

@@ -8,17 +8,20 @@
  * ksim MixtureOfGaussians [U].
  *
  * Layout of one launch (n envs, one step):
- *   workgroup = 32 envs (the M = 32 tile of v_mfma_f32_32x32x2_f32) x 4 waves;
- *   wave w owns hidden units 32w .. 32w+31 of every layer, so the r / z / n
- *   gates of a unit land in the same lane and the GRU update happens in
- *   registers: per layer 6 accumulators (W_ih x and W_hh h for r, z, n),
- *   K = 128 in 64 MFMA steps each.
+ *   workgroup = 32 envs x 8 waves; the 32 envs are two row tiles of
+ *   v_mfma_f32_16x16x4_f32 (M = 16), and wave w owns the 16-unit tile w of
+ *   every layer for both row tiles, so each weight fragment a wave loads
+ *   feeds two MFMAs (the weight stream per env of a 32-env tile) while every
+ *   SIMD holds two waves: one wave's GRU epilogue, LDS traffic and barriers run
+ *   under the other's MFMAs. The r / z / n gates of a unit land in the same
+ *   lane and the GRU update happens in registers: per layer 12 accumulators
+ *   (W_ih x and W_hh h for r, z, n, two row tiles), K = 128 in 32 MFMA steps.
  *   A operands (activations) live in LDS k-major, [k][env] with a 33-float
- *   row stride: one ds_read_b32 per operand per step, conflict-free.
+ *   row stride: one ds_read_b32 per operand per step.
  *   B operands (weights) are pre-packed on the host in fragment order —
- *   [tile][group of 4 k-steps][lane][4] — so each lane streams one 16-B load
- *   per 4 MFMA steps per matrix; every workgroup reads the whole weight set
- *   (2.0 MB actor, 2.2 MB critic), which stays L2-resident across the chip.
+ *   [16-unit tile][group of 4 k-steps][lane][4] — so each lane streams one 16-B
+ *   load per 4 MFMA steps per matrix tile; every workgroup reads the whole
+ *   weight set (2.0 MB actor, 2.2 MB critic), which stays L2-resident.
  *   The carry of layer l + 1 is loaded from HBM into registers while layer l
  *   runs (its latency hides behind the MFMAs) and layer l's new carry is
  *   written at its end ([n][5][128] fp32, 2.5 KB per env per step).
@@ -41,48 +44,54 @@ namespace pol {
 
 constexpr int H = ZB_POL_HIDDEN;
 constexpr int D = ZB_POL_DEPTH;
-constexpr int M = ZB_POL_ENVS_PER_BLOCK; /* envs per workgroup: the MFMA M tile */
-constexpr int NWAVE = H / 32;            /* one wave per 32 hidden units */
+constexpr int M = ZB_POL_ENVS_PER_BLOCK; /* envs per workgroup */
+constexpr int MT = 16;                   /* envs per MFMA row tile */
+constexpr int NET = M / MT;              /* row tiles per workgroup */
+constexpr int NWAVE = H / 16;            /* one wave per 16-unit tile */
 constexpr int NTHR = 64 * NWAVE;
 constexpr int LDA = M + 1;  /* row stride of the [k][env] activation tiles */
-constexpr int GH = H / 8;   /* 4-step (8-k) groups over K = H */
+constexpr int GH = H / 16;  /* 4-step (16-k) groups over K = H */
 constexpr int NJ = ZB_POL_JOINTS;
 constexpr int NMIX = ZB_POL_MIX;
+static_assert(M == 32 && NET == 2, "two 16-env row tiles of v_mfma_f32_16x16x4_f32");
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-/* env row of accumulator register i in lane l (32x32 f32 MFMA C/D map) */
-__device__ __forceinline__ int crow(int i, int l) { return (i & 3) + 8 * (i >> 2) + 4 * (l >> 5); }
+/* env of accumulator register v in lane l of row tile et (16x16 f32 MFMA C/D map) */
+__device__ __forceinline__ int crow(int et, int v, int l) { return MT * et + 4 * (l >> 4) + v; }
 
-__device__ __forceinline__ f32x16 mma(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ float q4(const float4& v, int u) {
   return u == 0 ? v.x : (u == 1 ? v.y : (u == 2 ? v.z : v.w));
 }
 
-/* one output tile (32 columns) of X[32][K] W^T over K = 8 * G, A from LDS */
-__device__ __forceinline__ f32x16 tile_gemm(const float* xs, const float4* wp, int G, int lane) {
-  const int c32 = lane & 31, h2 = lane >> 5;
-  f32x16 acc = {};
+/* one output tile (16 columns) of X[32][K] W^T over K = 16 * G for both row tiles, A from
+   LDS; each weight fragment feeds both row tiles */
+__device__ __forceinline__ void tile_gemm(const float* xs, const float4* wp, int G, int lane, f32x4 acc[NET]) {
+  const int c16 = lane & 15, k4 = lane >> 4;
+#pragma unroll
+  for (int et = 0; et < NET; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
   float4 b = wp[0];
   for (int g = 0; g < G; ++g) {
     const float4 bn = wp[(size_t)(g + 1 < G ? g + 1 : g) * 64];
     __builtin_amdgcn_sched_barrier(0); /* next group's load stays a group ahead */
-    const float* xp = xs + (8 * g + h2) * LDA + c32;
+    const float* xp = xs + (16 * g + k4) * LDA + c16;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc = mma(xp[2 * u * LDA], q4(b, u), acc);
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int et = 0; et < NET; ++et) acc[et] = mma(xp[4 * u * LDA + MT * et], q4(b, u), acc[et]);
     b = bn;
   }
-  return acc;
 }
 
 template <int KIN, int NOUT, bool ACTOR>
 __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
 #pragma clang fp contract(off)
-  constexpr int KPAD = (KIN + 7) / 8 * 8;
-  constexpr int GIN = KPAD / 8;
-  constexpr int NTO = (NOUT + 31) / 32;
+  constexpr int KPAD = (KIN + 15) / 16 * 16;
+  constexpr int GIN = KPAD / 16;
+  constexpr int NTO = (NOUT + 15) / 16;
   constexpr int OUTS = NOUT + 1;
   constexpr int XIN = KPAD * LDA;
   constexpr int OUTW = ACTOR ? M * OUTS : 1;
@@ -92,12 +101,12 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   __shared__ float sh[H * LDA];     /* carry of the current layer [unit][env] */
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int c32 = lane & 31, h2 = lane >> 5;
+  const int c16 = lane & 15, k4 = lane >> 4;
   const int e0 = blockIdx.x * M;
-  const int unit = 32 * w + c32;
   const float4* wp4 = reinterpret_cast<const float4*>(a.wpack);
 
   constexpr int CPT = M * (H / 4) / NTHR;
+  static_assert(CPT * NTHR == M * (H / 4), "carry float4s per thread");
   float4 cr[CPT];
   auto load_carry = [&](int l) {
 #pragma unroll
@@ -114,8 +123,7 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
 
   /* 1. observation tile [k][env], zero-padded to KPAD. The block's 32 observation rows are one
         contiguous chunk of M * KIN floats: stream it with 16-B loads, all issued before the
-        first LDS store (a load-then-store loop would wait out one HBM round trip per pass:
-        61 passes for the critic's 484 features). */
+        first LDS store (a load-then-store loop would wait out one HBM round trip per pass). */
   {
     constexpr int FL = M * KIN, NV4 = (FL + 3) / 4, PASSES = (NV4 + NTHR - 1) / NTHR;
     const int lim = (a.n - e0 < M ? a.n - e0 : M) * KIN; /* valid floats of this block */
@@ -160,17 +168,21 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   }
   __syncthreads();
 
-  /* 2. input projection (no activation: train.py:944) */
+  /* 2. input projection (no activation: train.py:944): the wave's unit tile */
   {
-    const f32x16 acc = tile_gemm(su, wp4 + (size_t)w * GIN * 64 + lane, GIN, lane);
+    const int unit = 16 * w + c16;
+    f32x4 acc[NET];
+    tile_gemm(su, wp4 + (size_t)w * GIN * 64 + lane, GIN, lane, acc);
     const float bu = a.bias[unit];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sx[0][unit * LDA + crow(i, lane)] = acc[i] + bu;
+    for (int et = 0; et < NET; ++et)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) sx[0][unit * LDA + crow(et, v, lane)] = acc[et][v] + bu;
   }
 
   /* 3. GRU stack (train.py:945-948) */
-  const size_t off_gru = (size_t)(H / 32) * GIN * 64;  /* float4 offset of layer 0's W_ih pack */
-  constexpr size_t MAT = (size_t)12 * GH * 64;         /* one packed [3H][H] matrix, float4 */
+  const size_t off_gru = (size_t)(H / 16) * GIN * 64;  /* float4 offset of layer 0's W_ih pack */
+  constexpr size_t MAT = (size_t)(3 * H / 16) * GH * 64; /* one packed [3H][H] matrix, float4 */
   int cur = 0;
   for (int l = 0; l < D; ++l) {
     /* carry of layer l (prefetched during layer l - 1) -> sh */
@@ -189,45 +201,69 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
     const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
     const float4* whh = wih + MAT;
     const float* xs = sx[cur];
-    /* gate tiles of this wave's units: r = w, z = 4 + w, n = 8 + w */
-    const size_t tr = (size_t)w * GH * 64, tz = (size_t)(4 + w) * GH * 64, tn = (size_t)(8 + w) * GH * 64;
-    f32x16 ir = {}, iz = {}, in = {}, hr = {}, hz = {}, hn = {};
-    float4 b0 = wih[tr], b1 = wih[tz], b2 = wih[tn], b3 = whh[tr], b4 = whh[tz], b5 = whh[tn];
+    /* gate tiles of this wave's units: r = w, z = 8 + w, n = 16 + w */
+    size_t to[3];
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt) to[gt] = (size_t)(8 * gt + w) * GH * 64;
+    /* accumulators [gate][row tile] */
+    f32x4 ia[3][NET], ha[3][NET];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int et = 0; et < NET; ++et) ia[i][et] = ha[i][et] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 bi[3], bh[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      bi[i] = wih[to[i]];
+      bh[i] = whh[to[i]];
+    }
     for (int g = 0; g < GH; ++g) {
       const size_t gn = (size_t)(g + 1 < GH ? g + 1 : g) * 64;
-      const float4 n0 = wih[tr + gn], n1 = wih[tz + gn], n2 = wih[tn + gn];
-      const float4 n3 = whh[tr + gn], n4 = whh[tz + gn], n5 = whh[tn + gn];
-      /* keep the next group's loads here, a whole group (24 MFMAs) ahead of their use: the
-         fully unrolled loop otherwise lets the scheduler sink them next to their first MFMA */
-      __builtin_amdgcn_sched_barrier(0);
-      const float* xp = xs + (8 * g + h2) * LDA + c32;
-      const float* hp = sh + (8 * g + h2) * LDA + c32;
+      float4 ni[3], nh[3];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float ax = xp[2 * u * LDA], ah = hp[2 * u * LDA];
-        ir = mma(ax, q4(b0, u), ir);
-        iz = mma(ax, q4(b1, u), iz);
-        in = mma(ax, q4(b2, u), in);
-        hr = mma(ah, q4(b3, u), hr);
-        hz = mma(ah, q4(b4, u), hz);
-        hn = mma(ah, q4(b5, u), hn);
+      for (int i = 0; i < 3; ++i) {
+        ni[i] = wih[to[i] + gn];
+        nh[i] = whh[to[i] + gn];
       }
-      b0 = n0; b1 = n1; b2 = n2; b3 = n3; b4 = n4; b5 = n5;
+      /* keep the next group's loads here, a whole group (48 MFMAs) ahead of their use */
+      __builtin_amdgcn_sched_barrier(0);
+      const float* xp = xs + (16 * g + k4) * LDA + c16;
+      const float* hp = sh + (16 * g + k4) * LDA + c16;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int et = 0; et < NET; ++et) {
+          const float ax = xp[4 * u * LDA + MT * et], ah = hp[4 * u * LDA + MT * et];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ia[i][et] = mma(ax, q4(bi[i], u), ia[i][et]);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ha[i][et] = mma(ah, q4(bh[i], u), ha[i][et]);
+        }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        bi[i] = ni[i];
+        bh[i] = nh[i];
+      }
     }
     /* equinox GRUCell: r, z, n gates; h' = n + z (h - n) */
     const float* bl = a.bias + H + (size_t)l * 4 * H;
-    const float br = bl[unit], bz = bl[H + unit], bni = bl[2 * H + unit], bnh = bl[3 * H + unit];
     float* xo = sx[cur ^ 1];
+    {
+      const int unit = 16 * w + c16;
+      const float br = bl[unit], bz = bl[H + unit], bni = bl[2 * H + unit], bnh = bl[3 * H + unit];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int e = crow(i, lane);
-      const float r = zbf_sigmoid((ir[i] + br) + hr[i]);
-      const float z = zbf_sigmoid((iz[i] + bz) + hz[i]);
-      const float nn = zbf_tanh((in[i] + bni) + r * (hn[i] + bnh));
-      const float ho = sh[unit * LDA + e];
-      const float hv = nn + z * (ho - nn);
-      xo[unit * LDA + e] = hv;
-      if (e0 + e < a.n) a.carry[((size_t)(e0 + e) * D + l) * H + unit] = hv;
+      for (int et = 0; et < NET; ++et)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int e = crow(et, v, lane);
+        const float r = zbf_sigmoid((ia[0][et][v] + br) + ha[0][et][v]);
+        const float z = zbf_sigmoid((ia[1][et][v] + bz) + ha[1][et][v]);
+        const float nn = zbf_tanh((ia[2][et][v] + bni) + r * (ha[2][et][v] + bnh));
+        const float ho = sh[unit * LDA + e];
+        const float hv = nn + z * (ho - nn);
+        xo[unit * LDA + e] = hv;
+        if (e0 + e < a.n) a.carry[((size_t)(e0 + e) * D + l) * H + unit] = hv;
+      }
     }
     __syncthreads();
     cur ^= 1;
@@ -240,12 +276,15 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
     /* output projection (train.py:950) into su[env][c] */
     const float4* wo = wp4 + off_gru + (size_t)D * 2 * MAT + lane;
     for (int nt = w; nt < NTO; nt += NWAVE) {
-      const f32x16 acc = tile_gemm(xs, wo + (size_t)nt * GH * 64, GH, lane);
-      const int c = nt * 32 + c32;
+      f32x4 acc[NET];
+      tile_gemm(xs, wo + (size_t)nt * GH * 64, GH, lane, acc);
+      const int c = nt * 16 + c16;
       if (c < NOUT) {
         const float bc = tail[c];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) su[crow(i, lane) * OUTS + c] = acc[i] + bc;
+        for (int et = 0; et < NET; ++et)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) su[crow(et, v, lane) * OUTS + c] = acc[et][v] + bc;
       }
     }
     __syncthreads();
