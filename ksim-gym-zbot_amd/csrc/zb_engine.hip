@@ -899,19 +899,28 @@ typedef float v4f __attribute__((ext_vector_type(4)));
  * envs of the wave: G[i][e] = sum_k D_k L(k,i) L(k,e), i,e < NROOT, k over the
  * limb dofs NROOT..NV-1 (their eliminated rows are in LDS L[][] / Dk[]). Per
  * env five v_mfma_f32_16x16x4_f32 (K = 4 limb dofs each; lane l supplies row
- * NROOT + 4*chunk + l/16, entry l%16 < NROOT). Lane l ends with
- * G[4*(l/16) + v][l%16]; the lower triangle (21 values, packed i(i+1)/2 + e) is
- * left in the env's vec[V_TMP2], free during every factorization. Replaces 21
- * team reductions (126 DPP/permlane VALU instructions per factor).
+ * NROOT + 4*chunk + l/16, entry l%16 < NROOT), accumulating from the parked root
+ * block. Lane l ends with (A_root - G)[4*(l/16) + v][l%16]; the lower triangle (21
+ * values, packed i(i+1)/2 + e) is left in the env's vec[V_TMP2], free during every
+ * factorization. Replaces 21 team reductions (126 DPP/permlane VALU instructions per
+ * factor) and the 21 subtractions from the parked block.
  * Wave-uniform: call with every lane active (the MFMA reads all 64 lanes). */
 __device__ __forceinline__ void root_schur_mfma() {
   static_assert(NV - NROOT == 20, "five K=4 chunks cover the 20 limb dofs");
   const int l = threadIdx.x & 63;
   const int i = l & 15, kk = l >> 4;
   const int ic = i < RMAX ? i : 0;
+  /* the accumulators start from the parked root block (its diagonal parked in L[r][r] too),
+     so the result is A_root - G; entries above the diagonal or outside the 6 x 6 block are
+     never stored */
   v4f acc[NTEAM];
 #pragma unroll
-  for (int t = 0; t < NTEAM; t++) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NTEAM; t++)
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+      const int row = 4 * kk + v;
+      acc[t][v] = g_lds[t].L[row < RMAX ? row : 0][ic];
+    }
 #pragma unroll
   for (int ch = 0; ch < (NV - NROOT) / 4; ch++)
 #pragma unroll
@@ -920,7 +929,7 @@ __device__ __forceinline__ void root_schur_mfma() {
       const float lv = g_lds[t].L[k][ic];
       const float dv = g_lds[t].Dk[k];
       /* no masks: lanes i >= RMAX feed rows / columns of G that are never stored */
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv * lv, lv, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(-(dv * lv), lv, acc[t], 0, 0, 0);
     }
 #pragma unroll
   for (int t = 0; t < NTEAM; t++)
@@ -951,6 +960,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
   /* root rows are only touched by the dense block at the end: park them */
   if (isroot) {
     st_row(&L->L[c.l][0], X);
+    L->L[c.l][c.l] = Xd; /* the diagonal in place too (root_schur_mfma starts from the block) */
     L->Dk[c.l] = Xd;
   }
   /* limb levels by chain position q = NLIMBLV-1 .. 1 (leaves first; chains
@@ -1059,9 +1069,16 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
       for (int i = 0; i < RMAX; i++) {
 #pragma unroll
         for (int j = 0; j < RMAX; j++) A[i][j] = 0.f;
+        if constexpr (MFMA_SCHUR) {
+          /* the matrix cores already subtracted the Schur complement from the parked block */
 #pragma unroll
-        for (int j = 0; j < i; j++) A[i][j] = i < nroot ? L->L[i][j] - g[t + j] : 0.f;
-        D[i] = i < nroot ? L->Dk[i] - g[t + i] : 1.f;
+          for (int j = 0; j < i; j++) A[i][j] = i < nroot ? g[t + j] : 0.f;
+          D[i] = i < nroot ? g[t + i] : 1.f;
+        } else {
+#pragma unroll
+          for (int j = 0; j < i; j++) A[i][j] = i < nroot ? L->L[i][j] - g[t + j] : 0.f;
+          D[i] = i < nroot ? L->Dk[i] - g[t + i] : 1.f;
+        }
         t += i + 1;
       }
     }
