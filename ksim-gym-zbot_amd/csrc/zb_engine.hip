@@ -1196,17 +1196,17 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   }
   /* backward pass down the limbs: the shallower chain values and W(a, p), all in flight */
   {
+    /* W(a, p) for chain position a: zero for a >= p (stored W rows are zero at and before
+       their own position), so no mask inside the chain; positions past the chain read its
+       last row (zero there too), and a non-chain lane reads the zero rows 26.. */
     float va[NLIMBLV - 1], wa[NLIMBLV - 1];
-    const LdsF wcol = lds_opq(&L->L[chd][NROOT + cps]);
-    const int npre = vopq(ischain ? c.cps : 0); /* shallower chain positions */
+    static_assert(NV + NLIMBLV - 1 <= 31, "zero rows NV .. NV + 4");
+    const int chz = vopq(ischain ? c.chd : NV);
+    const int alast = vopq(ischain ? c.cln - 1 : NLIMBLV - 2);
 #pragma unroll
-    for (int a = 0; a < NLIMBLV - 1; a++) {
-      /* W(a, p) of a shallower chain position (consecutive rows: paired loads), masked */
-      /* a multiply, not a select: a select would let the compiler sink the load into a branch */
-      wa[a] = wcol[a * CAP] * (a < npre ? 1.f : 0.f);
-    }
+    for (int a = 0; a < NLIMBLV - 1; a++) wa[a] = L->L[chz + min(a, alast)][NROOT + cps];
 #pragma unroll
-    for (int a = 0; a < NLIMBLV - 1; a++) va[a] = tsh(x, chd + a);
+    for (int a = 0; a < NLIMBLV - 1; a++) va[a] = tsh(x, chz + a);
     float y = x;
 #pragma unroll
     for (int a = 0; a < NLIMBLV - 1; a++) y += wa[a] * va[a];
