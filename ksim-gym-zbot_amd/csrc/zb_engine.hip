@@ -316,15 +316,6 @@ __device__ __forceinline__ float keepf(float v) {
   asm volatile("" : "+v"(v));
   return v;
 }
-/* an LDS pointer whose whole address sits in one register: loads at small constant
-   offsets from it pair into ds_read2 (the 8-bit dword offsets of ds_read2_b32 cannot
-   hold a field offset inside EnvL, so the compiler would not pair them otherwise) */
-typedef const __attribute__((address_space(3))) float* LdsF;
-__device__ __forceinline__ LdsF lds_opq(const float* p) {
-  uint32_t v = (uint32_t)(uintptr_t)(LdsF)p;
-  asm volatile("" : "+v"(v));
-  return (LdsF)(uintptr_t)v;
-}
 /* bitmask over the team's lanes of predicate p */
 __device__ __forceinline__ uint32_t team_ballot(bool p) { return (uint32_t)(__ballot(p) >> (threadIdx.x & 32)); }
 /* An opaque copy of a per-lane constant: stops the compiler from hoisting
