@@ -3,7 +3,8 @@
 A legged robot in contact is chaotic: two fp32 implementations that agree to rounding at every
 substep (tests/test_gpu_parity.py) separate after tens of control steps. What must still agree
 is the distribution they sample. Over 512 envs and 150 control steps with pushes and action
-noise, from the same reset states and with the same actions, the time-averaged ensemble means
+noise (and per-env randomization in the second configuration), from the same reset states and
+with the same actions, the time-averaged ensemble means
 of the reward, its terms, the base height, the joint speed and the episode ends match the
 oracle's within their statistical spread (tolerances below, several standard errors wide).
 """
@@ -19,15 +20,16 @@ pytestmark = pytest.mark.gpu
 N, T, STD = 512, 150, 0.2
 
 
-@pytest.fixture(scope="module")
-def runs(cmodel, oracle_mod):
+@pytest.fixture(scope="module", params=[(True, False), (True, True)], ids=["push", "push_randomize"])
+def runs(request, cmodel, oracle_mod):
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from zbot_amd.engine import HipEngine
 
-    cfg = default_config(push=True)
+    push, randomize = request.param
+    cfg = default_config(push=push, randomize=randomize)
     ref = oracle_mod.OracleEnv(cmodel.cmodel, cfg, N, seed=11)
     ref.reset()
     eng = HipEngine(cmodel, cfg, N, seed=11)
