@@ -84,3 +84,40 @@ def test_episode_ends_match(runs):
     print(f"episode ends: oracle {do:.0f} engine {de:.0f}")
     # counts of rare events: Poisson spread
     assert abs(de - do) <= 5.0 * np.sqrt(max(do, 1.0)) + 2
+
+
+def test_long_soak_full_size(cmodel):
+    """C5-shaped soak: 8192 envs, pushes and per-env randomization, noisy actions, 1500 control
+    steps (30 000 physics substeps, many episodes per env). Nothing goes non-finite, no env
+    raises the NaN flag, quaternions stay unit, episodes keep ending and restarting, and the
+    per-step reward stays finite and bounded."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from zbot_amd.engine import HipEngine
+
+    n, steps = 8192, 1500
+    cfg = default_config(push=True, randomize=True)
+    eng = HipEngine(cmodel, cfg, n, seed=5)
+    eng.reset()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    bias = torch.tensor([cmodel.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    acts = [bias + 0.2 * torch.randn(n, 20, device="cuda", generator=g) for _ in range(16)]
+    rmin, rmax, dones = float("inf"), float("-inf"), 0
+    for t in range(steps):
+        out = eng.step(acts[t % len(acts)])
+        if t % 100 == 99:
+            r = out["reward"]
+            assert torch.isfinite(r).all()
+            rmin, rmax = min(rmin, float(r.min())), max(rmax, float(r.max()))
+    st = eng.get_state()
+    stats = eng.get_stats(clear=True)
+    dones = float(stats[:, cs.ST_DONE].sum())
+    assert torch.isfinite(st[:, :58]).all() and torch.isfinite(out["obs_critic"]).all()
+    assert (st[:, cs.S_NAN].view(torch.int32) == 0).all()
+    assert torch.allclose(st[:, 3:7].norm(dim=1), torch.ones(n, device="cuda"), atol=2e-6)
+    print(f"soak: {dones:.0f} episode ends over {n} envs x {steps} steps, reward range [{rmin:.3g}, {rmax:.3g}]")
+    assert dones > n  # envs fall and restart, repeatedly
+    assert -100.0 < rmin and rmax < 100.0
