@@ -25,11 +25,15 @@ def build(force: bool = False) -> None:
 
 
 def lib(precision: str = "f32") -> C.CDLL:
-    name = "liboracle_zbot.so" if precision == "f32" else "liboracle_zbot_f64.so"
+    """precision: "f32" (the twin), "f64" (accuracy reference) or "flops" (the fp32 twin with
+    counted arithmetic, zbo_flops_get / zbo_flops_reset; scripts/count_flops.py)."""
+    name = {"f32": "liboracle_zbot.so", "f64": "liboracle_zbot_f64.so", "flops": "liboracle_flops.so"}[precision]
     if name in _LIBS:
         return _LIBS[name]
     path = os.path.join(HERE, name)
-    if not os.path.exists(path):
+    if precision == "flops":
+        subprocess.run(["make", "-C", HERE, "-s", name], check=True)
+    elif not os.path.exists(path):
         build()
     L = C.CDLL(path)
     fp = C.POINTER(C.c_float)
@@ -53,6 +57,9 @@ def lib(precision: str = "f32") -> C.CDLL:
     L.zbo_field_offset.restype = C.c_long
     L.zbo_struct_bytes.argtypes = [C.c_int]
     L.zbo_struct_bytes.restype = C.c_size_t
+    if precision == "flops":
+        L.zbo_flops_get.argtypes = [C.POINTER(C.c_uint64)]
+        L.zbo_flops_reset.argtypes = []
     _LIBS[name] = L
     return L
 

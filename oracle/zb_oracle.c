@@ -42,7 +42,10 @@
 #include "zbot_layout.h"
 #include "zbot_model.h"
 
-#ifdef ZBO_DOUBLE
+#if defined(ZBO_COUNT)
+/* oracle/zb_flops.cpp: `real` is a float that counts its arithmetic, and the math macros
+   (SQRT ... ASIN) are its counting overloads; defined by the including file */
+#elif defined(ZBO_DOUBLE)
 typedef double real;
 #define RS(x) x
 #define SQRT sqrt
@@ -1327,7 +1330,7 @@ static void rewards_and_done(const EnvCtx* c, ZbData* d, float* st, float cur, f
       int prev = st[ZB_S_PREV_CONT + s] > (float)0.5;
       int td = cont[s] && !prev;
       r += (air_prev - cfg->feet_airtime_touchdown_penalty) * (real)td;
-      real air = (cont[s] || done) ? 0 : air_prev + cfg->ctrl_dt;
+      real air = (cont[s] || done) ? (real)0 : air_prev + cfg->ctrl_dt;
       st[ZB_S_AIRTIME + s] = (float)air;
       st[ZB_S_PREV_CONT + s] = (float)cont[s];
     }
