@@ -457,6 +457,30 @@ __device__ __forceinline__ float dot6(const float a[6], const float b[6]) {
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
 __device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
 
+/* State-row words handed from one workgroup to another inside a launch (the chunked step,
+   step_kernel): agent-scope relaxed atomics lower to global_load / global_store with sc1, which
+   bypass the CU's L1. Every load and store of those words uses them, the storing wave waits for
+   its stores (vmcnt(0)) before one lane publishes the progress flag with an sc1 store, and the
+   consumer polls that flag with sc1 loads: the sc1 hand-off of MI355X_MICROARCH.md (inter-
+   workgroup visibility, first row of its hand-off table). */
+typedef __attribute__((address_space(1))) float gfloat_t;
+typedef __attribute__((address_space(1))) uint32_t guint_t;
+__device__ __forceinline__ float ld_cg(const float* p) {
+  return __hip_atomic_load((gfloat_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_cg(float* p, float v) {
+  __hip_atomic_store((gfloat_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ldu_cg(const uint32_t* p) {
+  return __hip_atomic_load((guint_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stu_cg(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((guint_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t addu_cg(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add((guint_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 /* ------------------------ RNG: threefry2x32-20 (Random123) ------------------ */
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 __device__ __forceinline__ void threefry2x32(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t& o0,
@@ -2423,31 +2447,31 @@ __device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, 
 /* ------------------------------ state I/O ---------------------------------- */
 __device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, const float* st) {
   const int l = c.l;
-  for (int k = 0; k < 3; k++) s.bp[k] = st[ZB_S_QPOS + k];
-  for (int k = 0; k < 4; k++) s.bq[k] = st[ZB_S_QPOS + 3 + k];
-  for (int k = 0; k < 4; k++) s.ema[k] = st[ZB_S_IMU_EMA + k];
-  s.lag = st[ZB_S_IMU_LAG];
-  s.air[0] = st[ZB_S_AIRTIME]; s.air[1] = st[ZB_S_AIRTIME + 1];
-  s.push_timer = st[ZB_S_PUSH_TIMER];
-  s.touch[0] = st[ZB_S_TOUCH]; s.touch[1] = st[ZB_S_TOUCH + 1];
-  s.feet_dist = st[ZB_S_FEET_DIST];
-  s.ep_ret = st[ZB_S_EP_RETURN];
-  s.ep_steps = fbits(st[ZB_S_EP_STEPS]);
-  s.rng_step = fbits(st[ZB_S_RNG_STEP]);
-  s.prev_cont[0] = st[ZB_S_PREV_CONT]; s.prev_cont[1] = st[ZB_S_PREV_CONT + 1];
-  s.episode = fbits(st[ZB_S_EPISODE]);
-  s.nanflag = fbits(st[ZB_S_NAN]);
+  for (int k = 0; k < 3; k++) s.bp[k] = ld_cg(st + ZB_S_QPOS + k);
+  for (int k = 0; k < 4; k++) s.bq[k] = ld_cg(st + ZB_S_QPOS + 3 + k);
+  for (int k = 0; k < 4; k++) s.ema[k] = ld_cg(st + ZB_S_IMU_EMA + k);
+  s.lag = ld_cg(st + ZB_S_IMU_LAG);
+  s.air[0] = ld_cg(st + ZB_S_AIRTIME); s.air[1] = ld_cg(st + ZB_S_AIRTIME + 1);
+  s.push_timer = ld_cg(st + ZB_S_PUSH_TIMER);
+  s.touch[0] = ld_cg(st + ZB_S_TOUCH); s.touch[1] = ld_cg(st + ZB_S_TOUCH + 1);
+  s.feet_dist = ld_cg(st + ZB_S_FEET_DIST);
+  s.ep_ret = ld_cg(st + ZB_S_EP_RETURN);
+  s.ep_steps = fbits(ld_cg(st + ZB_S_EP_STEPS));
+  s.rng_step = fbits(ld_cg(st + ZB_S_RNG_STEP));
+  s.prev_cont[0] = ld_cg(st + ZB_S_PREV_CONT); s.prev_cont[1] = ld_cg(st + ZB_S_PREV_CONT + 1);
+  s.episode = fbits(ld_cg(st + ZB_S_EPISODE));
+  s.nanflag = fbits(ld_cg(st + ZB_S_NAN));
   ls.q = ls.v = ls.w = 0.f;
   ls.pp = ls.pv = ls.ptau = 0.f;
   if (l < NV) {
-    ls.v = st[ZB_S_QVEL + l];
-    ls.w = st[ZB_S_QACCW + l];
-    if (c.qadr >= 0) ls.q = st[ZB_S_QPOS + c.qadr];
+    ls.v = ld_cg(st + ZB_S_QVEL + l);
+    ls.w = ld_cg(st + ZB_S_QACCW + l);
+    if (c.qadr >= 0) ls.q = ld_cg(st + ZB_S_QPOS + c.qadr);
   }
   if (c.act >= 0) {
-    ls.pp = st[ZB_S_PLAN_POS + c.act];
-    ls.pv = st[ZB_S_PLAN_VEL + c.act];
-    ls.ptau = st[ZB_S_PLAN_TAU + c.act];
+    ls.pp = ld_cg(st + ZB_S_PLAN_POS + c.act);
+    ls.pv = ld_cg(st + ZB_S_PLAN_VEL + c.act);
+    ls.ptau = ld_cg(st + ZB_S_PLAN_TAU + c.act);
   }
   ls.ctrl = 0.f;
   ls.qacc = 0.f;
@@ -2457,30 +2481,30 @@ __device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, con
 __device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const LaneS& ls, float* st) {
   const int l = c.l;
   if (l < NV) {
-    st[ZB_S_QVEL + l] = ls.v;
-    st[ZB_S_QACCW + l] = ls.w;
-    if (c.qadr >= 0) st[ZB_S_QPOS + c.qadr] = ls.q;
+    st_cg(st + ZB_S_QVEL + l, ls.v);
+    st_cg(st + ZB_S_QACCW + l, ls.w);
+    if (c.qadr >= 0) st_cg(st + ZB_S_QPOS + c.qadr, ls.q);
   }
   if (c.act >= 0) {
-    st[ZB_S_PLAN_POS + c.act] = ls.pp;
-    st[ZB_S_PLAN_VEL + c.act] = ls.pv;
-    st[ZB_S_PLAN_TAU + c.act] = ls.ptau;
+    st_cg(st + ZB_S_PLAN_POS + c.act, ls.pp);
+    st_cg(st + ZB_S_PLAN_VEL + c.act, ls.pv);
+    st_cg(st + ZB_S_PLAN_TAU + c.act, ls.ptau);
   }
   if (l == 0) {
-    for (int k = 0; k < 3; k++) st[ZB_S_QPOS + k] = s.bp[k];
-    for (int k = 0; k < 4; k++) st[ZB_S_QPOS + 3 + k] = s.bq[k];
-    for (int k = 0; k < 4; k++) st[ZB_S_IMU_EMA + k] = s.ema[k];
-    st[ZB_S_IMU_LAG] = s.lag;
-    st[ZB_S_AIRTIME] = s.air[0]; st[ZB_S_AIRTIME + 1] = s.air[1];
-    st[ZB_S_PUSH_TIMER] = s.push_timer;
-    st[ZB_S_TOUCH] = s.touch[0]; st[ZB_S_TOUCH + 1] = s.touch[1];
-    st[ZB_S_FEET_DIST] = s.feet_dist;
-    st[ZB_S_EP_RETURN] = s.ep_ret;
-    st[ZB_S_EP_STEPS] = bitsf(s.ep_steps);
-    st[ZB_S_RNG_STEP] = bitsf(s.rng_step);
-    st[ZB_S_PREV_CONT] = s.prev_cont[0]; st[ZB_S_PREV_CONT + 1] = s.prev_cont[1];
-    st[ZB_S_EPISODE] = bitsf(s.episode);
-    st[ZB_S_NAN] = bitsf(s.nanflag);
+    for (int k = 0; k < 3; k++) st_cg(st + ZB_S_QPOS + k, s.bp[k]);
+    for (int k = 0; k < 4; k++) st_cg(st + ZB_S_QPOS + 3 + k, s.bq[k]);
+    for (int k = 0; k < 4; k++) st_cg(st + ZB_S_IMU_EMA + k, s.ema[k]);
+    st_cg(st + ZB_S_IMU_LAG, s.lag);
+    st_cg(st + ZB_S_AIRTIME, s.air[0]); st_cg(st + ZB_S_AIRTIME + 1, s.air[1]);
+    st_cg(st + ZB_S_PUSH_TIMER, s.push_timer);
+    st_cg(st + ZB_S_TOUCH, s.touch[0]); st_cg(st + ZB_S_TOUCH + 1, s.touch[1]);
+    st_cg(st + ZB_S_FEET_DIST, s.feet_dist);
+    st_cg(st + ZB_S_EP_RETURN, s.ep_ret);
+    st_cg(st + ZB_S_EP_STEPS, bitsf(s.ep_steps));
+    st_cg(st + ZB_S_RNG_STEP, bitsf(s.rng_step));
+    st_cg(st + ZB_S_PREV_CONT, s.prev_cont[0]); st_cg(st + ZB_S_PREV_CONT + 1, s.prev_cont[1]);
+    st_cg(st + ZB_S_EPISODE, bitsf(s.episode));
+    st_cg(st + ZB_S_NAN, bitsf(s.nanflag));
   }
 }
 
@@ -2598,7 +2622,36 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 #endif
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
-  const int e = blockIdx.x * NTEAM + team;
+  /* Chunked step (a.nchunk > 1, one control step): the launch has npair * nchunk workgroups, each
+     running n_substeps / nchunk substeps of one pair of envs. A workgroup takes the next unit from
+     the counter sched[0] in chunk-major order (every pair's chunk 0, then every pair's chunk 1,
+     ...) and waits until the pair's previous chunk has published its state. Taking units in
+     order means a unit's predecessor was taken by a running workgroup, so every wait ends. The
+     slow pairs of the last round of waves then hold up the launch by a chunk, not by a whole
+     control step. The state passes between chunks through the state row exactly
+     as it passes between control steps, so the results do not depend on the chunking. */
+  const int K = a.nchunk;
+  const int npair = (a.n_envs + NTEAM - 1) / NTEAM;
+  int pair = blockIdx.x, ch = 0;
+  bool timed_out = false;
+  if (K > 1) {
+    uint32_t u = 0;
+    if (threadIdx.x == 0) u = addu_cg(a.sched, 1u);
+    u = __builtin_amdgcn_readfirstlane(u);
+    ch = (int)(u / (uint32_t)npair);
+    pair = (int)(u - (uint32_t)ch * (uint32_t)npair);
+    if (ch > 0) {
+      /* bounded: a wait that outlives ~2 s gives up and marks the env's iteration count */
+      for (uint32_t spins = 0; ldu_cg(a.sched + 2 + pair) < (uint32_t)ch; spins++) {
+        if (spins > (1u << 23)) {
+          timed_out = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+  }
+  const int e = pair * NTEAM + team;
   /* Both teams of a wave stay live to the end: forward()'s J'DJ runs on the
      matrix cores with operands from all 64 lanes (jdj_mfma). A team past the
      last env (odd n) runs as a ghost copy of env n-1 that stores nothing. */
@@ -2622,18 +2675,21 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   BodyK B;
   Rows r;
   Sensors& sen = c.L->sen;
-  int iters = 0;
+  int iters = (K > 1 && ch > 0) ? (int)ldu_cg((const uint32_t*)a.itpart + ee) : 0;
+  if (timed_out) iters -= 1 << 24;
   float rsum = 0.f;
   bool done = false;
   bool success = false; /* done by the time limit alone (ksim successful termination) */
   const int nsteps = a.nsteps;
   const bool rollout = nsteps > 1;
+  const int ss_end = (ch + 1) * cfg->n_substeps / K; /* this unit's substeps: [ss0, ss_end) */
+  bool partial = false;                               /* a chunk before the last one */
   for (int t = 0; t < nsteps; t++) {
     const bool last_t = t == nsteps - 1;
     if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + ee) * ZB_NJ + c.act];
-    if (cfg->flags & ZB_F_PUSH) push_event(c, s, ls, a.curriculum);
+    if (ch == 0 && (cfg->flags & ZB_F_PUSH)) push_event(c, s, ls, a.curriculum);
     float total = 0.f;
-    int ss = 0;
+    int ss = ch * cfg->n_substeps / K;
     bool resetting = false; /* this team re-enters forward() for its reset state */
     bool ghost = false;     /* the other team resets: a discarded forward() pass */
     bool done_reset = false;
@@ -2653,7 +2709,11 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       if (!resetting && !ghost) {
         integrate(c, s, ls);
         STAMP(S_INT);
-        if (++ss < cfg->n_substeps) continue;
+        if (++ss < cfg->n_substeps) {
+          if (ss < ss_end) continue;
+          partial = true; /* wave-uniform: no team resets before the last substep */
+          break;
+        }
         {
           bool bad = (c.l < NV) && !(isfinite(ls.q) && isfinite(ls.v));
           if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
@@ -2692,6 +2752,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
         ghost = true;
       }
     }
+    if (partial) break;
     s.rng_step += 1u;
     if (live && c.l == 0 && last_t) {
       if (a.reward) a.reward[e] = rollout ? rsum : total;
@@ -2699,8 +2760,29 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       if (a.success) a.success[e] = success ? 1 : 0;
     }
   }
-  if (live && a.iters && c.l == 0) a.iters[e] = iters;
+  if (partial) {
+    if (live && c.l == 0) stu_cg((uint32_t*)a.itpart + e, (uint32_t)iters);
+  } else if (live && a.iters && c.l == 0) {
+    a.iters[e] = iters;
+  }
   if (live) store_state(c, s, ls, st);
+  if (K > 1) {
+    /* publish: every store of this wave has completed before lane 0's flag store */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) {
+      if (partial) {
+        stu_cg(a.sched + 2 + pair, (uint32_t)(ch + 1));
+      } else {
+        /* last chunk: leave the pair's flag and (after the last pair's last chunk, when every
+           unit has been taken) both counters at zero for the next launch */
+        stu_cg(a.sched + 2 + pair, 0u);
+        if (addu_cg(a.sched + 1, 1u) == (uint32_t)npair - 1u) {
+          stu_cg(a.sched, 0u);
+          stu_cg(a.sched + 1, 0u);
+        }
+      }
+    }
+  }
 #ifdef ZB_STAMPS
   STAMP(S_STEPEND);
   if (live && a.dbg && c.l == 0)
@@ -2818,10 +2900,24 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   }
 }
 
+int step_resident_blocks(int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel, 64, 0) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  return per_cu * cus;
+}
+
 hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
-  dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  hipLaunchKernelGGL(step_kernel, grid, block, 0, s, a);
+  if (a.nchunk < 1 || (a.nchunk > 1 && (a.nsteps != 1 || !a.sched || !a.itpart))) return hipErrorInvalidValue;
+#ifdef ZB_STAMPS
+  StepArgs b = a;
+  b.nchunk = 1; /* the phase stamps are per env-step */
+#else
+  const StepArgs& b = a;
+#endif
+  dim3 grid((unsigned)((b.n_envs + NTEAM - 1) / NTEAM * b.nchunk)), block(64);
+  hipLaunchKernelGGL(step_kernel, grid, block, 0, s, b);
   return hipGetLastError();
 }
 hipError_t launch_reset(const StepArgs& a, hipStream_t s) {

@@ -61,7 +61,15 @@ struct StepArgs {
   int32_t* iters;           /* [n] */
   const uint8_t* reset_mask;
   float* dbg;               /* [n, ZB_DBG_STRIDE] */
+  /* chunked step (nsteps == 1, step_kernel): the n_substeps of a control step split into
+     nchunk work units per pair of envs, taken in chunk-major order from a counter */
+  int nchunk;               /* 1: one workgroup per pair runs all substeps */
+  uint32_t* sched;          /* [2 + npair]: units taken, pairs finished, per-pair chunks done */
+  int32_t* itpart;          /* [n] Newton iterations of the chunks so far */
 };
+
+/* workgroups of step_kernel resident on the device at once (occupancy x CUs) */
+int step_resident_blocks(int device);
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s);
 hipError_t launch_reset(const StepArgs& a, hipStream_t s);

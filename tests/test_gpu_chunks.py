@@ -1,0 +1,94 @@
+"""Chunked step (zb_step's substeps split into work units handed between workgroups inside one
+launch) against the unchunked step: bit for bit, with odd env counts (a ghost
+team), pushes, randomization and automatic resets. ZB_STEP_CHUNKS is read when an engine is
+created."""
+import os
+
+import pytest
+
+from zbot_amd import default_config
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def make(cm, cfg, n, k):
+    from zbot_amd.engine import HipEngine
+
+    old = os.environ.get("ZB_STEP_CHUNKS")
+    os.environ["ZB_STEP_CHUNKS"] = str(k)
+    try:
+        return HipEngine(cm, cfg, n, seed=3)
+    finally:
+        if old is None:
+            os.environ.pop("ZB_STEP_CHUNKS")
+        else:
+            os.environ["ZB_STEP_CHUNKS"] = old
+
+
+def same(torch, a, b):
+    if a.dtype == torch.float32:
+        return torch.equal(a.view(torch.int32), b.view(torch.int32))
+    return torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,k,push", [(37, 2, True), (37, 7, True), (64, 20, False), (1, 3, True)])
+def test_chunked_step_bit_exact(torch_gpu, cmodel, n, k, push):
+    torch = torch_gpu
+    cfg = default_config(push=push, randomize=push)
+    ref, chk = make(cmodel, cfg, n, 1), make(cmodel, cfg, n, k)
+    ref.reset()
+    chk.reset()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    bias = torch.tensor([cmodel.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    dones = 0
+    for t in range(60):
+        # large action noise: the robot falls, so automatic resets happen inside chunks' launches
+        act = bias + 0.4 * torch.randn(n, 20, device="cuda", generator=g)
+        o1 = {k_: v.clone() for k_, v in ref.step(act, curriculum=0.5).items()}
+        o2 = chk.step(act, curriculum=0.5)
+        for name in o1:
+            assert same(torch, o1[name], o2[name]), (t, name)
+        assert same(torch, ref.get_state(), chk.get_state()), t
+        assert torch.equal(ref.solver_iters(), chk.solver_iters()), t
+        dones += int(o1["done"].sum().item())
+    assert same(torch, ref.get_stats(), chk.get_stats())
+    assert same(torch, ref.get_rand(), chk.get_rand())
+    if push:
+        assert dones > 0  # the resets were exercised
+
+
+@pytest.mark.parametrize("n", [8192, 6144, 5121])
+def test_default_chunking(torch_gpu, cmodel, n):
+    """The library's own chunk choice (whole rounds of resident workgroups: unchunked, as at the
+    C2 bench size of 8192 envs; a partial last round: 2 or 4 chunks) against unchunked."""
+    torch = torch_gpu
+    from zbot_amd.engine import HipEngine
+
+    cfg = default_config()
+    old = os.environ.pop("ZB_STEP_CHUNKS", None)
+    try:
+        auto = HipEngine(cmodel, cfg, n, seed=3)
+    finally:
+        if old is not None:
+            os.environ["ZB_STEP_CHUNKS"] = old
+    ref = make(cmodel, cfg, n, 1)
+    auto.reset()
+    ref.reset()
+    bias = torch.tensor([cmodel.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    for t in range(6):
+        act = bias + 0.05 * torch.randn(n, 20, device="cuda")
+        o1 = {k_: v.clone() for k_, v in ref.step(act).items()}
+        o2 = auto.step(act)
+        for name in o1:
+            assert same(torch, o1[name], o2[name]), (t, name)
+    assert same(torch, ref.get_state(), auto.get_state())
