@@ -465,11 +465,15 @@ __device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); 
    workgroup visibility, first row of its hand-off table). */
 typedef __attribute__((address_space(1))) float gfloat_t;
 typedef __attribute__((address_space(1))) uint32_t guint_t;
+template <bool CG = true>
 __device__ __forceinline__ float ld_cg(const float* p) {
-  return __hip_atomic_load((gfloat_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (CG) return __hip_atomic_load((gfloat_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
 }
+template <bool CG = true>
 __device__ __forceinline__ void st_cg(float* p, float v) {
-  __hip_atomic_store((gfloat_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (CG) __hip_atomic_store((gfloat_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
 }
 __device__ __forceinline__ uint32_t ldu_cg(const uint32_t* p) {
   return __hip_atomic_load((guint_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2445,66 +2449,69 @@ __device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, 
 }
 
 /* ------------------------------ state I/O ---------------------------------- */
+/* CG: sc1 accesses (the chunked step hands state rows between workgroups); plain otherwise */
+template <bool CG = false>
 __device__ __forceinline__ void load_state(const Ctx& c, EnvS& s, LaneS& ls, const float* st) {
   const int l = c.l;
-  for (int k = 0; k < 3; k++) s.bp[k] = ld_cg(st + ZB_S_QPOS + k);
-  for (int k = 0; k < 4; k++) s.bq[k] = ld_cg(st + ZB_S_QPOS + 3 + k);
-  for (int k = 0; k < 4; k++) s.ema[k] = ld_cg(st + ZB_S_IMU_EMA + k);
-  s.lag = ld_cg(st + ZB_S_IMU_LAG);
-  s.air[0] = ld_cg(st + ZB_S_AIRTIME); s.air[1] = ld_cg(st + ZB_S_AIRTIME + 1);
-  s.push_timer = ld_cg(st + ZB_S_PUSH_TIMER);
-  s.touch[0] = ld_cg(st + ZB_S_TOUCH); s.touch[1] = ld_cg(st + ZB_S_TOUCH + 1);
-  s.feet_dist = ld_cg(st + ZB_S_FEET_DIST);
-  s.ep_ret = ld_cg(st + ZB_S_EP_RETURN);
-  s.ep_steps = fbits(ld_cg(st + ZB_S_EP_STEPS));
-  s.rng_step = fbits(ld_cg(st + ZB_S_RNG_STEP));
-  s.prev_cont[0] = ld_cg(st + ZB_S_PREV_CONT); s.prev_cont[1] = ld_cg(st + ZB_S_PREV_CONT + 1);
-  s.episode = fbits(ld_cg(st + ZB_S_EPISODE));
-  s.nanflag = fbits(ld_cg(st + ZB_S_NAN));
+  for (int k = 0; k < 3; k++) s.bp[k] = ld_cg<CG>(st + ZB_S_QPOS + k);
+  for (int k = 0; k < 4; k++) s.bq[k] = ld_cg<CG>(st + ZB_S_QPOS + 3 + k);
+  for (int k = 0; k < 4; k++) s.ema[k] = ld_cg<CG>(st + ZB_S_IMU_EMA + k);
+  s.lag = ld_cg<CG>(st + ZB_S_IMU_LAG);
+  s.air[0] = ld_cg<CG>(st + ZB_S_AIRTIME); s.air[1] = ld_cg<CG>(st + ZB_S_AIRTIME + 1);
+  s.push_timer = ld_cg<CG>(st + ZB_S_PUSH_TIMER);
+  s.touch[0] = ld_cg<CG>(st + ZB_S_TOUCH); s.touch[1] = ld_cg<CG>(st + ZB_S_TOUCH + 1);
+  s.feet_dist = ld_cg<CG>(st + ZB_S_FEET_DIST);
+  s.ep_ret = ld_cg<CG>(st + ZB_S_EP_RETURN);
+  s.ep_steps = fbits(ld_cg<CG>(st + ZB_S_EP_STEPS));
+  s.rng_step = fbits(ld_cg<CG>(st + ZB_S_RNG_STEP));
+  s.prev_cont[0] = ld_cg<CG>(st + ZB_S_PREV_CONT); s.prev_cont[1] = ld_cg<CG>(st + ZB_S_PREV_CONT + 1);
+  s.episode = fbits(ld_cg<CG>(st + ZB_S_EPISODE));
+  s.nanflag = fbits(ld_cg<CG>(st + ZB_S_NAN));
   ls.q = ls.v = ls.w = 0.f;
   ls.pp = ls.pv = ls.ptau = 0.f;
   if (l < NV) {
-    ls.v = ld_cg(st + ZB_S_QVEL + l);
-    ls.w = ld_cg(st + ZB_S_QACCW + l);
-    if (c.qadr >= 0) ls.q = ld_cg(st + ZB_S_QPOS + c.qadr);
+    ls.v = ld_cg<CG>(st + ZB_S_QVEL + l);
+    ls.w = ld_cg<CG>(st + ZB_S_QACCW + l);
+    if (c.qadr >= 0) ls.q = ld_cg<CG>(st + ZB_S_QPOS + c.qadr);
   }
   if (c.act >= 0) {
-    ls.pp = ld_cg(st + ZB_S_PLAN_POS + c.act);
-    ls.pv = ld_cg(st + ZB_S_PLAN_VEL + c.act);
-    ls.ptau = ld_cg(st + ZB_S_PLAN_TAU + c.act);
+    ls.pp = ld_cg<CG>(st + ZB_S_PLAN_POS + c.act);
+    ls.pv = ld_cg<CG>(st + ZB_S_PLAN_VEL + c.act);
+    ls.ptau = ld_cg<CG>(st + ZB_S_PLAN_TAU + c.act);
   }
   ls.ctrl = 0.f;
   ls.qacc = 0.f;
   ls.actforce = 0.f;
 }
 
+template <bool CG = false>
 __device__ __forceinline__ void store_state(const Ctx& c, const EnvS& s, const LaneS& ls, float* st) {
   const int l = c.l;
   if (l < NV) {
-    st_cg(st + ZB_S_QVEL + l, ls.v);
-    st_cg(st + ZB_S_QACCW + l, ls.w);
-    if (c.qadr >= 0) st_cg(st + ZB_S_QPOS + c.qadr, ls.q);
+    st_cg<CG>(st + ZB_S_QVEL + l, ls.v);
+    st_cg<CG>(st + ZB_S_QACCW + l, ls.w);
+    if (c.qadr >= 0) st_cg<CG>(st + ZB_S_QPOS + c.qadr, ls.q);
   }
   if (c.act >= 0) {
-    st_cg(st + ZB_S_PLAN_POS + c.act, ls.pp);
-    st_cg(st + ZB_S_PLAN_VEL + c.act, ls.pv);
-    st_cg(st + ZB_S_PLAN_TAU + c.act, ls.ptau);
+    st_cg<CG>(st + ZB_S_PLAN_POS + c.act, ls.pp);
+    st_cg<CG>(st + ZB_S_PLAN_VEL + c.act, ls.pv);
+    st_cg<CG>(st + ZB_S_PLAN_TAU + c.act, ls.ptau);
   }
   if (l == 0) {
-    for (int k = 0; k < 3; k++) st_cg(st + ZB_S_QPOS + k, s.bp[k]);
-    for (int k = 0; k < 4; k++) st_cg(st + ZB_S_QPOS + 3 + k, s.bq[k]);
-    for (int k = 0; k < 4; k++) st_cg(st + ZB_S_IMU_EMA + k, s.ema[k]);
-    st_cg(st + ZB_S_IMU_LAG, s.lag);
-    st_cg(st + ZB_S_AIRTIME, s.air[0]); st_cg(st + ZB_S_AIRTIME + 1, s.air[1]);
-    st_cg(st + ZB_S_PUSH_TIMER, s.push_timer);
-    st_cg(st + ZB_S_TOUCH, s.touch[0]); st_cg(st + ZB_S_TOUCH + 1, s.touch[1]);
-    st_cg(st + ZB_S_FEET_DIST, s.feet_dist);
-    st_cg(st + ZB_S_EP_RETURN, s.ep_ret);
-    st_cg(st + ZB_S_EP_STEPS, bitsf(s.ep_steps));
-    st_cg(st + ZB_S_RNG_STEP, bitsf(s.rng_step));
-    st_cg(st + ZB_S_PREV_CONT, s.prev_cont[0]); st_cg(st + ZB_S_PREV_CONT + 1, s.prev_cont[1]);
-    st_cg(st + ZB_S_EPISODE, bitsf(s.episode));
-    st_cg(st + ZB_S_NAN, bitsf(s.nanflag));
+    for (int k = 0; k < 3; k++) st_cg<CG>(st + ZB_S_QPOS + k, s.bp[k]);
+    for (int k = 0; k < 4; k++) st_cg<CG>(st + ZB_S_QPOS + 3 + k, s.bq[k]);
+    for (int k = 0; k < 4; k++) st_cg<CG>(st + ZB_S_IMU_EMA + k, s.ema[k]);
+    st_cg<CG>(st + ZB_S_IMU_LAG, s.lag);
+    st_cg<CG>(st + ZB_S_AIRTIME, s.air[0]); st_cg<CG>(st + ZB_S_AIRTIME + 1, s.air[1]);
+    st_cg<CG>(st + ZB_S_PUSH_TIMER, s.push_timer);
+    st_cg<CG>(st + ZB_S_TOUCH, s.touch[0]); st_cg<CG>(st + ZB_S_TOUCH + 1, s.touch[1]);
+    st_cg<CG>(st + ZB_S_FEET_DIST, s.feet_dist);
+    st_cg<CG>(st + ZB_S_EP_RETURN, s.ep_ret);
+    st_cg<CG>(st + ZB_S_EP_STEPS, bitsf(s.ep_steps));
+    st_cg<CG>(st + ZB_S_RNG_STEP, bitsf(s.rng_step));
+    st_cg<CG>(st + ZB_S_PREV_CONT, s.prev_cont[0]); st_cg<CG>(st + ZB_S_PREV_CONT + 1, s.prev_cont[1]);
+    st_cg<CG>(st + ZB_S_EPISODE, bitsf(s.episode));
+    st_cg<CG>(st + ZB_S_NAN, bitsf(s.nanflag));
   }
 }
 
@@ -2670,7 +2677,8 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
 #endif
   EnvS& s = c.L->s;
   LaneS ls;
-  load_state(c, s, ls, st);
+  if (K > 1) load_state<true>(c, s, ls, st);
+  else load_state<false>(c, s, ls, st);
   load_params(c, s, ls, rnd);
   BodyK B;
   Rows r;
@@ -2765,7 +2773,10 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   } else if (live && a.iters && c.l == 0) {
     a.iters[e] = iters;
   }
-  if (live) store_state(c, s, ls, st);
+  if (live) {
+    if (K > 1) store_state<true>(c, s, ls, st);
+    else store_state<false>(c, s, ls, st);
+  }
   if (K > 1) {
     /* publish: every store of this wave has completed before lane 0's flag store */
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
