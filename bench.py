@@ -1,6 +1,6 @@
 """Benchmark: env-steps/s of the fused HIP Z-Bot env.step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--config c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--config c1|c2|c3|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
 A "step" is one zb_step over all E envs of a GPU (20 physics substeps each,
@@ -25,14 +25,18 @@ sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
 METRIC = "env-steps/sec at N envs per GPU, 1/2/4/8 MI355X; % HBM roofline"
 
 CONFIGS = {
+    "c1": dict(envs=64, push=False, randomize=False,
+               name="C1: {n} envs, the reference's CPU-runnable case (its JAX-CPU path; here the GPU, with the "
+                    "CPU twin timed over the same 64 envs x 128 steps)"),
     "c2": dict(envs=8192, push=False, randomize=False, name="C2: {n} envs/GPU, flat-floor stand"),
     "c3": dict(envs=32768, push=True, randomize=False, name="C3: {n} envs/GPU, push-perturbation curriculum"),
     "c5": dict(envs=16384, push=False, randomize=True, name="C5: {n} envs/GPU, per-env domain randomization"),
 }
 
 
-def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int = 256) -> dict:
-    """Time the CPU oracle (fp32 C, OpenMP over envs) on a bounded sample."""
+def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int = 256, max_steps: int = 0) -> dict:
+    """Time the CPU oracle (fp32 C, OpenMP over envs) on a bounded sample (max_steps > 0: exactly
+    that many env-steps, the C1 rollout)."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     os.environ["OMP_NUM_THREADS"] = str(threads)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -48,7 +52,7 @@ def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int = 256) -> 
         env.step(acts[steps % 4])
         steps += 1
         el = time.perf_counter() - t0
-        if el >= budget_s:
+        if (max_steps and steps >= max_steps) or (not max_steps and el >= budget_s):
             break
     return {
         "value": n_envs * steps / el,
@@ -328,6 +332,13 @@ def main() -> None:
         if tj.get("envs") == n:
             traffic = tj.get("hbm_bytes_per_launch")
             flop_per_env_step = tj.get("issued_fp32_flop_per_env_step")
+    # algorithmic FLOPs per env-step, counted by the instrumented CPU twin on the C2 workload
+    # (scripts/count_flops.py)
+    algo_flop = None
+    fpath = os.path.join(ROOT, "profiles", "r02_flops_count.json")
+    if os.path.exists(fpath):
+        with open(fpath) as f:
+            algo_flop = json.load(f)["as_run"]["flops_per_env_step"]
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
     policy_leg = None if args.no_policy else bench_policy_in_loop(eng, n, 48, dev, rank)
@@ -373,14 +384,20 @@ def main() -> None:
                 "algorithmic_bytes_per_env_step": bpe,
                 "note": "the path is FP32-VALU/latency bound (DESIGN.md §Roofline); HBM fraction reported as required",
             },
-            "roofline_fp32": None if flop_per_env_step is None else {
+            "roofline_fp32": None if algo_flop is None else {
                 "bound": "fp32-valu",
-                "achieved": flop_per_env_step * n / (avg_ms * 1e-3) / 1e12,
+                "achieved": algo_flop * n / (avg_ms * 1e-3) / 1e12,
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": flop_per_env_step * n / (avg_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
-                "note": "issued VALU lane-FLOP (PMC SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32, FMA=2) per env-step "
-                        "x envs / kernel time; the binding resource of this latency/VALU-bound kernel",
+                "frac": algo_flop * n / (avg_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                "algorithmic_flop_per_env_step": algo_flop,
+                "issued_flop_per_env_step": flop_per_env_step,
+                "issued_achieved": None if flop_per_env_step is None else
+                flop_per_env_step * n / (avg_ms * 1e-3) / 1e12,
+                "note": "achieved = algorithmic FLOPs per env-step (counted by the instrumented CPU twin on the C2 "
+                        "workload, FMA=2, profiles/r02_flops_count.json) x envs / kernel time; issued = PMC "
+                        "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 lane-FLOP; the binding resource of this "
+                        "latency/VALU-bound kernel",
             },
             "episode_stats": {
                 "episodes_done": float(total_stats[2].item()),
@@ -394,7 +411,10 @@ def main() -> None:
         if pipe_leg is not None:
             out["rollout_pipeline"] = pipe_leg
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper())
+            if args.config == "c1":  # the whole C1 rollout on the CPU twin: 64 envs x 128 env-steps
+                out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, "C1", n_envs=n, max_steps=128)
+            else:
+                out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper())
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
