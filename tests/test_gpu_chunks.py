@@ -67,14 +67,15 @@ def test_chunked_step_bit_exact(torch_gpu, cmodel, n, k, push):
         assert dones > 0  # the resets were exercised
 
 
-@pytest.mark.parametrize("n", [8192, 6144, 5121])
-def test_default_chunking(torch_gpu, cmodel, n):
+@pytest.mark.parametrize("n,push,steps", [(8192, False, 6), (6144, False, 6), (5121, True, 40)])
+def test_default_chunking(torch_gpu, cmodel, n, push, steps):
     """The library's own chunk choice (whole rounds of resident workgroups: unchunked, as at the
-    C2 bench size of 8192 envs; a partial last round: 2 or 4 chunks) against unchunked."""
+    C2 bench size of 8192 envs; a partial last round: 2 or 4 chunks) against unchunked; at 5121
+    envs (4 chunks) with pushes, per-env randomization and resets."""
     torch = torch_gpu
     from zbot_amd.engine import HipEngine
 
-    cfg = default_config()
+    cfg = default_config(push=push, randomize=push)
     old = os.environ.pop("ZB_STEP_CHUNKS", None)
     try:
         auto = HipEngine(cmodel, cfg, n, seed=3)
@@ -85,10 +86,13 @@ def test_default_chunking(torch_gpu, cmodel, n):
     auto.reset()
     ref.reset()
     bias = torch.tensor([cmodel.cmodel.joint_bias[i] for i in range(20)], device="cuda")
-    for t in range(6):
-        act = bias + 0.05 * torch.randn(n, 20, device="cuda")
+    std = 0.4 if push else 0.05
+    for t in range(steps):
+        act = bias + std * torch.randn(n, 20, device="cuda")
         o1 = {k_: v.clone() for k_, v in ref.step(act).items()}
         o2 = auto.step(act)
         for name in o1:
             assert same(torch, o1[name], o2[name]), (t, name)
     assert same(torch, ref.get_state(), auto.get_state())
+    assert torch.equal(ref.solver_iters(), auto.solver_iters())
+    assert same(torch, ref.get_stats(), auto.get_stats())
