@@ -96,8 +96,8 @@ def _sgb(nvalu):
 
 VARIANTS = {
     "base": [],
-    # the product before the 16-B observation staging (r01_v18): ZB_POL_OLD or variants/zb_policy_v17.hip
-    "v17": "file:" + os.environ.get("ZB_POL_OLD", os.path.join(OUT, "zb_policy_v17.hip")),
+    # an earlier product kernel (e.g. `git show HEAD:.../zb_policy.hip`): ZB_POL_OLD or variants/zb_policy_prev.hip
+    "prev": "file:" + os.environ.get("ZB_POL_OLD", os.path.join(OUT, "zb_policy_prev.hip")),
     "base2": [],
 }
 
