@@ -926,7 +926,7 @@ typedef float v4f __attribute__((ext_vector_type(4)));
  * Wave-uniform: call with every lane active (the MFMA reads all 64 lanes). */
 __device__ __forceinline__ void root_schur_mfma() {
   static_assert(NV - NROOT == 20, "five K=4 chunks cover the 20 limb dofs");
-  const int l = threadIdx.x & 63;
+  const int l = vopq(threadIdx.x & 63); /* opaque: the store masks below are rebuilt per call */
   const int i = l & 15, kk = l >> 4;
   const int ic = i < RMAX ? i : 0;
   /* the accumulators start from the parked root block (its diagonal parked in L[r][r] too),
@@ -989,6 +989,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
      the pivot row afterwards) and applies its Schur update. Position 0 has no
      receivers inside the chain. */
   const int cps = vopq(c.cps);
+  const int clnv = vopq(c.cln); /* opaque per call: the level masks are recomputed, not kept live */
   const int chdv = ischain ? c.chd : 0;
   /* Alongside, each chain lane p builds row p of W = (I + Lt)^-1, the inverse of
      its chain's unit triangular block (Lt(p, k) = L(k, p), k deeper in the chain),
@@ -1002,7 +1003,7 @@ __device__ __forceinline__ float factor_ldl(const Ctx& c, float X[CAP], float Xd
   for (int k = 0; k < NLIMBLV; k++) wacc[k] = 0.f;
 #pragma unroll
   for (int q = NLIMBLV - 1; q >= 1; q--) {
-    const bool has = ischain && cps < q && q < c.cln;
+    const bool has = cps < q && q < clnv; /* clnv = 0 off the chains */
     /* lanes without a pivot at this level pull from any lane of a valid index and
        discard it (sc = 0 below; every pulled value is finite) */
     const int src = chdv + q;
