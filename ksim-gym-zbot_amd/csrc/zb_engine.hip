@@ -2669,8 +2669,12 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
-  float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
-  float* rnd = live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)ee * ZB_RAND_STRIDE : nullptr;
+  /* per-env row addresses are formed where they are used, from an opaque copy of the env
+     index: held across the substep loop they were 64-bit values spilled to scratch */
+  auto state_row = [&]() { return a.state + (size_t)vopq(ee) * ZB_STATE_STRIDE; };
+  auto rand_row = [&]() {
+    return live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)vopq(ee) * ZB_RAND_STRIDE : nullptr;
+  };
 #ifdef ZB_STAMPS
   if (c.l < NSTAMP) c.L->stamp[c.l] = 0;
   if (c.l == 0) c.L->stamp_last = __builtin_amdgcn_s_memtime();
@@ -2678,9 +2682,9 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
 #endif
   EnvS& s = c.L->s;
   LaneS ls;
-  if (K > 1) load_state<true>(c, s, ls, st);
-  else load_state<false>(c, s, ls, st);
-  load_params(c, s, ls, rnd);
+  if (K > 1) load_state<true>(c, s, ls, state_row());
+  else load_state<false>(c, s, ls, state_row());
+  load_params(c, s, ls, rand_row());
   BodyK B;
   Rows r;
   Sensors& sen = c.L->sen;
@@ -2695,7 +2699,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   bool partial = false;                               /* a chunk before the last one */
   for (int t = 0; t < nsteps; t++) {
     const bool last_t = t == nsteps - 1;
-    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + ee) * ZB_NJ + c.act];
+    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + vopq(ee)) * ZB_NJ + c.act];
     if (ch == 0 && (cfg->flags & ZB_F_PUSH)) push_event(c, s, ls, a.curriculum);
     float total = 0.f;
     int ss = ch * cfg->n_substeps / K;
@@ -2728,12 +2732,12 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
           if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
         }
         bool fail;
-        float* terms = (live && a.reward_terms && !rollout) ? a.reward_terms + (size_t)e * ZB_NUM_TERMS : nullptr;
+        float* terms = (live && a.reward_terms && !rollout) ? a.reward_terms + (size_t)vopq(e) * ZB_NUM_TERMS : nullptr;
         done = rewards(c, s, ls, B, a.curriculum, terms, total, fail);
         success = done && !fail;
         rsum += total;
         if (live && a.stats && c.l == 0) {
-          float* sp = a.stats + (size_t)e * ZB_NUM_STATS;
+          float* sp = a.stats + (size_t)vopq(e) * ZB_NUM_STATS;
           sp[ZB_ST_REWARD] += total;
           if (done) {
             sp[ZB_ST_RETURN] += s.ep_ret;
@@ -2748,14 +2752,15 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       c.cfg = opaque((CP)cfg);
       if (!ghost && (resetting || !done_reset)) {
         const bool out = live && last_t;
-        observe(c, s, ls, B, sen, (out && a.obs_actor) ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
-                (out && a.obs_critic) ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
-                (out && a.obs_extra) ? a.obs_extra + (size_t)e * ZB_OBS_EXTRA : nullptr);
+        const size_t eo = (size_t)vopq(e);
+        observe(c, s, ls, B, sen, (out && a.obs_actor) ? a.obs_actor + eo * ZB_OBS_ACTOR : nullptr,
+                (out && a.obs_critic) ? a.obs_critic + eo * ZB_OBS_CRITIC : nullptr,
+                (out && a.obs_extra) ? a.obs_extra + eo * ZB_OBS_EXTRA : nullptr);
       }
       if (resetting || ghost) break;
       if (__ballot(done_reset) == 0ull) break;
       if (done_reset) {
-        reset_prepare(c, s, ls, rnd);
+        reset_prepare(c, s, ls, rand_row());
         resetting = true;
       } else {
         ghost = true;
@@ -2764,19 +2769,20 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
     if (partial) break;
     s.rng_step += 1u;
     if (live && c.l == 0 && last_t) {
-      if (a.reward) a.reward[e] = rollout ? rsum : total;
-      if (a.done) a.done[e] = done ? 1 : 0;
-      if (a.success) a.success[e] = success ? 1 : 0;
+      const int eo = vopq(e);
+      if (a.reward) a.reward[eo] = rollout ? rsum : total;
+      if (a.done) a.done[eo] = done ? 1 : 0;
+      if (a.success) a.success[eo] = success ? 1 : 0;
     }
   }
   if (partial) {
-    if (live && c.l == 0) stu_cg((uint32_t*)a.itpart + e, (uint32_t)iters);
+    if (live && c.l == 0) stu_cg((uint32_t*)a.itpart + vopq(e), (uint32_t)iters);
   } else if (live && a.iters && c.l == 0) {
-    a.iters[e] = iters;
+    a.iters[vopq(e)] = iters;
   }
   if (live) {
-    if (K > 1) store_state<true>(c, s, ls, st);
-    else store_state<false>(c, s, ls, st);
+    if (K > 1) store_state<true>(c, s, ls, state_row());
+    else store_state<false>(c, s, ls, state_row());
   }
   if (K > 1) {
     /* publish: every store of this wave has completed before lane 0's flag store */
