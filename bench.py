@@ -128,10 +128,13 @@ def bench_ppo_inputs(n: int, T: int, reps: int, dev, world: int) -> dict:
     }
 
 
-def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int) -> dict:
+def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) -> dict:
     """The GRU actor in the rollout loop: per control step the actor samples
     every env's action from its observation on the f32 matrix cores, then zb_step advances the
-    envs (ksim sample_action -> env.step, train.py:1737-1763)."""
+    envs (ksim sample_action -> env.step, train.py:1737-1763). The actor's kernel time and
+    roofline come from one handle on the current stream (isolated launches); with `grouped` (an
+    EnvGroups) the leg's throughput is that of PolicyRollout running each group's actor -> zb_step
+    chain on its own stream."""
     import torch  # noqa: PLC0415
     from zbot_amd import policy as P  # noqa: PLC0415
     from zbot_amd.metrics import FP32_PEAK_TFLOPS  # noqa: PLC0415
@@ -162,15 +165,27 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int) -> dict:
     wall = time.perf_counter() - t0
     actor_ms = sum(a.elapsed_time(b) for a, b in evs) / steps
     tf = P.FLOP_ACTOR * n / (actor_ms * 1e-3) / 1e12
-    return {
+    out = {
         "workload": f"GRU actor (5 x GRU 128, mixture-of-Gaussians head) sampling the actions of {n} envs, then "
                     "zb_step, per control step",
         "env_steps_per_s_with_policy": n * steps / wall,
         "actor_kernel_ms": actor_ms,
         "roofline": {"bound": "mfma", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tf / FP32_PEAK_TFLOPS, "kernel": "zb::pol::policy_kernel<50, 300, true>",
-                     "flop_per_env_step": P.FLOP_ACTOR, "dtype": "f32 (v_mfma_f32_32x32x2_f32)"},
+                     "flop_per_env_step": P.FLOP_ACTOR, "dtype": "f32 (v_mfma_f32_16x16x4_f32)"},
     }
+    if grouped is not None:
+        ro = P.PolicyRollout(grouped, actor, seed=1)
+        ro.reset()
+        ro.run(2)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ro.run(steps)
+        torch.cuda.synchronize(dev)
+        out["env_steps_per_s_with_policy_one_stream"] = out["env_steps_per_s_with_policy"]
+        out["env_steps_per_s_with_policy"] = n * steps / (time.perf_counter() - t0)
+        out["workload"] += f"; {grouped.G} env groups, each running its actor -> zb_step chain on its own stream"
+    return out
 
 
 def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> dict:
@@ -232,6 +247,9 @@ def main() -> None:
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default: the config's)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--groups", type=int, default=2,
+                    help="env groups per GPU, each stepping on its own HIP stream (zbot_amd.EnvGroups, "
+                         "DESIGN.md §4f); 1 = one handle on the current stream")
     ap.add_argument("--cpu-baseline-sec", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
@@ -247,7 +265,7 @@ def main() -> None:
     from zbot_amd import compile_model, default_config  # noqa: PLC0415
     from zbot_amd import cstructs as cs  # noqa: PLC0415
     from zbot_amd.constants import JOINT_BIASES  # noqa: PLC0415
-    from zbot_amd.engine import HipEngine  # noqa: PLC0415
+    from zbot_amd.engine import EnvGroups, HipEngine  # noqa: PLC0415
     from zbot_amd.metrics import FP32_PEAK_TFLOPS, HBM_PEAK_GBS, bytes_per_env_step  # noqa: PLC0415
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -265,7 +283,11 @@ def main() -> None:
     n = args.envs or conf["envs"]
     cm = compile_model()
     cfg = default_config(push=conf["push"], randomize=conf["randomize"])
-    eng = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
+    G = max(1, args.groups)
+    if G > 1:
+        eng = EnvGroups(cm, cfg, n, groups=G, env_offset=rank * n, device=dev.index, seed=args.seed)
+    else:
+        eng = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
 
     # synthetic actions for the headline env-step leg, generated before timing (the
     # policy-in-the-loop leg below drives the same engine with the GRU actor instead)
@@ -298,12 +320,20 @@ def main() -> None:
     torch.cuda.synchronize(dev)
 
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # per-launch HIP events on the stream each launch runs on (one per group and step)
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+          for _ in range(args.steps)]
     t0 = time.perf_counter()
     for t in range(args.steps):
-        ev[t][0].record(stream)
-        eng.step(acts[(args.warmup + t) % acts.shape[0]], extras=False)
-        ev[t][1].record(stream)
+        a_t = acts[(args.warmup + t) % acts.shape[0]]
+        if G > 1:
+            eng.step(a_t, extras=False, events=ev[t])
+        else:
+            ev[t][0][0].record(stream)
+            eng.step(a_t, extras=False)
+            ev[t][0][1].record(stream)
+    if G > 1:
+        eng.join()
     total_stats = reduce_stats()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -315,9 +345,11 @@ def main() -> None:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     elapsed = float(el_t.item())
 
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = [a.elapsed_time(b) for evt in ev for a, b in evt]
     avg_ms = sum(kern_ms) / len(kern_ms)
     bpe = bytes_per_env_step(extras=False, terms=True)
+    # G launches of n/G envs run concurrently, one per group stream: the aggregate algorithmic
+    # rate is G x (bytes of n/G envs) / the average launch duration
     achieved = bpe * n / (avg_ms * 1e-3) / 1e9
     iters = eng.solver_iters().float().mean().item()
 
@@ -341,7 +373,11 @@ def main() -> None:
             algo_flop = json.load(f)["as_run"]["flops_per_env_step"]
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
-    policy_leg = None if args.no_policy else bench_policy_in_loop(eng, n, 48, dev, rank)
+    # the actor's roofline is timed on one handle on the current stream (isolated launches)
+    eng1 = eng if G == 1 else None
+    if G > 1 and not (args.no_policy and args.no_pipeline):
+        eng1 = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
+    policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, eng if G > 1 else None)
     pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(eng, n, 32, 2, dev, world)
 
     if rank == 0:
@@ -369,7 +405,9 @@ def main() -> None:
                 "substeps_per_step": cfg.n_substeps,
                 "solver": f"newton, {cfg.iterations} iters / {cfg.ls_iterations} ls iters",
                 "parallelism": f"env-shard x{world} (one process per GPU)" + (
-                    "" if world == 1 or args.dist_backend == "nccl" else f", {args.dist_backend} rehearsal"),
+                    "" if world == 1 or args.dist_backend == "nccl" else f", {args.dist_backend} rehearsal")
+                + (f"; {G} env groups of {n // G} per GPU, each zb_step-ing on its own HIP stream" if G > 1 else ""),
+                "groups_per_gpu": G,
                 "avg_solver_iters_per_env_step": iters,
             },
             "roofline": {
@@ -381,6 +419,8 @@ def main() -> None:
                 "traffic": traffic,
                 "kernel": "zb::step_kernel",
                 "kernel_avg_ms": avg_ms,
+                "concurrent_launches": G,
+                "envs_per_launch": n // G,
                 "algorithmic_bytes_per_env_step": bpe,
                 "note": "the path is FP32-VALU/latency bound (DESIGN.md §Roofline); HBM fraction reported as required",
             },

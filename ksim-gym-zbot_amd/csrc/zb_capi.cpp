@@ -318,7 +318,7 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMalloc(&h->itpart, n * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(h->itpart, 0, n * sizeof(int32_t));
   h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device));
-#ifdef ZB_STAMPS
+#if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
   if (e == hipSuccess) e = hipMalloc(&h->stamps, n * ZB_NSTAMP * sizeof(unsigned long long));
 #endif
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -681,7 +681,7 @@ int zb_policy_critic(ZbPolicy* p, const float* obs, int T, int n, float* carry, 
                     stream);
 }
 
-#ifdef ZB_STAMPS
+#if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
 int zb_get_stamps(ZbHandle* h, void* out_dev, void* stream) {
   if (!h || !h->stamps) return fail(ZB_EARG, "no stamps");
   return copy_rows(h, out_dev, h->stamps, (size_t)h->n * ZB_NSTAMP * sizeof(unsigned long long), stream);

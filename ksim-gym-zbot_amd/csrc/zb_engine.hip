@@ -2660,6 +2660,10 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
     }
   }
   const int e = pair * NTEAM + team;
+#ifdef ZB_WAVETIME
+  /* diagnostic build: the pair's start / end on the 100 MHz constant clock and its CU */
+  const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   /* Both teams of a wave stay live to the end: forward()'s J'DJ runs on the
      matrix cores with operands from all 64 lanes (jdj_mfma). A team past the
      last env (odd n) runs as a ghost copy of env n-1 that stores nothing. */
@@ -2801,6 +2805,15 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       }
     }
   }
+#ifdef ZB_WAVETIME
+  if (threadIdx.x == 0 && a.dbg) {
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(a.dbg) + ((size_t)ch * npair + pair) * 4;
+    w[0] = wt0;
+    w[1] = __builtin_amdgcn_s_memrealtime();
+    w[2] = (unsigned long long)__smid();
+    w[3] = (unsigned long long)iters;
+  }
+#endif
 #ifdef ZB_STAMPS
   STAMP(S_STEPEND);
   if (live && a.dbg && c.l == 0)

@@ -231,3 +231,148 @@ class HipEngine:
         out = self.torch.zeros(self.n, DBG_STRIDE, dtype=self.torch.float32, device=self.device)
         _check(self.L.zb_debug_forward(self.h, _ptr(s), _ptr(c), _ptr(out), self._stream()))
         return out
+
+
+def group_bounds(n_envs: int, groups: int) -> list[tuple[int, int]]:
+    """Consecutive env ranges of EnvGroups: cut on even env indices (whole pairs of envs, one wave
+    each) where that leaves every group non-empty, else evenly."""
+    if groups < 1 or n_envs < groups:
+        raise ZbError(f"need 1 <= groups <= n_envs, got groups={groups}, n_envs={n_envs}")
+    cuts = [0] + [min(n_envs, 2 * ((n_envs * g // groups + 1) // 2)) for g in range(1, groups)] + [n_envs]
+    if any(b <= a for a, b in zip(cuts[:-1], cuts[1:])):
+        cuts = [n_envs * g // groups for g in range(groups + 1)]
+    return list(zip(cuts[:-1], cuts[1:]))
+
+
+class EnvGroups:
+    """N envs on one GPU as G engine handles over consecutive env ranges, each stepping on its own
+    HIP stream.
+
+    A zb_step launch ends in a drain: its last round of waves finishes ragged, and the next launch
+    cannot start before the slowest pair of envs is done. With G groups, step t of group g waits
+    only on step t - 1 of group g, so the other group's waves fill the slots the drain frees. Every
+    group keeps the global env ids of its range (env_offset), so each env's RNG streams, and with
+    them the results, are bit-identical to one handle over all N envs, as for the shards of a
+    multi-GPU run.
+
+    The outputs are views into full [N, ...] buffers. step() returns them pending: work on the
+    caller's stream that reads them must come after join(), which makes the current stream wait
+    for every group's last launch. Calls that read or write engine state (reset, get_state, ...)
+    join first and run on the current stream; the next step() orders every group after them."""
+
+    OUTPUTS = ("obs_actor", "obs_critic", "obs_extra", "reward_terms", "reward", "done", "success")
+
+    def __init__(self, model, cfg: cs.ZbEnvConfig, n_envs: int, groups: int = 2, env_offset: int = 0,
+                 device: int = 0, seed: int = 0, lib_path: str | None = None):
+        import torch  # noqa: PLC0415
+
+        self.torch = torch
+        self.n = n_envs
+        self.env_offset = env_offset
+        self.G = groups
+        self.bounds = group_bounds(n_envs, groups)
+        self.engines = [HipEngine(model, cfg, b - a, env_offset=env_offset + a, device=device, seed=seed,
+                                  lib_path=lib_path) for a, b in self.bounds]
+        e0 = self.engines[0]
+        self.L, self.device, self.cfg, self.seed = e0.L, e0.device, cfg, seed
+        for name in self.OUTPUTS:
+            t = getattr(e0, name)
+            full = torch.zeros((n_envs,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
+            setattr(self, name, full)
+            for e, (a, b) in zip(self.engines, self.bounds):
+                setattr(e, name, full[a:b])
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(groups)]
+        self._tail = [None] * groups  # each group's last enqueued event
+
+    def groups(self):
+        """(engine, stream, env range) of every group."""
+        return list(zip(self.engines, self.streams, self.bounds))
+
+    def outputs(self) -> dict:
+        return {k: getattr(self, k) for k in self.OUTPUTS}
+
+    def fork(self) -> None:
+        """Order every group stream after the work enqueued so far on the current stream."""
+        ev = self.torch.cuda.Event()
+        ev.record(self.torch.cuda.current_stream(self.device))
+        for s in self.streams:
+            s.wait_event(ev)
+
+    def mark(self, g: int) -> None:
+        """Record group g's tail (after the work just enqueued on its stream)."""
+        ev = self.torch.cuda.Event()
+        ev.record(self.streams[g])
+        self._tail[g] = ev
+
+    def join(self) -> None:
+        """Make the current stream wait for every group's enqueued work."""
+        cur = self.torch.cuda.current_stream(self.device)
+        for ev in self._tail:
+            if ev is not None:
+                cur.wait_event(ev)
+
+    def step(self, action, curriculum: float = 1.0, extras: bool = True, terms: bool = True, events=None) -> dict:
+        """events: optional per-group (start, end) torch.cuda.Event pairs recorded around each group's
+        launch on its stream (bench.py's per-launch timing)."""
+        a = action
+        if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if tuple(a.shape) != (self.n, cs.NJ):
+            raise ZbError(f"action must be [{self.n}, {cs.NJ}], got {tuple(a.shape)}")
+        self.fork()
+        for g, (e, s, (lo, hi)) in enumerate(self.groups()):
+            with self.torch.cuda.stream(s):
+                if events is not None:
+                    events[g][0].record(s)
+                e.step(a[lo:hi], curriculum=curriculum, extras=extras, terms=terms)
+                if events is not None:
+                    events[g][1].record(s)
+            self.mark(g)
+        return self.outputs()
+
+    def rollout(self, actions, curriculum: float = 1.0, reward_sum=None) -> dict:
+        a = actions.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if a.dim() != 3 or tuple(a.shape[1:]) != (self.n, cs.NJ):
+            raise ZbError("actions must be [T, n_envs, 20] with T >= 1")
+        if reward_sum is not None:
+            self.engines[0]._check_out(reward_sum, "reward_sum", (self.n,), self.torch.float32)
+        self.fork()
+        for g, (e, s, (lo, hi)) in enumerate(self.groups()):
+            with self.torch.cuda.stream(s):
+                e.rollout(a[:, lo:hi].contiguous(), curriculum=curriculum,
+                          reward_sum=None if reward_sum is None else reward_sum[lo:hi])
+            self.mark(g)
+        return self.outputs()
+
+    def _each(self, fn):
+        self.join()
+        return [fn(e, lo, hi) for e, (lo, hi) in zip(self.engines, self.bounds)]
+
+    def reset(self, mask=None, extras: bool = True) -> dict:
+        m = None if mask is None else mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
+        self._each(lambda e, lo, hi: e.reset(None if m is None else m[lo:hi], extras=extras))
+        return self.outputs()
+
+    def get_state(self):
+        return self.torch.cat(self._each(lambda e, lo, hi: e.get_state()))
+
+    def set_state(self, state) -> None:
+        s = state.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if tuple(s.shape) != (self.n, cs.STATE_STRIDE):
+            raise ZbError("state must be [n_envs, ZB_STATE_STRIDE]")
+        self._each(lambda e, lo, hi: e.set_state(s[lo:hi]))
+
+    def get_rand(self):
+        return self.torch.cat(self._each(lambda e, lo, hi: e.get_rand()))
+
+    def set_rand(self, rand) -> None:
+        r = rand.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if tuple(r.shape) != (self.n, cs.RAND_STRIDE):
+            raise ZbError(f"rand must be [n_envs, ZB_RAND_STRIDE] = [{self.n}, {cs.RAND_STRIDE}], got {tuple(r.shape)}")
+        self._each(lambda e, lo, hi: e.set_rand(r[lo:hi]))
+
+    def get_stats(self, clear: bool = False):
+        return self.torch.cat(self._each(lambda e, lo, hi: e.get_stats(clear=clear)))
+
+    def solver_iters(self):
+        return self.torch.cat(self._each(lambda e, lo, hi: e.solver_iters()))

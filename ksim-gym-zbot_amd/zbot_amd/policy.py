@@ -19,6 +19,7 @@ buffers on the GPU.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import numpy as np
@@ -185,7 +186,9 @@ class PolicyRollout:
     """ksim's rollout loop with the GRU actor in it (sample_action -> env.step, train.py:1737-1763),
     entirely on the GPU: per control step one actor launch and one zb_step launch, whose rows go
     straight into [T, n] buffers. Episode ends reset the actor carry (get_ppo_variables,
-    train.py:1719-1723)."""
+    train.py:1719-1723). `engine` is a HipEngine, or an EnvGroups whose groups each run their own
+    actor -> zb_step chain on their own stream (bit-identical: the actor's RNG is keyed by global
+    env id)."""
 
     def __init__(self, engine, actor: GruPolicy, seed: int = 0, curriculum: float = 1.0):
         if actor.kind != ACTOR:
@@ -232,15 +235,29 @@ class PolicyRollout:
         done = torch.zeros(T, n, dtype=torch.uint8, device=dev)
         success = torch.zeros(T, n, dtype=torch.uint8, device=dev)
         L = self.eng.L
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        # an EnvGroups engine runs each group's actor -> zb_step chain on the group's own stream
+        # (DESIGN.md §4f); a HipEngine is one group on the current stream
+        grouped = hasattr(self.eng, "groups")
+        parts = self.eng.groups() if grouped else [(self.eng, None, (0, n))]
+        if grouped:
+            self.eng.fork()
         for t in range(T):
-            self.actor.actor(obs[t], self.carry, reset=(done[t - 1] if t > 0 else self.done), mode=SAMPLE,
-                             seed=self.seed, env_offset=self.eng.env_offset, step=self.step_count, actions=acts[t],
-                             log_prob=lp[t])
-            _check(L.zb_step(self.eng.h, acts[t].data_ptr(), obs[t + 1].data_ptr(),
-                             crit[t + 1].data_ptr() if record_critic else None, None, None, rew[t].data_ptr(),
-                             done[t].data_ptr(), success[t].data_ptr(), float(self.curriculum), stream))
+            for g, (e, s, (lo, hi)) in enumerate(parts):
+                with (torch.cuda.stream(s) if s is not None else contextlib.nullcontext()):
+                    stream = torch.cuda.current_stream(dev).cuda_stream
+                    r = done[t - 1][lo:hi] if t > 0 else (None if self.done is None else self.done[lo:hi])
+                    self.actor.actor(obs[t][lo:hi], self.carry[lo:hi], reset=r, mode=SAMPLE, seed=self.seed,
+                                     env_offset=e.env_offset, step=self.step_count, actions=acts[t][lo:hi],
+                                     log_prob=lp[t][lo:hi])
+                    _check(L.zb_step(e.h, acts[t][lo:hi].data_ptr(), obs[t + 1][lo:hi].data_ptr(),
+                                     crit[t + 1][lo:hi].data_ptr() if record_critic else None, None, None,
+                                     rew[t][lo:hi].data_ptr(), done[t][lo:hi].data_ptr(),
+                                     success[t][lo:hi].data_ptr(), float(self.curriculum), stream))
+                if grouped:
+                    self.eng.mark(g)
             self.step_count += 1
+        if grouped:
+            self.eng.join()
         self.obs = obs[T].clone()
         self.obs_c = crit[T].clone() if record_critic else None
         self.done = done[T - 1].clone()

@@ -1,0 +1,116 @@
+"""EnvGroups: N envs as G handles on G HIP streams give bit-identical results to one
+handle over all N envs — every output of every step, the engine state, the open-loop rollout, and
+PolicyRollout's actor-in-the-loop trajectories — with pushes, per-env randomization and automatic
+resets on, at env counts that leave odd groups and ghost teams.
+"""
+
+import numpy as np
+import pytest
+
+from zbot_amd import default_config
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _actions(torch, cm, T, n, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    bias = torch.tensor([cm.cmodel.joint_bias[a] for a in range(20)], device="cuda")
+    return bias + 0.3 * torch.randn(T, n, 20, device="cuda", generator=g)
+
+
+def _bits(t):
+    return t.contiguous().view(-1).cpu().numpy().view(np.uint8)
+
+
+@pytest.mark.parametrize("n,G", [(517, 2), (300, 3), (64, 4)])
+def test_grouped_steps_bit_identical(torch_gpu, cmodel, n, G):
+    torch = torch_gpu
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    cfg = default_config(push=True, randomize=True, max_episode_sec=0.3)
+    one = HipEngine(cmodel, cfg, n, seed=7)
+    grp = EnvGroups(cmodel, cfg, n, groups=G, seed=7)
+    assert [b - a for a, b in grp.bounds] and grp.bounds[-1][1] == n
+    one.reset()
+    grp.reset()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_bits(grp.get_rand()), _bits(one.get_rand()))
+    acts = _actions(torch, cmodel, 24, n, 3)
+    ends = 0
+    for t in range(24):
+        o1 = one.step(acts[t])
+        o2 = grp.step(acts[t])
+        grp.join()
+        torch.cuda.synchronize()
+        for k in ("obs_actor", "obs_critic", "obs_extra", "reward_terms", "reward", "done", "success"):
+            np.testing.assert_array_equal(_bits(o2[k]), _bits(o1[k]), err_msg=f"{k} at step {t}")
+        ends += int(o1["done"].sum())
+    np.testing.assert_array_equal(_bits(grp.get_state()), _bits(one.get_state()))
+    np.testing.assert_array_equal(grp.solver_iters().cpu().numpy(), one.solver_iters().cpu().numpy())
+    np.testing.assert_array_equal(_bits(grp.get_stats()), _bits(one.get_stats()))
+    assert ends > 0  # automatic resets were exercised
+
+
+def test_grouped_rollout_and_state_io(torch_gpu, cmodel):
+    torch = torch_gpu
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    cfg = default_config(push=True)
+    n = 130
+    one = HipEngine(cmodel, cfg, n, seed=4)
+    grp = EnvGroups(cmodel, cfg, n, groups=2, seed=4)
+    one.reset()
+    grp.reset()
+    acts = _actions(torch, cmodel, 6, n, 5)
+    r1 = torch.empty(n, device="cuda")
+    r2 = torch.empty(n, device="cuda")
+    o1 = one.rollout(acts, reward_sum=r1)
+    o2 = grp.rollout(acts, reward_sum=r2)
+    grp.join()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_bits(r2), _bits(r1))
+    np.testing.assert_array_equal(_bits(o2["obs_actor"]), _bits(o1["obs_actor"]))
+    np.testing.assert_array_equal(_bits(grp.get_state()), _bits(one.get_state()))
+    # set_state through the groups, then one more step each
+    st = one.get_state()
+    st[:, 2] += 0.01
+    one.set_state(st)
+    grp.set_state(st)
+    o1 = one.step(acts[0])
+    o2 = grp.step(acts[0])
+    grp.join()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_bits(o2["obs_critic"]), _bits(o1["obs_critic"]))
+
+
+def test_grouped_policy_rollout_bit_identical(torch_gpu, cmodel):
+    torch = torch_gpu
+    from zbot_amd import policy as P
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    cfg = default_config(max_episode_sec=0.2)
+    n, T = 200, 14
+    actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0))
+    outs = []
+    for eng in (HipEngine(cmodel, cfg, n, seed=9), EnvGroups(cmodel, cfg, n, groups=2, seed=9)):
+        ro = P.PolicyRollout(eng, actor, seed=2)
+        ro.reset()
+        a = ro.run(T, record_critic=True)
+        b = ro.run(3, record_critic=True)  # continues across run() calls: carry, done, step counter
+        torch.cuda.synchronize()
+        outs.append((a, b, ro.carry.clone()))
+    (a1, b1, c1), (a2, b2, c2) = outs
+    for k in a1:
+        np.testing.assert_array_equal(_bits(a2[k]), _bits(a1[k]), err_msg=k)
+        np.testing.assert_array_equal(_bits(b2[k]), _bits(b1[k]), err_msg=k)
+    np.testing.assert_array_equal(_bits(c2), _bits(c1))
+    assert int(a1["done"].sum()) > 0
