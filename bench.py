@@ -131,10 +131,10 @@ def bench_ppo_inputs(n: int, T: int, reps: int, dev, world: int) -> dict:
 def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) -> dict:
     """The GRU actor in the rollout loop: per control step the actor samples
     every env's action from its observation on the f32 matrix cores, then zb_step advances the
-    envs (ksim sample_action -> env.step, train.py:1737-1763). The actor's kernel time and
-    roofline come from one handle on the current stream (isolated launches); with `grouped` (an
-    EnvGroups) the leg's throughput is that of PolicyRollout running each group's actor -> zb_step
-    chain on its own stream."""
+    envs (ksim sample_action -> env.step, train.py:1737-1763), one handle on the current stream.
+    With `grouped` (an EnvGroups) the leg also times PolicyRollout running each group's actor ->
+    zb_step chain on its own stream: slower, because an actor workgroup needs most of a CU's LDS and
+    waits for the other group's step waves to leave it."""
     import torch  # noqa: PLC0415
     from zbot_amd import policy as P  # noqa: PLC0415
     from zbot_amd.metrics import FP32_PEAK_TFLOPS  # noqa: PLC0415
@@ -182,9 +182,7 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
         t0 = time.perf_counter()
         ro.run(steps)
         torch.cuda.synchronize(dev)
-        out["env_steps_per_s_with_policy_one_stream"] = out["env_steps_per_s_with_policy"]
-        out["env_steps_per_s_with_policy"] = n * steps / (time.perf_counter() - t0)
-        out["workload"] += f"; {grouped.G} env groups, each running its actor -> zb_step chain on its own stream"
+        out[f"env_steps_per_s_with_policy_{grouped.G}_groups"] = n * steps / (time.perf_counter() - t0)
     return out
 
 
@@ -373,12 +371,13 @@ def main() -> None:
             algo_flop = json.load(f)["as_run"]["flops_per_env_step"]
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
-    # the actor's roofline is timed on one handle on the current stream (isolated launches)
+    # the actor-in-the-loop legs run one handle on the current stream: env groups do not pay
+    # there
     eng1 = eng if G == 1 else None
     if G > 1 and not (args.no_policy and args.no_pipeline):
         eng1 = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
     policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, eng if G > 1 else None)
-    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(eng, n, 32, 2, dev, world)
+    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(eng1, n, 32, 2, dev, world)
 
     if rank == 0:
         value = world * n * args.steps / elapsed
