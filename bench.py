@@ -420,6 +420,9 @@ def main() -> None:
                 "kernel_avg_ms": avg_ms,
                 "concurrent_launches": G,
                 "envs_per_launch": n // G,
+                "traffic_note": "HBM bytes per n env-steps (one launch over all n envs in a separate rocprofv3 --pmc pass, "
+                                "FETCH_SIZE x2 + WRITE_SIZE); achieved = algorithmic bytes of the G concurrent launches / "
+                                "their average duration",
                 "algorithmic_bytes_per_env_step": bpe,
                 "note": "the path is FP32-VALU/latency bound (DESIGN.md §Roofline); HBM fraction reported as required",
             },
