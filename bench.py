@@ -131,10 +131,11 @@ def bench_ppo_inputs(n: int, T: int, reps: int, dev, world: int) -> dict:
 def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) -> dict:
     """The GRU actor in the rollout loop: per control step the actor samples
     every env's action from its observation on the f32 matrix cores, then zb_step advances the
-    envs (ksim sample_action -> env.step, train.py:1737-1763), one handle on the current stream.
-    With `grouped` (an EnvGroups) the leg also times PolicyRollout running each group's actor ->
-    zb_step chain on its own stream: slower, because an actor workgroup needs most of a CU's LDS and
-    waits for the other group's step waves to leave it."""
+    envs (ksim sample_action -> env.step, train.py:1737-1763). The actor's kernel time and roofline
+    come from one handle on the current stream with the 8-wave actor (isolated launches). With
+    `grouped` (an EnvGroups on high-priority streams) the leg's throughput is PolicyRollout running
+    each group's actor -> zb_step chain on its own stream with the one-wave actor layout, whose
+    workgroups fit the slots the other groups' step launches free."""
     import torch  # noqa: PLC0415
     from zbot_amd import policy as P  # noqa: PLC0415
     from zbot_amd.metrics import FP32_PEAK_TFLOPS  # noqa: PLC0415
@@ -175,6 +176,7 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
                      "flop_per_env_step": P.FLOP_ACTOR, "dtype": "f32 (v_mfma_f32_16x16x4_f32)"},
     }
     if grouped is not None:
+        actor.set_layout(P.LAYOUT_WAVE)
         ro = P.PolicyRollout(grouped, actor, seed=1)
         ro.reset()
         ro.run(2)
@@ -182,7 +184,10 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
         t0 = time.perf_counter()
         ro.run(steps)
         torch.cuda.synchronize(dev)
-        out[f"env_steps_per_s_with_policy_{grouped.G}_groups"] = n * steps / (time.perf_counter() - t0)
+        out["env_steps_per_s_with_policy_one_stream"] = out["env_steps_per_s_with_policy"]
+        out["env_steps_per_s_with_policy"] = n * steps / (time.perf_counter() - t0)
+        out["workload"] += (f"; {grouped.G} env groups on high-priority streams, each running its actor (one-wave "
+                            "layout) -> zb_step chain")
     return out
 
 
@@ -198,7 +203,8 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
     from zbot_amd import policy as P  # noqa: PLC0415
     from zbot_amd.ppo import compute_ppo_inputs  # noqa: PLC0415
 
-    actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), device=dev.index)
+    actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), device=dev.index,
+                        layout=P.LAYOUT_WAVE if hasattr(eng, "groups") else P.LAYOUT_BLOCK)
     critic = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=1), device=dev.index)
     ro = P.PolicyRollout(eng, actor, seed=3)
     ro.reset()
@@ -230,7 +236,9 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
     assert bool(torch.isfinite(res.advantages_t).all())
     return {
         "workload": f"per GPU: {T}-step rollout of {n} envs with the GRU actor sampling every action, the GRU "
-                    "critic over the rollout, GAE + value targets + advantage normalization (moments over RCCL)",
+                    "critic over the rollout, GAE + value targets + advantage normalization (moments over RCCL)"
+                    + (f"; the rollout over {eng.G} env groups on high-priority streams (one-wave actor)"
+                       if hasattr(eng, "groups") else ""),
         "env_steps_per_s": world * n * T * reps / wall,
         "ms_per_rollout": 1e3 * wall / reps,
         "rollout_steps": T,
@@ -248,6 +256,9 @@ def main() -> None:
     ap.add_argument("--groups", type=int, default=2,
                     help="env groups per GPU, each stepping on its own HIP stream (zbot_amd.EnvGroups, "
                          "DESIGN.md §4f); 1 = one handle on the current stream")
+    ap.add_argument("--policy-groups", type=int, default=3,
+                    help="env groups of the actor-in-the-loop legs (high-priority streams, one-wave actor "
+                         "layout; DESIGN.md §4f); 1 = one handle, 8-wave actor, current stream")
     ap.add_argument("--cpu-baseline-sec", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
@@ -371,13 +382,18 @@ def main() -> None:
             algo_flop = json.load(f)["as_run"]["flops_per_env_step"]
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
-    # the actor-in-the-loop legs run one handle on the current stream: env groups do not pay
-    # there
+    # the actor-in-the-loop legs: one handle on the current stream for the actor's kernel time, and
+    # args.policy_groups env groups on high-priority streams with the one-wave actor
     eng1 = eng if G == 1 else None
-    if G > 1 and not (args.no_policy and args.no_pipeline):
-        eng1 = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
-    policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, eng if G > 1 else None)
-    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(eng1, n, 32, 2, dev, world)
+    engp = None
+    if not (args.no_policy and args.no_pipeline):
+        if G > 1:
+            eng1 = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
+        if args.policy_groups > 1:
+            engp = EnvGroups(cm, cfg, n, groups=args.policy_groups, env_offset=rank * n, device=dev.index,
+                             seed=args.seed, priority=-1)
+    policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, engp)
+    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(engp or eng1, n, 32, 2, dev, world)
 
     if rank == 0:
         value = world * n * args.steps / elapsed

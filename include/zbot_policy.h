@@ -70,6 +70,18 @@ size_t zb_policy_param_count(int kind);
 int zb_policy_create(int kind, const float* params, size_t n_params, int device, ZbPolicy** out);
 int zb_policy_destroy(ZbPolicy* p);
 
+/* Kernel layout of the handle's launches (bit-identical results either way):
+ *   ZB_POL_LAYOUT_BLOCK  32 envs x 8 waves a workgroup, 89 KB (actor) / 116 KB (critic) of LDS:
+ *                        the fastest alone on the GPU;
+ *   ZB_POL_LAYOUT_WAVE   16 envs on one wave, <= 20 KB of LDS: a workgroup fits the slot of one
+ *                        zb_step wave, so its launches fill the slots a concurrent step launch
+ *                        frees (env groups on their own streams).
+ * The default is ZB_POL_LAYOUT_BLOCK, or the environment's ZB_POLICY_LAYOUT=wave|block at
+ * zb_policy_create. */
+#define ZB_POL_LAYOUT_BLOCK 0
+#define ZB_POL_LAYOUT_WAVE 1
+int zb_policy_set_layout(ZbPolicy* p, int layout);
+
 /*
  * Actor over T consecutive steps of n envs (T = 1 in the rollout loop).
  *   mode ZB_POL_SAMPLE / ZB_POL_MODE: actions written; ZB_POL_EVAL: read.

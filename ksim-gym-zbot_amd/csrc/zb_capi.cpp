@@ -541,6 +541,7 @@ struct ZbPolicy {
   int device;
   float* wpack;
   float* bias;
+  int layout; /* ZB_POL_LAYOUT_* */
 };
 
 static int pol_in(int kind) { return kind == ZB_POL_ACTOR ? ZB_POL_ACTOR_IN : ZB_POL_CRITIC_IN; }
@@ -603,6 +604,10 @@ int zb_policy_create(int kind, const float* params, size_t n_params, int device,
   HIPCHK(hipSetDevice(device));
   ZbPolicy* h = new ZbPolicy();
   h->kind = kind;
+  {
+    const char* lay = getenv("ZB_POLICY_LAYOUT");
+    h->layout = (lay && lay[0] == 'w') ? ZB_POL_LAYOUT_WAVE : ZB_POL_LAYOUT_BLOCK;
+  }
   h->device = device;
   h->wpack = nullptr;
   h->bias = nullptr;
@@ -663,9 +668,17 @@ static int policy_run(ZbPolicy* h, int kind, const float* obs, int T, int n, flo
     a.value = value ? value + (size_t)t * n : nullptr;
     a.wpack = h->wpack;
     a.bias = h->bias;
+    a.layout = h->layout;
     hipError_t e = zb::launch_policy(kind, a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ZB_ELAUNCH, "policy launch: %s", hipGetErrorString(e));
   }
+  return ZB_OK;
+}
+
+int zb_policy_set_layout(ZbPolicy* p, int layout) {
+  if (!p) return fail(ZB_EARG, "null policy handle");
+  if (layout != ZB_POL_LAYOUT_BLOCK && layout != ZB_POL_LAYOUT_WAVE) return fail(ZB_EARG, "unknown layout %d", layout);
+  p->layout = layout;
   return ZB_OK;
 }
 

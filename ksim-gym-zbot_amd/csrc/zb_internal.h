@@ -108,6 +108,7 @@ struct PolicyArgs {
   float* value;           /* [n] (critic) */
   const float* wpack;     /* fragment-packed weights */
   const float* bias;      /* biases and head constants */
+  int layout;             /* ZB_POL_LAYOUT_BLOCK / ZB_POL_LAYOUT_WAVE */
 };
 hipError_t launch_policy(int kind, const PolicyArgs& a, hipStream_t s);
 

@@ -324,10 +324,221 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   }
 }
 
+/* ---------------------------------------------------------------------------------------------
+ * One-wave layout (policy_wave_kernel): a workgroup is ONE wave over 16 envs (one row tile) that
+ * runs every unit tile of every layer itself. It is sized to take the slot of one step-kernel wave
+ * (<= 256 VGPRs, <= 20 KB of LDS), so its waves can start in the slots a step launch frees as it
+ * drains instead of waiting for whole CUs. The A operands of a layer (its input
+ * and the carry) are held in registers in the MFMA A layout, 32 values a lane for K = 128; the
+ * layer's outputs go through one [unit][env] LDS tile back into that layout. Every product is the
+ * same k-ordered chain from 0 as in policy_kernel, and the epilogue and heads are the same code, so
+ * the two layouts are bit-identical.
+ * ------------------------------------------------------------------------------------------- */
+constexpr int WM = 16;       /* envs per one-wave workgroup */
+constexpr int WLDA = WM + 1; /* row stride of the [unit][env] tile */
+
+template <int KIN, int NOUT, bool ACTOR>
+__global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
+#pragma clang fp contract(off)
+  constexpr int KPAD = (KIN + 15) / 16 * 16;
+  constexpr int GIN = KPAD / 16;
+  constexpr int NTO = (NOUT + 15) / 16;
+  constexpr int OUTS = NOUT + 1;
+  constexpr int TW = H * WLDA;                          /* [unit][env] tile */
+  constexpr int OW = ACTOR ? WM * OUTS : 1;             /* actor output [env][c] */
+  constexpr int SW = 2 * TW > OW ? 2 * TW : OW;
+  __shared__ float st[SW]; /* layer output tile, then the old carry tile; the actor output after */
+  static_assert(SW * 4 <= 20 * 1024, "one step-wave slot of LDS");
+  float* const so = st + TW;
+
+  const int lane = threadIdx.x, c16 = lane & 15, k4 = lane >> 4;
+  const int e0 = blockIdx.x * WM;
+  const int ge_a = e0 + c16; /* env of this lane's A operands */
+  const bool va = ge_a < a.n;
+  const float4* wp4 = reinterpret_cast<const float4*>(a.wpack);
+
+  /* 1. input projection: A = observation values k = 16 g + 4 u + k4 of env c16, in registers */
+  float xa[4 * GIN];
+  {
+    const float* src = a.obs + (size_t)ge_a * KIN;
+#pragma unroll
+    for (int i = 0; i < 4 * GIN; ++i) {
+      const int k = 4 * i + k4; /* i = 4 g + u */
+      xa[i] = (va && k < KIN) ? src[k] : 0.f;
+    }
+  }
+  float xr[4 * GH]; /* the current layer's input in A layout */
+  for (int w = 0; w < NWAVE; ++w) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float4* wp = wp4 + (size_t)w * GIN * 64 + lane;
+    float4 b = wp[0];
+#pragma unroll
+    for (int g = 0; g < GIN; ++g) {
+      const float4 bn = wp[(size_t)(g + 1 < GIN ? g + 1 : g) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = mma(xa[4 * g + u], q4(b, u), acc);
+      b = bn;
+    }
+    const int unit = 16 * w + c16;
+    const float bu = a.bias[unit];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) st[unit * WLDA + crow(0, v, lane)] = acc[v] + bu;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4 * GH; ++i) xr[i] = st[(4 * i + k4) * WLDA + c16];
+  __syncthreads();
+
+  /* 2. GRU stack */
+  const size_t off_gru = (size_t)(H / 16) * GIN * 64;
+  constexpr size_t MAT = (size_t)(3 * H / 16) * GH * 64;
+  for (int l = 0; l < D; ++l) {
+    float hr[4 * GH]; /* carry of layer l in A layout */
+    {
+      const bool live = va && !(a.reset && a.reset[ge_a]);
+      const float* cp = a.carry + ((size_t)ge_a * D + l) * H;
+#pragma unroll
+      for (int i = 0; i < 4 * GH; ++i) hr[i] = live ? cp[4 * i + k4] : 0.f;
+      /* and in [unit][env] for the GRU update's old carry */
+#pragma unroll
+      for (int i = 0; i < 4 * GH; ++i) so[(4 * i + k4) * WLDA + c16] = hr[i];
+      __syncthreads();
+    }
+    const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
+    const float4* whh = wih + MAT;
+    const float* bl = a.bias + H + (size_t)l * 4 * H;
+    for (int w = 0; w < NWAVE; ++w) {
+      size_t to[3];
+#pragma unroll
+      for (int gt = 0; gt < 3; ++gt) to[gt] = (size_t)(8 * gt + w) * GH * 64;
+      f32x4 ia[3], ha[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ia[i] = ha[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float4 bi[3], bh[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        bi[i] = wih[to[i]];
+        bh[i] = whh[to[i]];
+      }
+#pragma unroll
+      for (int g = 0; g < GH; ++g) {
+        /* the next group's fragments are loaded a whole group (24 MFMAs) ahead of their use */
+        float4 ni[3], nh[3];
+        const size_t gn = (size_t)(g + 1 < GH ? g + 1 : g) * 64;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          ni[i] = wih[to[i] + gn];
+          nh[i] = whh[to[i] + gn];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ia[i] = mma(xr[4 * g + u], q4(bi[i], u), ia[i]);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ha[i] = mma(hr[4 * g + u], q4(bh[i], u), ha[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          bi[i] = ni[i];
+          bh[i] = nh[i];
+        }
+      }
+      const int unit = 16 * w + c16;
+      const float br = bl[unit], bz = bl[H + unit], bni = bl[2 * H + unit], bnh = bl[3 * H + unit];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int e = crow(0, v, lane), ge = e0 + e;
+        const float r = zbf_sigmoid((ia[0][v] + br) + ha[0][v]);
+        const float z = zbf_sigmoid((ia[1][v] + bz) + ha[1][v]);
+        const float nn = zbf_tanh((ia[2][v] + bni) + r * (ha[2][v] + bnh));
+        const float ho = so[unit * WLDA + e]; /* the old carry of (env e, unit) */
+        const float hv = nn + z * (ho - nn);
+        st[unit * WLDA + e] = hv;
+        if (ge < a.n) a.carry[((size_t)ge * D + l) * H + unit] = hv;
+      }
+    }
+    __syncthreads();
+    if (l + 1 < D || ACTOR) {
+#pragma unroll
+      for (int i = 0; i < 4 * GH; ++i) xr[i] = st[(4 * i + k4) * WLDA + c16];
+      __syncthreads();
+    }
+  }
+
+  /* 3. heads */
+  const float* tail = a.bias + H + (size_t)D * 4 * H;
+  if constexpr (ACTOR) {
+    const float4* wo = wp4 + off_gru + (size_t)D * 2 * MAT + lane;
+    for (int nt = 0; nt < NTO; ++nt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float4* wt = wo + (size_t)nt * GH * 64;
+      float4 b = wt[0];
+#pragma unroll
+      for (int g = 0; g < GH; ++g) {
+        const float4 bn = wt[(size_t)(g + 1 < GH ? g + 1 : g) * 64];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = mma(xr[4 * g + u], q4(b, u), acc);
+        b = bn;
+      }
+      const int c = nt * 16 + c16;
+      if (c < NOUT) {
+        const float bc = tail[c];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) st[crow(0, v, lane) * OUTS + c] = acc[v] + bc;
+      }
+    }
+    __syncthreads();
+    const float* mean_bias = tail + NOUT;
+    for (int it = lane; it < WM * NJ; it += 64) {
+      const int e = it / NJ, j = it - e * NJ, ge = e0 + e;
+      if (ge >= a.n) continue;
+      const float* o = st + e * OUTS;
+      float mu[NMIX], sd[NMIX], lg[NMIX];
+#pragma unroll
+      for (int m = 0; m < NMIX; ++m) {
+        mu[m] = o[j * NMIX + m] + mean_bias[j];
+        const float s = (zbf_softplus(o[NJ * NMIX + j * NMIX + m]) + 0.01f) * 1.0f;
+        sd[m] = s < 1.0f ? s : 1.0f;
+        lg[m] = o[2 * NJ * NMIX + j * NMIX + m];
+      }
+      const size_t ai = (size_t)ge * NJ + j;
+      float act;
+      if (a.mode == ZB_POL_EVAL) {
+        act = a.actions[ai];
+      } else {
+        act = zbf_mix_sample(mu, sd, lg, a.mode == ZB_POL_MODE, a.seed, ZB_RNG_POLICY, (uint32_t)j,
+                             (uint32_t)(NJ + j), (uint32_t)(a.env_offset + ge), a.step);
+        a.actions[ai] = act;
+      }
+      if (a.log_prob) a.log_prob[ai] = zbf_mix_log_prob(mu, sd, lg, act);
+    }
+  } else {
+    /* value head: one fmaf chain per env over the [unit][env] tile of the last layer */
+    if (lane < WM && e0 + lane < a.n) {
+      const float* wo = tail + NOUT;
+      float acc = 0.f;
+      for (int k = 0; k < H; ++k) acc = fmaf(st[k * WLDA + lane], wo[k], acc);
+      a.value[e0 + lane] = acc + tail[0];
+    }
+  }
+}
+
 }  // namespace pol
 
 hipError_t launch_policy(int kind, const PolicyArgs& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
+  if (a.layout == ZB_POL_LAYOUT_WAVE) {
+    const int nw = (a.n + pol::WM - 1) / pol::WM;
+    if (kind == ZB_POL_ACTOR)
+      hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_ACTOR_IN, ZB_POL_ACTOR_OUT, true>), dim3(nw), dim3(64), 0, s,
+                         a);
+    else
+      hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_CRITIC_IN, 1, false>), dim3(nw), dim3(64), 0, s, a);
+    return hipGetLastError();
+  }
   const int nblk = (a.n + pol::M - 1) / pol::M;
   if (kind == ZB_POL_ACTOR)
     hipLaunchKernelGGL((pol::policy_kernel<ZB_POL_ACTOR_IN, ZB_POL_ACTOR_OUT, true>), dim3(nblk), dim3(pol::NTHR), 0,

@@ -83,7 +83,8 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.zb_policy_actor.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_uint64, C.c_int, C.c_uint32, vp, vp,
                                   vp]
     L.zb_policy_critic.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, vp]
-    for f in ("zb_policy_create", "zb_policy_destroy", "zb_policy_actor", "zb_policy_critic"):
+    L.zb_policy_set_layout.argtypes = [vp, C.c_int]
+    for f in ("zb_policy_create", "zb_policy_destroy", "zb_policy_actor", "zb_policy_critic", "zb_policy_set_layout"):
         getattr(L, f).restype = C.c_int
     if L.zb_abi_version() != ABI_VERSION:
         raise ZbError(f"{lp}: ABI version {L.zb_abi_version()}, this binding speaks {ABI_VERSION}: rebuild it")
@@ -263,7 +264,7 @@ class EnvGroups:
     OUTPUTS = ("obs_actor", "obs_critic", "obs_extra", "reward_terms", "reward", "done", "success")
 
     def __init__(self, model, cfg: cs.ZbEnvConfig, n_envs: int, groups: int = 2, env_offset: int = 0,
-                 device: int = 0, seed: int = 0, lib_path: str | None = None):
+                 device: int = 0, seed: int = 0, lib_path: str | None = None, priority: int = 0):
         import torch  # noqa: PLC0415
 
         self.torch = torch
@@ -281,7 +282,8 @@ class EnvGroups:
             setattr(self, name, full)
             for e, (a, b) in zip(self.engines, self.bounds):
                 setattr(e, name, full[a:b])
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(groups)]
+        # priority < 0: high-priority group streams (torch.cuda.Stream priority)
+        self.streams = [torch.cuda.Stream(device=self.device, priority=priority) for _ in range(groups)]
         self._tail = [None] * groups  # each group's last enqueued event
 
     def groups(self):

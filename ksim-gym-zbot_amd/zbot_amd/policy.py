@@ -31,6 +31,7 @@ HIDDEN, DEPTH, MIXTURES, JOINTS = 128, 5, 5, 20
 ACTOR_IN, CRITIC_IN, ACTOR_OUT = 50, 484, 300
 ACTOR, CRITIC = 0, 1
 SAMPLE, MODE, EVAL = 0, 1, 2
+LAYOUT_BLOCK, LAYOUT_WAVE = 0, 1  # include/zbot_policy.h ZB_POL_LAYOUT_*
 # matrix-core FLOP per env per step (FMA = 2): the roofline unit bench.py reports
 FLOP_ACTOR = 2 * (ACTOR_IN * HIDDEN + DEPTH * 6 * HIDDEN * HIDDEN + HIDDEN * ACTOR_OUT)
 FLOP_CRITIC = 2 * (CRITIC_IN * HIDDEN + DEPTH * 6 * HIDDEN * HIDDEN + HIDDEN)
@@ -78,7 +79,7 @@ def init_params(kind: int, seed: int = 0) -> np.ndarray:
 class GruPolicy:
     """One actor or critic network on one GPU (a zb_policy handle)."""
 
-    def __init__(self, kind: int, params=None, device: int = 0, seed: int = 0):
+    def __init__(self, kind: int, params=None, device: int = 0, seed: int = 0, layout: int | None = None):
         import torch  # noqa: PLC0415
 
         if not torch.cuda.is_available():
@@ -96,6 +97,13 @@ class GruPolicy:
         h = C.c_void_p()
         _check(self.L.zb_policy_create(kind, p.ctypes.data_as(C.POINTER(C.c_float)), p.size, device, C.byref(h)))
         self.h = h
+        if layout is not None:
+            self.set_layout(layout)
+
+    def set_layout(self, layout: int) -> None:
+        """LAYOUT_BLOCK (32 envs x 8 waves a workgroup) or LAYOUT_WAVE (16 envs on one wave, the size
+        of a zb_step wave's slot); bit-identical results (include/zbot_policy.h)."""
+        _check(self.L.zb_policy_set_layout(self.h, int(layout)))
 
     def __del__(self):
         h = getattr(self, "h", None)

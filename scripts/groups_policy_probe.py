@@ -8,6 +8,7 @@ Variants (each: 2 warm-up control steps, then --steps timed, best of --reps):
   groups   EnvGroups(G): each group's actor -> zb_step chain on the group's stream
   prio     as groups, the group streams created with high priority
   actprio  as groups, each group's actor on its own high-priority stream (event hand-offs)
+A "+wave" suffix runs the actor in the one-wave layout (ZB_POL_LAYOUT_WAVE).
 """
 
 import argparse
@@ -37,13 +38,13 @@ def main():
     cfg = default_config()
     n, T = args.n, args.steps
     actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0))
-    for v in args.variants.split(","):
+    for vv in args.variants.split(","):
+        v, _, lay = vv.partition("+")  # "+wave": the one-wave actor layout
+        actor.set_layout(P.LAYOUT_WAVE if lay == "wave" else P.LAYOUT_BLOCK)
         if v == "one":
             eng = HipEngine(cm, cfg, n, seed=1)
         else:
-            eng = EnvGroups(cm, cfg, n, groups=args.groups, seed=1)
-            if v in ("prio",):
-                eng.streams = [torch.cuda.Stream(priority=-1) for _ in range(eng.G)]
+            eng = EnvGroups(cm, cfg, n, groups=args.groups, seed=1, priority=-1 if v == "prio" else 0)
         if v == "actprio":
             astreams = [torch.cuda.Stream(priority=-1) for _ in range(eng.G)]
             carry = actor.initial_carry(n)
@@ -85,7 +86,7 @@ def main():
             torch.cuda.synchronize()
             best = min(best, time.perf_counter() - w0)
             t += T
-        print(json.dumps({"variant": v, "n": n, "groups": 1 if v == "one" else args.groups,
+        print(json.dumps({"variant": vv, "n": n, "groups": 1 if v == "one" else args.groups,
                           "env_steps_per_s": round(n * T / best / 1e6, 4)}), flush=True)
 
 

@@ -25,10 +25,10 @@ from zbot_amd.constants import JOINT_BIASES  # noqa: E402
 from zbot_amd.engine import HipEngine  # noqa: E402
 
 
-def run(cm, cfg, n, G, acts, warmup, steps, reps):
+def run(cm, cfg, n, G, acts, warmup, steps, reps, prio=0):
     ng = n // G
     engs = [HipEngine(cm, cfg, ng, env_offset=g * ng) for g in range(G)]
-    streams = [torch.cuda.Stream() for _ in range(G)]
+    streams = [torch.cuda.Stream(priority=prio) for _ in range(G)]
     for e, s in zip(engs, streams):
         with torch.cuda.stream(s):
             e.reset()
@@ -75,15 +75,16 @@ def main():
     acts = bias + 0.05 * torch.randn(64, args.n, cs.NJ, device="cuda", generator=g)
     ref = None
     out = {}
-    for G in [int(x) for x in args.groups.split(",")]:
-        best, mean, st = run(cm, cfg, args.n, G, acts, args.warmup, args.steps, args.reps)
+    for GG in args.groups.split(","):
+        G = int(GG.rstrip("p"))  # "4p": high-priority streams
+        best, mean, st = run(cm, cfg, args.n, G, acts, args.warmup, args.steps, args.reps, -1 if GG.endswith("p") else 0)
         same = None
         if ref is None:
             ref = st
         else:
             same = bool(torch.equal(st.view(torch.int32), ref.view(torch.int32)))
-        out[G] = dict(best=round(best / 1e6, 4), mean=round(mean / 1e6, 4), bit_identical_to_G1=same)
-        print(json.dumps({"n": args.n, "config": args.config, "groups": G, **out[G]}), flush=True)
+        out[GG] = dict(best=round(best / 1e6, 4), mean=round(mean / 1e6, 4), bit_identical_to_G1=same)
+        print(json.dumps({"n": args.n, "config": args.config, "groups": GG, **out[GG]}), flush=True)
 
 
 if __name__ == "__main__":
