@@ -205,6 +205,9 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
 
     actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), device=dev.index,
                         layout=P.LAYOUT_WAVE if hasattr(eng, "groups") else P.LAYOUT_BLOCK)
+    # the critic runs over the whole rollout afterwards, 8-wave layout on the current stream: inside
+    # the group chains (PolicyRollout.run(critic=...), one-wave layout) it measured slower,
+    # 5.49 M vs 6.02 M env-steps/s (profiles/r02_v16d_bench_inloop_critic.json)
     critic = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=1), device=dev.index)
     ro = P.PolicyRollout(eng, actor, seed=3)
     ro.reset()
@@ -237,8 +240,8 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
     return {
         "workload": f"per GPU: {T}-step rollout of {n} envs with the GRU actor sampling every action, the GRU "
                     "critic over the rollout, GAE + value targets + advantage normalization (moments over RCCL)"
-                    + (f"; the rollout over {eng.G} env groups on high-priority streams (one-wave actor)"
-                       if hasattr(eng, "groups") else ""),
+                    + (f"; the rollout over {eng.G} env groups on high-priority streams (one-wave actor), the "
+                       "critic (8-wave) over the rollout afterwards" if hasattr(eng, "groups") else ""),
         "env_steps_per_s": world * n * T * reps / wall,
         "ms_per_rollout": 1e3 * wall / reps,
         "rollout_steps": T,

@@ -218,12 +218,20 @@ class PolicyRollout:
         self.carry.zero_()
         self.done = None
 
-    def run(self, T: int, record_critic: bool = False) -> dict:
+    def run(self, T: int, record_critic: bool = False, critic: GruPolicy | None = None,
+            critic_carry=None) -> dict:
         """T control steps. With record_critic, out["obs_critic"][t] is the critic observation of
         the state the actor acted in at step t (what get_ppo_variables evaluates the critic on,
         train.py:1683-1729) and out["obs_critic_next"] that of the state after step T-1 (the
         bootstrap value's input). out["success"][t] flags the steps whose episode ended at the
-        time limit without a failure (ksim's successes_t for compute_ppo_inputs)."""
+        time limit without a failure (ksim's successes_t for compute_ppo_inputs).
+
+        With `critic` (and record_critic), the critic runs inside the loop: V(s_t) right after
+        step t's launch, in the same group chain, with `critic_carry` ([n, 5, 128], updated in
+        place) reset where the previous step ended an episode (none at t = 0), then the bootstrap
+        V(s_T) (reset where step T-1 ended one). out["value"] [T, n] and out["value_next"] [n] are
+        bit-identical to critic.critic(out["obs_critic"], carry, reset=[0, done[:-1]]) followed by
+        critic.critic(out["obs_critic_next"], carry, reset=done[-1]) after the rollout."""
         torch = self.actor.torch
         n, dev = self.eng.n, self.eng.device
         if self.obs is None:
@@ -242,6 +250,11 @@ class PolicyRollout:
         rew = torch.empty(T, n, **f32)
         done = torch.zeros(T, n, dtype=torch.uint8, device=dev)
         success = torch.zeros(T, n, dtype=torch.uint8, device=dev)
+        if critic is not None:
+            if not record_critic or critic.kind != CRITIC or critic_carry is None:
+                raise ZbError("an in-loop critic needs record_critic=True, a critic handle and its carry")
+            critic._check_carry(critic_carry, n)
+            val = torch.empty(T + 1, n, **f32)
         L = self.eng.L
         # an EnvGroups engine runs each group's actor -> zb_step chain on the group's own stream
         # (DESIGN.md §4f); a HipEngine is one group on the current stream
@@ -261,6 +274,12 @@ class PolicyRollout:
                                      crit[t + 1][lo:hi].data_ptr() if record_critic else None, None, None,
                                      rew[t][lo:hi].data_ptr(), done[t][lo:hi].data_ptr(),
                                      success[t][lo:hi].data_ptr(), float(self.curriculum), stream))
+                    if critic is not None:  # V(s_t): its input crit[t] is ready since step t-1
+                        critic.critic(crit[t][lo:hi], critic_carry[lo:hi],
+                                      reset=done[t - 1][lo:hi] if t > 0 else None, value=val[t][lo:hi])
+                        if t == T - 1:  # the bootstrap V(s_T)
+                            critic.critic(crit[T][lo:hi], critic_carry[lo:hi], reset=done[T - 1][lo:hi],
+                                          value=val[T][lo:hi])
                 if grouped:
                     self.eng.mark(g)
             self.step_count += 1
@@ -273,4 +292,7 @@ class PolicyRollout:
         if record_critic:
             out["obs_critic"] = crit[:T]
             out["obs_critic_next"] = crit[T]
+        if critic is not None:
+            out["value"] = val[:T]
+            out["value_next"] = val[T]
         return out

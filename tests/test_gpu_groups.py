@@ -114,3 +114,33 @@ def test_grouped_policy_rollout_bit_identical(torch_gpu, cmodel):
         np.testing.assert_array_equal(_bits(b2[k]), _bits(b1[k]), err_msg=k)
     np.testing.assert_array_equal(_bits(c2), _bits(c1))
     assert int(a1["done"].sum()) > 0
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_in_loop_critic_matches_post_hoc(torch_gpu, cmodel, G):
+    """PolicyRollout's in-loop critic (V(s_t) after each step launch, per group, one-wave layout)
+    equals the critic run over the recorded observations afterwards (8-wave layout)."""
+    torch = torch_gpu
+    from zbot_amd import policy as P
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    cfg = default_config(max_episode_sec=0.2)
+    n, T = 150, 12
+    actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), layout=P.LAYOUT_WAVE)
+    crit_in = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=1), layout=P.LAYOUT_WAVE)
+    crit_ph = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=1), layout=P.LAYOUT_BLOCK)
+    eng = HipEngine(cmodel, cfg, n, seed=3) if G == 1 else EnvGroups(cmodel, cfg, n, groups=G, seed=3, priority=-1)
+    ro = P.PolicyRollout(eng, actor, seed=2)
+    ro.reset()
+    ro.run(2, record_critic=True)
+    cc = crit_in.initial_carry(n)
+    traj = ro.run(T, record_critic=True, critic=crit_in, critic_carry=cc)
+    cp = crit_ph.initial_carry(n)
+    zeros = torch.zeros(1, n, dtype=torch.uint8, device="cuda")
+    v = crit_ph.critic(traj["obs_critic"], cp, reset=torch.cat([zeros, traj["done"][:-1]]))
+    b = crit_ph.critic(traj["obs_critic_next"], cp, reset=traj["done"][-1])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_bits(traj["value"]), _bits(v))
+    np.testing.assert_array_equal(_bits(traj["value_next"]), _bits(b))
+    np.testing.assert_array_equal(_bits(cc), _bits(cp))
+    assert int(traj["done"].sum()) > 0
