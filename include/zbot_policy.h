@@ -80,6 +80,7 @@ int zb_policy_destroy(ZbPolicy* p);
  * zb_policy_create. */
 #define ZB_POL_LAYOUT_BLOCK 0
 #define ZB_POL_LAYOUT_WAVE 1
+#define ZB_POL_LAYOUT_WAVE2 2 /* the one-wave layout's unit tiles split over two waves (2 slots, 19 KB) */
 int zb_policy_set_layout(ZbPolicy* p, int layout);
 
 /*

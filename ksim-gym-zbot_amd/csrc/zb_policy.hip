@@ -337,8 +337,8 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
 constexpr int WM = 16;       /* envs per one-wave workgroup */
 constexpr int WLDA = WM + 1; /* row stride of the [unit][env] tile */
 
-template <int KIN, int NOUT, bool ACTOR>
-__global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
+template <int KIN, int NOUT, bool ACTOR, int NWV>
+__global__ __launch_bounds__(64 * NWV, 2) void policy_wave_kernel(PolicyArgs a) {
 #pragma clang fp contract(off)
   constexpr int KPAD = (KIN + 15) / 16 * 16;
   constexpr int GIN = KPAD / 16;
@@ -351,7 +351,8 @@ __global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
   static_assert(SW * 4 <= 20 * 1024, "one step-wave slot of LDS");
   float* const so = st + TW;
 
-  const int lane = threadIdx.x, c16 = lane & 15, k4 = lane >> 4;
+  /* NWV waves (1 or 2) share the 16 envs: wave v takes the unit tiles v, v + NWV, ... */
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, c16 = lane & 15, k4 = lane >> 4;
   const int e0 = blockIdx.x * WM;
   const int ge_a = e0 + c16; /* env of this lane's A operands */
   const bool va = ge_a < a.n;
@@ -368,7 +369,7 @@ __global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
     }
   }
   float xr[4 * GH]; /* the current layer's input in A layout */
-  for (int w = 0; w < NWAVE; ++w) {
+  for (int w = wv; w < NWAVE; w += NWV) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     const float4* wp = wp4 + (size_t)w * GIN * 64 + lane;
     float4 b = wp[0];
@@ -402,13 +403,14 @@ __global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
       for (int i = 0; i < 4 * GH; ++i) hr[i] = live ? cp[4 * i + k4] : 0.f;
       /* and in [unit][env] for the GRU update's old carry */
 #pragma unroll
-      for (int i = 0; i < 4 * GH; ++i) so[(4 * i + k4) * WLDA + c16] = hr[i];
+      for (int i = 0; i < 4 * GH; ++i)
+        if (wv == 0) so[(4 * i + k4) * WLDA + c16] = hr[i];
       __syncthreads();
     }
     const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
     const float4* whh = wih + MAT;
     const float* bl = a.bias + H + (size_t)l * 4 * H;
-    for (int w = 0; w < NWAVE; ++w) {
+    for (int w = wv; w < NWAVE; w += NWV) {
       size_t to[3];
 #pragma unroll
       for (int gt = 0; gt < 3; ++gt) to[gt] = (size_t)(8 * gt + w) * GH * 64;
@@ -471,7 +473,7 @@ __global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
   const float* tail = a.bias + H + (size_t)D * 4 * H;
   if constexpr (ACTOR) {
     const float4* wo = wp4 + off_gru + (size_t)D * 2 * MAT + lane;
-    for (int nt = 0; nt < NTO; ++nt) {
+    for (int nt = wv; nt < NTO; nt += NWV) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
       const float4* wt = wo + (size_t)nt * GH * 64;
       float4 b = wt[0];
@@ -492,7 +494,7 @@ __global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
     }
     __syncthreads();
     const float* mean_bias = tail + NOUT;
-    for (int it = lane; it < WM * NJ; it += 64) {
+    for (int it = tid; it < WM * NJ; it += 64 * NWV) {
       const int e = it / NJ, j = it - e * NJ, ge = e0 + e;
       if (ge >= a.n) continue;
       const float* o = st + e * OUTS;
@@ -517,11 +519,11 @@ __global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
     }
   } else {
     /* value head: one fmaf chain per env over the [unit][env] tile of the last layer */
-    if (lane < WM && e0 + lane < a.n) {
+    if (tid < WM && e0 + tid < a.n) {
       const float* wo = tail + NOUT;
       float acc = 0.f;
-      for (int k = 0; k < H; ++k) acc = fmaf(st[k * WLDA + lane], wo[k], acc);
-      a.value[e0 + lane] = acc + tail[0];
+      for (int k = 0; k < H; ++k) acc = fmaf(st[k * WLDA + tid], wo[k], acc);
+      a.value[e0 + tid] = acc + tail[0];
     }
   }
 }
@@ -530,13 +532,21 @@ __global__ __launch_bounds__(64, 2) void policy_wave_kernel(PolicyArgs a) {
 
 hipError_t launch_policy(int kind, const PolicyArgs& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
-  if (a.layout == ZB_POL_LAYOUT_WAVE) {
+  if (a.layout == ZB_POL_LAYOUT_WAVE || a.layout == ZB_POL_LAYOUT_WAVE2) {
     const int nw = (a.n + pol::WM - 1) / pol::WM;
-    if (kind == ZB_POL_ACTOR)
-      hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_ACTOR_IN, ZB_POL_ACTOR_OUT, true>), dim3(nw), dim3(64), 0, s,
-                         a);
-    else
-      hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_CRITIC_IN, 1, false>), dim3(nw), dim3(64), 0, s, a);
+    if (a.layout == ZB_POL_LAYOUT_WAVE) {
+      if (kind == ZB_POL_ACTOR)
+        hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_ACTOR_IN, ZB_POL_ACTOR_OUT, true, 1>), dim3(nw), dim3(64), 0,
+                           s, a);
+      else
+        hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_CRITIC_IN, 1, false, 1>), dim3(nw), dim3(64), 0, s, a);
+    } else {
+      if (kind == ZB_POL_ACTOR)
+        hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_ACTOR_IN, ZB_POL_ACTOR_OUT, true, 2>), dim3(nw), dim3(128),
+                           0, s, a);
+      else
+        hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_CRITIC_IN, 1, false, 2>), dim3(nw), dim3(128), 0, s, a);
+    }
     return hipGetLastError();
   }
   const int nblk = (a.n + pol::M - 1) / pol::M;

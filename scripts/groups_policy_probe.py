@@ -40,7 +40,7 @@ def main():
     actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0))
     for vv in args.variants.split(","):
         v, _, lay = vv.partition("+")  # "+wave": the one-wave actor layout
-        actor.set_layout(P.LAYOUT_WAVE if lay == "wave" else P.LAYOUT_BLOCK)
+        actor.set_layout({"wave": P.LAYOUT_WAVE, "wave2": P.LAYOUT_WAVE2}.get(lay, P.LAYOUT_BLOCK))
         if v == "one":
             eng = HipEngine(cm, cfg, n, seed=1)
         else:
