@@ -135,6 +135,12 @@ int zb_get_stats(ZbHandle* h, float* stats_dev, int clear, void* stream);
  * its substeps, per env ([n_envs] int32, device). */
 int zb_get_solver_iters(ZbHandle* h, int32_t* iters_dev, void* stream);
 
+/* Work units per pair of envs in the handle's zb_step launches: 0 restores the
+ * automatic choice made at zb_create, 1 runs whole control steps, k > 1 splits every pair's
+ * substeps into k chunks (clamped to the substep count). Results are the same bits for every k.
+ * Env groups on their own streams fill the drain themselves and run unchunked. */
+int zb_set_step_chunks(ZbHandle* h, int k);
+
 /* Diagnostic: one forward pass (no integration) on the qpos/qvel stored in
  * state_dev [n_envs, ZB_STATE_STRIDE] with ctrl_dev [n_envs, 20] (nullable ->
  * zero ctrl); dumps M, bias, qacc_smooth, qacc, xpos, cinert, cvel and sensor

@@ -457,6 +457,19 @@ int zb_get_stats(ZbHandle* h, float* stats_dev, int clear, void* stream) {
   if (clear) HIPCHK(hipMemsetAsync(h->stats, 0, (size_t)h->n * ZB_NUM_STATS * sizeof(float), (hipStream_t)stream));
   return ZB_OK;
 }
+int zb_set_step_chunks(ZbHandle* h, int k) {
+  if (!h) return fail(ZB_EARG, "null handle");
+  if (k < 0) return fail(ZB_EARG, "zb_set_step_chunks: k = %d < 0", k);
+  if (k == 0) {
+    int rc = use_device(h);
+    if (rc) return rc;
+    h->nchunk = choose_chunks(h->n, h->cfg.n_substeps, zb::step_resident_blocks(h->device));
+  } else {
+    h->nchunk = k > h->cfg.n_substeps ? h->cfg.n_substeps : k;
+  }
+  return ZB_OK;
+}
+
 int zb_get_solver_iters(ZbHandle* h, int32_t* iters_dev, void* stream) {
   if (!h) return fail(ZB_EARG, "null handle");
   return copy_rows(h, iters_dev, h->iters, (size_t)h->n * sizeof(int32_t), stream);

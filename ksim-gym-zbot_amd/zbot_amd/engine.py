@@ -63,9 +63,11 @@ def load_library(path: str | None = None) -> C.CDLL:
     for f in ("zb_get_state", "zb_set_state", "zb_get_rand", "zb_set_rand", "zb_get_solver_iters"):
         getattr(L, f).argtypes = [vp, vp, vp]
     L.zb_get_stats.argtypes = [vp, vp, C.c_int, vp]
+    L.zb_set_step_chunks.argtypes = [vp, C.c_int]
     L.zb_debug_forward.argtypes = [vp, vp, vp, vp, vp]
     for f in ("zb_create", "zb_destroy", "zb_reset", "zb_step", "zb_rollout", "zb_get_state", "zb_set_state",
-              "zb_get_rand", "zb_set_rand", "zb_get_stats", "zb_get_solver_iters", "zb_debug_forward"):
+              "zb_get_rand", "zb_set_rand", "zb_get_stats", "zb_get_solver_iters", "zb_debug_forward",
+              "zb_set_step_chunks"):
         getattr(L, f).restype = C.c_int
     # post-rollout PPO inputs (include/zbot_ppo.h)
     L.zb_gae_partials_words.argtypes = [C.c_int]
@@ -221,6 +223,11 @@ class HipEngine:
         _check(self.L.zb_get_stats(self.h, _ptr(out), int(clear), self._stream()))
         return out
 
+    def set_step_chunks(self, k: int) -> None:
+        """Work units per pair of envs in step() (0: the automatic choice, 1: whole control steps;
+        DESIGN.md §4e). The same bits for every k."""
+        _check(self.L.zb_set_step_chunks(self.h, int(k)))
+
     def solver_iters(self):
         out = self.torch.empty(self.n, dtype=self.torch.int32, device=self.device)
         _check(self.L.zb_get_solver_iters(self.h, _ptr(out), self._stream()))
@@ -264,7 +271,8 @@ class EnvGroups:
     OUTPUTS = ("obs_actor", "obs_critic", "obs_extra", "reward_terms", "reward", "done", "success")
 
     def __init__(self, model, cfg: cs.ZbEnvConfig, n_envs: int, groups: int = 2, env_offset: int = 0,
-                 device: int = 0, seed: int = 0, lib_path: str | None = None, priority: int = 0):
+                 device: int = 0, seed: int = 0, lib_path: str | None = None, priority: int = 0,
+                 chunks: int = 1):
         import torch  # noqa: PLC0415
 
         self.torch = torch
@@ -274,6 +282,10 @@ class EnvGroups:
         self.bounds = group_bounds(n_envs, groups)
         self.engines = [HipEngine(model, cfg, b - a, env_offset=env_offset + a, device=device, seed=seed,
                                   lib_path=lib_path) for a, b in self.bounds]
+        # the groups fill each other's drains, so a partial last round needs no chunking (§4e);
+        # chunks=0 keeps zb_create's automatic choice
+        for e in self.engines:
+            e.set_step_chunks(chunks)
         e0 = self.engines[0]
         self.L, self.device, self.cfg, self.seed = e0.L, e0.device, cfg, seed
         for name in self.OUTPUTS:

@@ -198,13 +198,16 @@ class PolicyRollout:
     actor -> zb_step chain on their own stream (bit-identical: the actor's RNG is keyed by global
     env id)."""
 
-    def __init__(self, engine, actor: GruPolicy, seed: int = 0, curriculum: float = 1.0):
+    def __init__(self, engine, actor: GruPolicy, seed: int = 0, curriculum: float = 1.0, stagger: bool = False):
         if actor.kind != ACTOR:
             raise ZbError("PolicyRollout needs an actor")
         self.eng = engine
         self.actor = actor
         self.seed = seed
         self.curriculum = curriculum
+        # with env groups: at the first step of a run(), group g's chain starts after group g-1's
+        # first actor launch, offsetting the groups' phases (bit-identical either way)
+        self.stagger = stagger
         self.carry = actor.initial_carry(engine.n)
         self.step_count = 0
         self.obs = None
@@ -267,9 +270,14 @@ class PolicyRollout:
                 with (torch.cuda.stream(s) if s is not None else contextlib.nullcontext()):
                     stream = torch.cuda.current_stream(dev).cuda_stream
                     r = done[t - 1][lo:hi] if t > 0 else (None if self.done is None else self.done[lo:hi])
+                    if self.stagger and grouped and t == 0 and g > 0:
+                        s.wait_event(prev_actor)
                     self.actor.actor(obs[t][lo:hi], self.carry[lo:hi], reset=r, mode=SAMPLE, seed=self.seed,
                                      env_offset=e.env_offset, step=self.step_count, actions=acts[t][lo:hi],
                                      log_prob=lp[t][lo:hi])
+                    if self.stagger and grouped and t == 0:
+                        prev_actor = torch.cuda.Event()
+                        prev_actor.record(s)
                     _check(L.zb_step(e.h, acts[t][lo:hi].data_ptr(), obs[t + 1][lo:hi].data_ptr(),
                                      crit[t + 1][lo:hi].data_ptr() if record_critic else None, None, None,
                                      rew[t][lo:hi].data_ptr(), done[t][lo:hi].data_ptr(),

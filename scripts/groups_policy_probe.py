@@ -8,10 +8,12 @@ Variants (each: 2 warm-up control steps, then --steps timed, best of --reps):
   groups   EnvGroups(G): each group's actor -> zb_step chain on the group's stream
   prio     as groups, the group streams created with high priority
   actprio  as groups, each group's actor on its own high-priority stream (event hand-offs)
-A "+wave" suffix runs the actor in the one-wave layout (ZB_POL_LAYOUT_WAVE).
+A "+wave" suffix runs the actor in the one-wave layout (ZB_POL_LAYOUT_WAVE); "priostag" / "groupsstag"
+stagger the groups' first actor launches (PolicyRollout(stagger=True)).
 """
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -33,18 +35,25 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--groups", type=int, default=2)
     ap.add_argument("--variants", default="one,groups,prio,actprio")
+    ap.add_argument("--chunks", type=int, default=1, help="EnvGroups chunks (0: automatic)")
     args = ap.parse_args()
     cm = compile_model()
     cfg = default_config()
     n, T = args.n, args.steps
     actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0))
     for vv in args.variants.split(","):
+        # drop the previous variant's handles first: a handle freed later by the garbage collector
+        # (hipFree synchronizes the device) would stall the next variant's timed loop
+        eng = ro = run = None
+        gc.collect()
+        torch.cuda.synchronize()
         v, _, lay = vv.partition("+")  # "+wave": the one-wave actor layout
         actor.set_layout({"wave": P.LAYOUT_WAVE, "wave2": P.LAYOUT_WAVE2}.get(lay, P.LAYOUT_BLOCK))
         if v == "one":
             eng = HipEngine(cm, cfg, n, seed=1)
         else:
-            eng = EnvGroups(cm, cfg, n, groups=args.groups, seed=1, priority=-1 if v == "prio" else 0)
+            eng = EnvGroups(cm, cfg, n, groups=args.groups, seed=1, priority=-1 if v.startswith("prio") else 0,
+                            chunks=args.chunks)
         if v == "actprio":
             astreams = [torch.cuda.Stream(priority=-1) for _ in range(eng.G)]
             carry = actor.initial_carry(n)
@@ -71,7 +80,7 @@ def main():
                         eng.mark(g)
                 eng.join()
         else:
-            ro = P.PolicyRollout(eng, actor, seed=1)
+            ro = P.PolicyRollout(eng, actor, seed=1, stagger=v.endswith("stag"))
             ro.reset()
 
             def run(k, t0):

@@ -144,3 +144,25 @@ def test_in_loop_critic_matches_post_hoc(torch_gpu, cmodel, G):
     np.testing.assert_array_equal(_bits(traj["value_next"]), _bits(b))
     np.testing.assert_array_equal(_bits(cc), _bits(cp))
     assert int(traj["done"].sum()) > 0
+
+
+def test_set_step_chunks_same_bits(torch_gpu, cmodel):
+    torch = torch_gpu
+    from zbot_amd.engine import HipEngine, ZbError
+
+    cfg = default_config(push=True, max_episode_sec=0.3)
+    n = 90
+    acts = _actions(torch, cmodel, 8, n, 11)
+    states = []
+    for k in (1, 3, 0):
+        e = HipEngine(cmodel, cfg, n, seed=12)
+        e.set_step_chunks(k)
+        e.reset()
+        for t in range(8):
+            e.step(acts[t])
+        states.append(e.get_state())
+    torch.cuda.synchronize()
+    for st in states[1:]:
+        np.testing.assert_array_equal(_bits(st), _bits(states[0]))
+    with pytest.raises(ZbError):
+        e.set_step_chunks(-1)
