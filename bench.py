@@ -133,7 +133,7 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
     every env's action from its observation on the f32 matrix cores, then zb_step advances the
     envs (ksim sample_action -> env.step, train.py:1737-1763). The actor's kernel time and roofline
     come from one handle on the current stream with the 8-wave actor (isolated launches). With
-    `grouped` (an EnvGroups on high-priority streams) the leg's throughput is PolicyRollout running
+    `grouped` (an EnvGroups) the leg's throughput is PolicyRollout running
     each group's actor -> zb_step chain on its own stream with the one-wave actor layout, whose
     workgroups fit the slots the other groups' step launches free."""
     import torch  # noqa: PLC0415
@@ -186,8 +186,8 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
         torch.cuda.synchronize(dev)
         out["env_steps_per_s_with_policy_one_stream"] = out["env_steps_per_s_with_policy"]
         out["env_steps_per_s_with_policy"] = n * steps / (time.perf_counter() - t0)
-        out["workload"] += (f"; {grouped.G} env groups on high-priority streams, each running its actor (one-wave "
-                            "layout) -> zb_step chain")
+        out["workload"] += (f"; {grouped.G} env groups, each running its actor (one-wave layout) -> zb_step chain "
+                            "on its own stream")
     return out
 
 
@@ -240,8 +240,8 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
     return {
         "workload": f"per GPU: {T}-step rollout of {n} envs with the GRU actor sampling every action, the GRU "
                     "critic over the rollout, GAE + value targets + advantage normalization (moments over RCCL)"
-                    + (f"; the rollout over {eng.G} env groups on high-priority streams (one-wave actor), the "
-                       "critic (8-wave) over the rollout afterwards" if hasattr(eng, "groups") else ""),
+                    + (f"; the rollout over {eng.G} env groups (one-wave actor), the critic (8-wave) over the "
+                       "rollout afterwards" if hasattr(eng, "groups") else ""),
         "env_steps_per_s": world * n * T * reps / wall,
         "ms_per_rollout": 1e3 * wall / reps,
         "rollout_steps": T,
@@ -260,8 +260,8 @@ def main() -> None:
                     help="env groups per GPU, each stepping on its own HIP stream (zbot_amd.EnvGroups, "
                          "DESIGN.md §4f); 1 = one handle on the current stream")
     ap.add_argument("--policy-groups", type=int, default=3,
-                    help="env groups of the actor-in-the-loop legs (high-priority streams, one-wave actor "
-                         "layout; DESIGN.md §4f); 1 = one handle, 8-wave actor, current stream")
+                    help="env groups of the actor-in-the-loop legs (one-wave actor layout; DESIGN.md §4f); "
+                         "1 = one handle, 8-wave actor, current stream")
     ap.add_argument("--cpu-baseline-sec", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
@@ -386,7 +386,7 @@ def main() -> None:
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
     # the actor-in-the-loop legs: one handle on the current stream for the actor's kernel time, and
-    # args.policy_groups env groups on high-priority streams with the one-wave actor
+    # args.policy_groups env groups with the one-wave actor
     eng1 = eng if G == 1 else None
     engp = None
     if not (args.no_policy and args.no_pipeline):
@@ -394,7 +394,7 @@ def main() -> None:
             eng1 = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
         if args.policy_groups > 1:
             engp = EnvGroups(cm, cfg, n, groups=args.policy_groups, env_offset=rank * n, device=dev.index,
-                             seed=args.seed, priority=-1)
+                             seed=args.seed)
     policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, engp)
     pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(engp or eng1, n, 32, 2, dev, world)
 
