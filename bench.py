@@ -134,7 +134,7 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
     envs (ksim sample_action -> env.step, train.py:1737-1763). The actor's kernel time and roofline
     come from one handle on the current stream with the 8-wave actor (isolated launches). With
     `grouped` (an EnvGroups) the leg's throughput is PolicyRollout running
-    each group's actor -> zb_step chain on its own stream with the one-wave actor layout, whose
+    each group's actor -> zb_step chain on its own stream with the two-wave slot-sized actor layout, whose
     workgroups fit the slots the other groups' step launches free."""
     import torch  # noqa: PLC0415
     from zbot_amd import policy as P  # noqa: PLC0415
@@ -176,7 +176,7 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
                      "flop_per_env_step": P.FLOP_ACTOR, "dtype": "f32 (v_mfma_f32_16x16x4_f32)"},
     }
     if grouped is not None:
-        actor.set_layout(P.LAYOUT_WAVE)
+        actor.set_layout(P.LAYOUT_WAVE2)
         ro = P.PolicyRollout(grouped, actor, seed=1)
         ro.reset()
         ro.run(2)
@@ -186,8 +186,8 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
         torch.cuda.synchronize(dev)
         out["env_steps_per_s_with_policy_one_stream"] = out["env_steps_per_s_with_policy"]
         out["env_steps_per_s_with_policy"] = n * steps / (time.perf_counter() - t0)
-        out["workload"] += (f"; {grouped.G} env groups, each running its actor (one-wave layout) -> zb_step chain "
-                            "on its own stream")
+        out["workload"] += (f"; {grouped.G} env groups, each running its actor (two-wave slot-sized layout) -> "
+                            "zb_step chain on its own stream")
     return out
 
 
@@ -204,7 +204,7 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
     from zbot_amd.ppo import compute_ppo_inputs  # noqa: PLC0415
 
     actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), device=dev.index,
-                        layout=P.LAYOUT_WAVE if hasattr(eng, "groups") else P.LAYOUT_BLOCK)
+                        layout=P.LAYOUT_WAVE2 if hasattr(eng, "groups") else P.LAYOUT_BLOCK)
     # the critic runs over the whole rollout afterwards, 8-wave layout on the current stream: inside
     # the group chains (PolicyRollout.run(critic=...), one-wave layout) it measured slower,
     # 5.49 M vs 6.02 M env-steps/s (profiles/r02_v16d_bench_inloop_critic.json)
@@ -240,8 +240,8 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
     return {
         "workload": f"per GPU: {T}-step rollout of {n} envs with the GRU actor sampling every action, the GRU "
                     "critic over the rollout, GAE + value targets + advantage normalization (moments over RCCL)"
-                    + (f"; the rollout over {eng.G} env groups (one-wave actor), the critic (8-wave) over the "
-                       "rollout afterwards" if hasattr(eng, "groups") else ""),
+                    + (f"; the rollout over {eng.G} env groups (two-wave slot-sized actor), the critic (8-wave) "
+                       "over the rollout afterwards" if hasattr(eng, "groups") else ""),
         "env_steps_per_s": world * n * T * reps / wall,
         "ms_per_rollout": 1e3 * wall / reps,
         "rollout_steps": T,
@@ -260,7 +260,7 @@ def main() -> None:
                     help="env groups per GPU, each stepping on its own HIP stream (zbot_amd.EnvGroups, "
                          "DESIGN.md §4f); 1 = one handle on the current stream")
     ap.add_argument("--policy-groups", type=int, default=3,
-                    help="env groups of the actor-in-the-loop legs (one-wave actor layout; DESIGN.md §4f); "
+                    help="env groups of the actor-in-the-loop legs (two-wave slot-sized actor layout; DESIGN.md §4f); "
                          "1 = one handle, 8-wave actor, current stream")
     ap.add_argument("--cpu-baseline-sec", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -386,7 +386,7 @@ def main() -> None:
 
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
     # the actor-in-the-loop legs: one handle on the current stream for the actor's kernel time, and
-    # args.policy_groups env groups with the one-wave actor
+    # args.policy_groups env groups with the slot-sized two-wave actor
     eng1 = eng if G == 1 else None
     engp = None
     if not (args.no_policy and args.no_pipeline):
