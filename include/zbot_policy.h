@@ -81,6 +81,7 @@ int zb_policy_destroy(ZbPolicy* p);
 #define ZB_POL_LAYOUT_BLOCK 0
 #define ZB_POL_LAYOUT_WAVE 1
 #define ZB_POL_LAYOUT_WAVE2 2 /* the one-wave layout's unit tiles split over two waves (2 slots, 19 KB) */
+#define ZB_POL_LAYOUT_WAVE4 3 /* ... over four waves (4 slots, 19 KB) */
 int zb_policy_set_layout(ZbPolicy* p, int layout);
 
 /*

@@ -690,7 +690,8 @@ static int policy_run(ZbPolicy* h, int kind, const float* obs, int T, int n, flo
 
 int zb_policy_set_layout(ZbPolicy* p, int layout) {
   if (!p) return fail(ZB_EARG, "null policy handle");
-  if (layout != ZB_POL_LAYOUT_BLOCK && layout != ZB_POL_LAYOUT_WAVE && layout != ZB_POL_LAYOUT_WAVE2)
+  if (layout != ZB_POL_LAYOUT_BLOCK && layout != ZB_POL_LAYOUT_WAVE && layout != ZB_POL_LAYOUT_WAVE2 &&
+      layout != ZB_POL_LAYOUT_WAVE4)
     return fail(ZB_EARG, "unknown layout %d", layout);
   p->layout = layout;
   return ZB_OK;

@@ -532,9 +532,15 @@ __global__ __launch_bounds__(64 * NWV, 2) void policy_wave_kernel(PolicyArgs a) 
 
 hipError_t launch_policy(int kind, const PolicyArgs& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
-  if (a.layout == ZB_POL_LAYOUT_WAVE || a.layout == ZB_POL_LAYOUT_WAVE2) {
+  if (a.layout == ZB_POL_LAYOUT_WAVE || a.layout == ZB_POL_LAYOUT_WAVE2 || a.layout == ZB_POL_LAYOUT_WAVE4) {
     const int nw = (a.n + pol::WM - 1) / pol::WM;
-    if (a.layout == ZB_POL_LAYOUT_WAVE) {
+    if (a.layout == ZB_POL_LAYOUT_WAVE4) {
+      if (kind == ZB_POL_ACTOR)
+        hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_ACTOR_IN, ZB_POL_ACTOR_OUT, true, 4>), dim3(nw), dim3(256),
+                           0, s, a);
+      else
+        hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_CRITIC_IN, 1, false, 4>), dim3(nw), dim3(256), 0, s, a);
+    } else if (a.layout == ZB_POL_LAYOUT_WAVE) {
       if (kind == ZB_POL_ACTOR)
         hipLaunchKernelGGL((pol::policy_wave_kernel<ZB_POL_ACTOR_IN, ZB_POL_ACTOR_OUT, true, 1>), dim3(nw), dim3(64), 0,
                            s, a);

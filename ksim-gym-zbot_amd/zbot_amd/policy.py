@@ -31,7 +31,7 @@ HIDDEN, DEPTH, MIXTURES, JOINTS = 128, 5, 5, 20
 ACTOR_IN, CRITIC_IN, ACTOR_OUT = 50, 484, 300
 ACTOR, CRITIC = 0, 1
 SAMPLE, MODE, EVAL = 0, 1, 2
-LAYOUT_BLOCK, LAYOUT_WAVE, LAYOUT_WAVE2 = 0, 1, 2  # include/zbot_policy.h ZB_POL_LAYOUT_*
+LAYOUT_BLOCK, LAYOUT_WAVE, LAYOUT_WAVE2, LAYOUT_WAVE4 = 0, 1, 2, 3  # include/zbot_policy.h ZB_POL_LAYOUT_*
 # matrix-core FLOP per env per step (FMA = 2): the roofline unit bench.py reports
 FLOP_ACTOR = 2 * (ACTOR_IN * HIDDEN + DEPTH * 6 * HIDDEN * HIDDEN + HIDDEN * ACTOR_OUT)
 FLOP_CRITIC = 2 * (CRITIC_IN * HIDDEN + DEPTH * 6 * HIDDEN * HIDDEN + HIDDEN)

@@ -48,7 +48,7 @@ def main():
         gc.collect()
         torch.cuda.synchronize()
         v, _, lay = vv.partition("+")  # "+wave": the one-wave actor layout
-        actor.set_layout({"wave": P.LAYOUT_WAVE, "wave2": P.LAYOUT_WAVE2}.get(lay, P.LAYOUT_BLOCK))
+        actor.set_layout({"wave": P.LAYOUT_WAVE, "wave2": P.LAYOUT_WAVE2, "wave4": P.LAYOUT_WAVE4}.get(lay, P.LAYOUT_BLOCK))
         if v == "one":
             eng = HipEngine(cm, cfg, n, seed=1)
         else:

@@ -35,7 +35,7 @@ def test_actor_layouts_bit_identical(torch_gpu, n, mode):
     carry0 = 0.5 * torch.randn(n, P.DEPTH, P.HIDDEN, device="cuda", generator=g)
     given = torch.randn(T, n, P.JOINTS, device="cuda", generator=g)
     outs = []
-    for layout in (P.LAYOUT_BLOCK, P.LAYOUT_WAVE, P.LAYOUT_WAVE2):
+    for layout in (P.LAYOUT_BLOCK, P.LAYOUT_WAVE, P.LAYOUT_WAVE2, P.LAYOUT_WAVE4):
         pol = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=4), layout=layout)
         carry = carry0.clone()
         acts = given.clone() if mode == P.EVAL else None
@@ -59,7 +59,7 @@ def test_critic_layouts_bit_identical(torch_gpu, n):
     reset = (torch.rand(T, n, device="cuda", generator=g) < 0.2).to(torch.uint8)
     carry0 = 0.5 * torch.randn(n, P.DEPTH, P.HIDDEN, device="cuda", generator=g)
     outs = []
-    for layout in (P.LAYOUT_BLOCK, P.LAYOUT_WAVE, P.LAYOUT_WAVE2):
+    for layout in (P.LAYOUT_BLOCK, P.LAYOUT_WAVE, P.LAYOUT_WAVE2, P.LAYOUT_WAVE4):
         pol = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=5), layout=layout)
         carry = carry0.clone()
         v = pol.critic(obs, carry, reset=reset)
