@@ -191,7 +191,7 @@ def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) 
     return out
 
 
-def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> dict:
+def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int, inloop_critic: int = 0) -> dict:
     """One PPO rollout per GPU end to end, everything before the PPO loss (SURVEY §8f f1 + f2):
     T control steps of GRU-actor sampling -> zb_step with the critic observations recorded
     (ksim rollout, sample_action train.py:1737-1763), the GRU critic over the T steps with the
@@ -209,11 +209,19 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int) -> d
     # the group chains (PolicyRollout.run(critic=...), one-wave layout) it measured slower,
     # 5.49 M vs 6.02 M env-steps/s (profiles/r02_v16d_bench_inloop_critic.json)
     critic = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=1), device=dev.index)
+    inloop = bool(inloop_critic) and hasattr(eng, "groups")
+    if inloop:  # --inloop-critic L: V(s_t) inside the group chains with policy layout L
+        critic.set_layout(inloop_critic)
     ro = P.PolicyRollout(eng, actor, seed=3)
     ro.reset()
     zeros = torch.zeros(1, n, dtype=torch.uint8, device=dev)
 
     def once():
+        if inloop:
+            cc = critic.initial_carry(n)
+            traj = ro.run(T, record_critic=True, critic=critic, critic_carry=cc)
+            return compute_ppo_inputs(traj["value"], traj["reward"], traj["done"], traj["success"],
+                                      bootstrap=traj["value_next"])
         traj = ro.run(T, record_critic=True)
         cc = critic.initial_carry(n)
         # V(s_t) on the states acted in (carry reset where an episode starts), then the
@@ -267,6 +275,9 @@ def main() -> None:
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
     ap.add_argument("--no-policy", action="store_true", help="skip the policy-in-the-loop leg")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end rollout-pipeline leg")
+    ap.add_argument("--inloop-critic", type=int, default=0,
+                    help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
+                         "(1 one-wave, 2 two-wave, 3 four-wave; DESIGN.md §4f); 0 = the 8-wave critic afterwards")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo rehearses the "
                          "multi-rank path on a one-GPU box, ranks sharing device local_rank %% device_count)")
@@ -396,7 +407,8 @@ def main() -> None:
             engp = EnvGroups(cm, cfg, n, groups=args.policy_groups, env_offset=rank * n, device=dev.index,
                              seed=args.seed)
     policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, engp)
-    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(engp or eng1, n, 32, 2, dev, world)
+    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(engp or eng1, n, 32, 2, dev, world,
+                                                                     args.inloop_critic)
 
     if rank == 0:
         value = world * n * args.steps / elapsed
