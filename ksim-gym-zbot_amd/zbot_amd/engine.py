@@ -283,7 +283,11 @@ class EnvGroups:
     The outputs are views into full [N, ...] buffers. step() returns them pending: work on the
     caller's stream that reads them must come after join(), which makes the current stream wait
     for every group's last launch. Calls that read or write engine state (reset, get_state, ...)
-    join first and run on the current stream; the next step() orders every group after them."""
+    join first and run on the current stream; the next step() orders every group after them.
+
+    The group streams come from one per-process set (group_streams). With HIP's default of four
+    hardware queues per process, up to three groups and the caller's stream get a queue each;
+    more groups share queues and run partly in series."""
 
     OUTPUTS = ("obs_actor", "obs_critic", "obs_extra", "reward_terms", "reward", "done", "success")
 
