@@ -34,34 +34,71 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int = 256, max_steps: int = 0) -> dict:
-    """Time the CPU oracle (fp32 C, OpenMP over envs) on a bounded sample (max_steps > 0: exactly
-    that many env-steps, the C1 rollout)."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
-    os.environ["OMP_NUM_THREADS"] = str(threads)
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O  # noqa: PLC0415  (cpu_baseline leg: the oracle is the CPU twin being timed)
+def host_cpu() -> dict:
+    """The host the CPU baseline ran on: logical CPUs, the ones this process may use, the model."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": model}
 
+
+def baseline_threads() -> int:
+    """OpenMP threads of the CPU twin: every CPU this process may run on (sched_getaffinity), unless
+    the host caps the job's CPU share through OMP_NUM_THREADS (the GPU box sets it to its
+    per-GPU share of 16 and asks jobs to keep it)."""
+    aff = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, cap) if cap > 0 else aff)
+
+
+def _time_twin(O, cm, cfg, n_envs: int, budget_s: float, max_steps: int, min_steps: int = 2):
     env = O.OracleEnv(cm.cmodel, cfg, n_envs, seed=0)
     env.reset()
     acts = [O.synthetic_actions(cm.cmodel, 0, n_envs, 0, t) for t in range(4)]
-    env.step(acts[0])  # warm-up (thread pool)
+    env.step(acts[0])  # warm-up (thread pool, first touch)
     steps = 0
     t0 = time.perf_counter()
     while True:
         env.step(acts[steps % 4])
         steps += 1
         el = time.perf_counter() - t0
-        if (max_steps and steps >= max_steps) or (not max_steps and el >= budget_s):
+        if (max_steps and steps >= max_steps) or (not max_steps and el >= budget_s and steps >= min_steps):
             break
-    return {
+    return steps, el
+
+
+def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int, max_steps: int = 0, c1_leg: bool = True) -> dict:
+    """Time the CPU twin (the oracle: fp32 C restatement, OpenMP over the env axis) on a bounded
+    sample of the headline workload: the same env count, as many env-steps as fit in budget_s
+    (max_steps > 0: exactly that many, the C1 rollout). With c1_leg, the reference's own
+    CPU-runnable case (C1: 64 envs x 128 env-steps) is timed beside it."""
+    threads = baseline_threads()
+    os.environ["OMP_NUM_THREADS"] = str(threads)  # read by the OpenMP runtime at the oracle's first load
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # noqa: PLC0415  (cpu_baseline leg: the oracle is the CPU twin being timed)
+
+    steps, el = _time_twin(O, cm, cfg, n_envs, budget_s, max_steps)
+    out = {
         "value": n_envs * steps / el,
         "unit": "env-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n_envs} envs x {steps} env-steps of the same workload ({workload}) on the oracle "
-                  f"(fp32 C restatement, OpenMP {threads} threads), {el:.1f} s",
+        "sample": f"{n_envs} envs x {steps} env-steps of the same workload ({workload}) on the CPU twin "
+                  f"(oracle/zb_oracle.c, fp32, OpenMP {threads} threads), {el:.1f} s",
+        "envs": n_envs,
+        "host": host_cpu(),
     }
+    if c1_leg:
+        s1, e1 = _time_twin(O, cm, cfg, 64, 0.0, 128)
+        out["c1"] = {"value": 64 * s1 / e1, "unit": "env-steps/s", "sample": f"64 envs x {s1} env-steps (C1), "
+                     f"{e1:.2f} s", "cores": threads}
+    return out
 
 
 def bench_ppo_inputs(n: int, T: int, reps: int, dev, world: int) -> dict:
@@ -125,6 +162,63 @@ def bench_ppo_inputs(n: int, T: int, reps: int, dev, world: int) -> dict:
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "zb::gae_kernel",
                      "algorithmic_bytes_per_unit": bpu, "unit_note": "one (step, env) element"},
+    }
+
+
+def bench_c2_rollout(eng, n: int, T: int, dev, rank: int, world: int, sigma: float = 0.2) -> dict:
+    """C2 as BASELINE.json states it: one T = 256-step rollout of all n envs, timed whole, with
+    automatic resets inside the window (actions JOINT_BIASES + sigma N(0,1), sigma = 0.2 as in the
+    soak test, so robots fall and episodes end), the reward / done rows of every step kept as a
+    [T, n] rollout buffer, and the FeetAirtime row 0 patched to ksim's trajectory form after the
+    last step (include/zbot.h zb_feet_airtime_exact)."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+    from zbot_amd import cstructs as cs  # noqa: PLC0415
+    from zbot_amd.constants import JOINT_BIASES  # noqa: PLC0415
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + rank)
+    bias = torch.tensor([b for _, b, _ in JOINT_BIASES], device=dev)
+    acts = bias + sigma * torch.randn(T, n, cs.NJ, device=dev, generator=g)
+    rew = torch.empty(T, n, device=dev)
+    done = torch.empty(T, n, dtype=torch.uint8, device=dev)
+    grouped = hasattr(eng, "groups")
+
+    def rollout():
+        eng.mark_rollout_start()
+        for t in range(T):  # zb_step writes the reward / done rows of the rollout buffer directly
+            eng.step(acts[t], extras=False, reward=rew[t], done=done[t])
+        eng.feet_airtime_exact(rew[0], None)
+        if grouped:
+            eng.join()
+
+    eng.reset(extras=False)
+    rollout()  # untimed: first use of the buffers
+    eng.reset(extras=False)
+    eng.get_stats(clear=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    rollout()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    wall = float(wall.item())
+    eng.check()
+    ends = int(done.sum().item())
+    assert bool(torch.isfinite(rew).all())
+    return {
+        "workload": f"C2 as stated: one {T}-step rollout of {n} envs per GPU from reset, actions JOINT_BIASES + "
+                    f"{sigma} N(0,1), automatic resets inside the window, [T, n] reward / done rows, FeetAirtime "
+                    "row 0 patched to ksim's trajectory form",
+        "env_steps_per_s": world * n * T / wall,
+        "ms_per_rollout": 1e3 * wall,
+        "rollout_steps": T,
+        "episodes_done": ends,
     }
 
 
@@ -275,6 +369,8 @@ def main() -> None:
     ap.add_argument("--no-ppo", action="store_true", help="skip the post-rollout PPO-inputs leg")
     ap.add_argument("--no-policy", action="store_true", help="skip the policy-in-the-loop leg")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end rollout-pipeline leg")
+    ap.add_argument("--no-c2-rollout", action="store_true",
+                    help="skip the C2-as-stated leg (one 256-step rollout with resets inside, timed whole)")
     ap.add_argument("--inloop-critic", type=int, default=0,
                     help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
                          "(1 one-wave, 2 two-wave, 3 four-wave; DESIGN.md §4f); 0 = the 8-wave critic afterwards")
@@ -337,15 +433,19 @@ def main() -> None:
     # objects / sets up the RCCL communicator, one-time costs that are not per-step work
     reduce_stats()
     eng.get_stats(clear=True)
+    stream = torch.cuda.current_stream(dev)
+    # per-launch HIP events on the stream each launch runs on (one per group and step); torch
+    # creates an event's HIP handle at its first record: do that here, not inside the timed loop
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+          for _ in range(args.steps)]
+    for evt in ev:
+        for a, b in evt:
+            a.record(stream)
+            b.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-
-    stream = torch.cuda.current_stream(dev)
-    # per-launch HIP events on the stream each launch runs on (one per group and step)
-    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
-          for _ in range(args.steps)]
     t0 = time.perf_counter()
     for t in range(args.steps):
         a_t = acts[(args.warmup + t) % acts.shape[0]]
@@ -368,12 +468,16 @@ def main() -> None:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     elapsed = float(el_t.item())
 
+    eng.check()  # no launch flagged its results invalid (zb_check)
     kern_ms = [a.elapsed_time(b) for evt in ev for a, b in evt]
     avg_ms = sum(kern_ms) / len(kern_ms)
+    wall_ms = 1e3 * elapsed / args.steps
     bpe = bytes_per_env_step(extras=False, terms=True)
-    # G launches of n/G envs run concurrently, one per group stream: the aggregate algorithmic
-    # rate is G x (bytes of n/G envs) / the average launch duration
-    achieved = bpe * n / (avg_ms * 1e-3) / 1e9
+    # G launches of n/G envs run concurrently, one per group stream. G x (bytes of n/G envs) / the
+    # average launch duration assumes they overlap fully; when they do not, the wall time per step
+    # is the longer one, so the rate is taken over max(launch average, wall time per step)
+    rate_ms = avg_ms if G == 1 else max(avg_ms, wall_ms)
+    achieved = bpe * n / (rate_ms * 1e-3) / 1e9
     iters = eng.solver_iters().float().mean().item()
 
     # HBM bytes per launch and issued fp32 FLOP per env-step from the separate
@@ -395,6 +499,7 @@ def main() -> None:
         with open(fpath) as f:
             algo_flop = json.load(f)["as_run"]["flops_per_env_step"]
 
+    c2_leg = None if args.no_c2_rollout else bench_c2_rollout(eng, n, 256, dev, rank, world)
     ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
     # the actor-in-the-loop legs: one handle on the current stream for the actor's kernel time, and
     # args.policy_groups env groups with the slot-sized two-wave actor
@@ -449,26 +554,28 @@ def main() -> None:
                 "traffic": traffic,
                 "kernel": "zb::step_kernel",
                 "kernel_avg_ms": avg_ms,
+                "rate_ms": rate_ms,
                 "concurrent_launches": G,
                 "envs_per_launch": n // G,
                 "traffic_note": "HBM bytes per n env-steps (one launch over all n envs in a separate rocprofv3 --pmc pass, "
-                                "FETCH_SIZE x2 + WRITE_SIZE); achieved = algorithmic bytes of the G concurrent launches / "
-                                "their average duration",
+                                "FETCH_SIZE x2 + WRITE_SIZE); achieved = algorithmic bytes of the n env-steps of a step / "
+                                "rate_ms: the average launch duration by HIP events on the launch's stream (G = 1), or with "
+                                "G concurrent group launches the larger of that and the wall time per step",
                 "algorithmic_bytes_per_env_step": bpe,
                 "note": "the path is FP32-VALU/latency bound (DESIGN.md §Roofline); HBM fraction reported as required",
             },
             "roofline_fp32": None if algo_flop is None else {
                 "bound": "fp32-valu",
-                "achieved": algo_flop * n / (avg_ms * 1e-3) / 1e12,
+                "achieved": algo_flop * n / (rate_ms * 1e-3) / 1e12,
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": algo_flop * n / (avg_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                "frac": algo_flop * n / (rate_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
                 "algorithmic_flop_per_env_step": algo_flop,
                 "issued_flop_per_env_step": flop_per_env_step,
                 "issued_achieved": None if flop_per_env_step is None else
-                flop_per_env_step * n / (avg_ms * 1e-3) / 1e12,
+                flop_per_env_step * n / (rate_ms * 1e-3) / 1e12,
                 "note": "achieved = algorithmic FLOPs per env-step (counted by the instrumented CPU twin on the C2 "
-                        "workload, FMA=2, profiles/r02_flops_count.json) x envs / kernel time; issued = PMC "
+                        "workload, FMA=2, profiles/r02_flops_count.json) x envs / rate_ms (as roofline); issued = PMC "
                         "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 lane-FLOP; the binding resource of this "
                         "latency/VALU-bound kernel",
             },
@@ -477,6 +584,8 @@ def main() -> None:
                 "mean_return": float((total_stats[0] / total_stats[2].clamp(min=1)).item()),
             },
         }
+        if c2_leg is not None:
+            out["c2_rollout"] = c2_leg
         if ppo_leg is not None:
             out["ppo_inputs"] = ppo_leg
         if policy_leg is not None:
@@ -485,9 +594,10 @@ def main() -> None:
             out["rollout_pipeline"] = pipe_leg
         if world == 1 and not args.no_cpu_baseline:
             if args.config == "c1":  # the whole C1 rollout on the CPU twin: 64 envs x 128 env-steps
-                out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, "C1", n_envs=n, max_steps=128)
-            else:
-                out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper())
+                out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, "C1", n_envs=n, max_steps=128,
+                                                   c1_leg=False)
+            else:  # the headline's env count (C2: 8192), a bounded number of env-steps
+                out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper(), n_envs=n)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

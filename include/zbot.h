@@ -44,6 +44,7 @@ extern "C" {
 #define ZB_EDEVICE    -2   /* HIP runtime error (device, alloc, copy) */
 #define ZB_ELAUNCH    -3   /* kernel launch failure */
 #define ZB_EMODEL     -4   /* model outside the engine's limits */
+#define ZB_ESTATE     -5   /* a launch flagged its results invalid (zb_check) */
 
 typedef struct ZbHandle ZbHandle;
 
@@ -119,6 +120,32 @@ int zb_rollout(ZbHandle* h, const float* actions, int n_steps,
                uint8_t* done, uint8_t* success, float curriculum_level,
                void* stream);
 
+/*
+ * ksim's FeetAirtimeReward, exactly, over a rollout of T steps
+ * (FeetAirtimeReward.get_reward_stateful, train.py:515-546, evaluated by ksim
+ * on the whole (T, ...) trajectory after the rollout).
+ *
+ * zb_step's FeetAirtime term is the causal per-step form
+ * Σ_feet (air[t-1] − penalty)·[c_t ∧ ¬c_{t-1}]. That is ksim's term for every
+ * t ≥ 1. At t = 0 ksim takes the previous contact as False
+ * (`concatenate([False], c[:-1])`, train.py:527) and the airtime of
+ * `roll(air, 1)` (train.py:533-534), i.e. air[T-1], known only after the last
+ * step. To get ksim's rows:
+ *   zb_mark_rollout_start(h);            before the rollout's first zb_step
+ *                                        (or zb_rollout); host-side flag only
+ *   ... T x zb_step ...
+ *   zb_feet_airtime_exact(h, reward[0], reward_terms[0], level, stream);
+ * which adds scale·(ksim term − causal term) to reward0[e] and writes ksim's
+ * term into reward_terms0[e][ZB_T_FEET_AIRTIME] (either pointer nullable;
+ * reward0 may be zb_rollout's reward_sum, the patch is additive). Rows t ≥ 1
+ * are untouched. curriculum_level is the level the first step ran at.
+ * ZB_EARG if no marked step ran since the mark (or the rollout was already
+ * patched). Added in ABI version 3.
+ */
+int zb_mark_rollout_start(ZbHandle* h);
+int zb_feet_airtime_exact(ZbHandle* h, float* reward0, float* reward_terms0,
+                          float curriculum_level, void* stream);
+
 /* Persistent state access: [n_envs, ZB_STATE_STRIDE] fp32 words (device).
  * get copies out, set copies in (checkpoint / parity tests). */
 int zb_get_state(ZbHandle* h, float* state_dev, void* stream);
@@ -130,6 +157,13 @@ int zb_set_rand(ZbHandle* h, const float* rand_dev, void* stream);
 /* Episode statistics [n_envs, ZB_NUM_STATS] accumulated by zb_step since the
  * last clear (deterministic per-env partials for the cross-GPU reduction). */
 int zb_get_stats(ZbHandle* h, float* stats_dev, int clear, void* stream);
+
+/* Synchronising health check: waits for the device, then reports ZB_ESTATE if a chunked
+ * zb_step since the last check timed out waiting for a predecessor chunk (never
+ * observed: the wait is bounded only as a guard). The unit that timed out stored no state, so the
+ * envs' rows are stale and the launch's outputs invalid; the chunk counters are cleared for the
+ * next launch. */
+int zb_check(ZbHandle* h);
 
 /* Solver diagnostics: total solver iterations of the last launch summed over
  * its substeps, per env ([n_envs] int32, device). */

@@ -54,7 +54,9 @@ extern "C" {
 #define ZB_S_PREV_CONT   170  /* [2]   contact flags of the previous step (touchdown) */
 #define ZB_S_EPISODE     172  /* u32   episode index of this env (RNG counter) */
 #define ZB_S_NAN         173  /* u32   sticky non-finite flag (diagnostic) */
-#define ZB_S_END         174
+#define ZB_S_AIR0_CONT   174  /* u32   first step of a marked rollout: contact bits (1 left, 2 right) */
+#define ZB_S_AIR0_TERM   175  /*       ... and its causal FeetAirtime term (zb_feet_airtime_exact) */
+#define ZB_S_END         176
 
 /* -------------- per-env randomized model parameters (config 5) -------------- */
 /* ksim randomizers named in train.py:1441-1454; sampled on every episode reset  */

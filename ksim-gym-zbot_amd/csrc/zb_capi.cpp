@@ -18,7 +18,12 @@
 
 #include "zb_internal.h"
 
-#define ZB_ABI_VERSION 2
+using zb::build_topology;
+using zb::check_cfg;
+using zb::check_model;
+using zb::fail;
+
+#define ZB_ABI_VERSION 3
 
 struct ZbHandle {
   int device;
@@ -38,6 +43,8 @@ struct ZbHandle {
   uint32_t* sched; /* chunked step: [2 + npair] counters and per-pair progress (zb_internal.h) */
   int32_t* itpart; /* chunked step: [n] Newton iterations so far */
   int nchunk;      /* work units per pair of envs in zb_step (1: unchunked) */
+  int air_mark;    /* zb_mark_rollout_start: the next zb_step / zb_rollout is a rollout's step 0 */
+  int air_marked;  /* a marked step has been launched since the last zb_feet_airtime_exact */
 };
 
 /* Chunks per control step for zb_step. The launch runs its pairs of envs in
@@ -63,18 +70,6 @@ static int choose_chunks(int n_envs, int n_substeps, int resident) {
   return k < 1 ? 1 : k;
 }
 
-static thread_local std::string g_err;
-
-static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-static int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
 #define HIPCHK(expr)                                                                       \
   do {                                                                                     \
     hipError_t _e = (expr);                                                                \
@@ -95,185 +90,6 @@ size_t zb_model_struct_bytes(void) { return sizeof(ZbModel); }
 size_t zb_config_struct_bytes(void) { return sizeof(ZbEnvConfig); }
 int zb_state_stride(void) { return ZB_STATE_STRIDE; }
 int zb_rand_stride(void) { return ZB_RAND_STRIDE; }
-const char* zb_last_error(void) { return g_err.c_str(); }
-
-void zb_default_config(ZbEnvConfig* c) {
-  if (!c) return;
-  memset(c, 0, sizeof *c);
-  const double PI = 3.14159265358979323846;
-  c->struct_bytes = (int32_t)sizeof(ZbEnvConfig);
-  c->flags = ZB_F_OBS_NOISE | ZB_F_AUTORESET;
-  c->n_substeps = 20;
-  c->iterations = 8;
-  c->ls_iterations = 8;
-  c->dt = 0.001f;
-  c->ctrl_dt = 0.02f;
-  c->tolerance = 1e-8f;
-  c->ls_tolerance = 0.01f;
-  c->imu_noise_std = (float)(PI / 180.0);
-  c->acc_noise_std = 0.5f;
-  c->reset_qvel_scale = 0.01f;
-  c->max_episode_sec = 80.f;
-  c->lag_range[0] = 0.f; c->lag_range[1] = 0.1f;
-  c->bad_z[0] = 0.05f; c->bad_z[1] = 0.5f;
-  c->max_tilt_rad = (float)(60.0 * PI / 180.0);
-  c->push_linvel[0] = 0.1f; c->push_linvel[1] = 0.1f; c->push_linvel[2] = 0.05f;
-  c->push_interval[0] = 2.f; c->push_interval[1] = 4.f;
-  c->push_vel_range[0] = 0.05f; c->push_vel_range[1] = 0.15f;
-  const float scales[ZB_NUM_TERMS] = {1.0f, 1.0f, 5.0f, 0.3f, -2.0f, 0.3f, 2.5f, 0.3f, -0.5f, -0.5f, -0.05f, -2.0f};
-  const int by_cur[ZB_NUM_TERMS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1};
-  for (int i = 0; i < ZB_NUM_TERMS; i++) {
-    c->reward_scale[i] = scales[i];
-    c->reward_by_curriculum[i] = by_cur[i];
-  }
-  c->feet_airtime_touchdown_penalty = 0.3f;
-  c->naive_forward_clip_max = 0.2f;
-  c->feet_orient_error_scale = 0.25f;
-  c->feet_too_close_threshold = 0.12f;
-  c->touch_threshold = 0.1f;
-  c->stay_alive_balance = 10.f;
-  c->rand_mass[0] = 0.95f; c->rand_mass[1] = 1.15f;
-  c->rand_armature[0] = 1.0f; c->rand_armature[1] = 1.05f;
-  c->rand_damping[0] = 0.95f; c->rand_damping[1] = 1.05f;
-  c->rand_friction[0] = 0.5f; c->rand_friction[1] = 1.5f;
-  c->rand_qpos0[0] = (float)(-2.0 * PI / 180.0); c->rand_qpos0[1] = (float)(2.0 * PI / 180.0);
-  c->rand_floor_mu[0] = 0.3f; c->rand_floor_mu[1] = 1.5f;
-  c->rand_imu_tilt_std = (float)(5.0 * PI / 180.0);
-  c->rand_imu_yaw_std = (float)(1.0 * PI / 180.0);
-  c->rand_imu_pos_std = 0.005f;
-}
-
-static int check_model(const ZbModel* m) {
-  if (m->magic != ZB_MODEL_MAGIC) return fail(ZB_EARG, "model magic mismatch");
-  if (m->version != ZB_MODEL_VERSION) return fail(ZB_EARG, "model version %d != %d", m->version, ZB_MODEL_VERSION);
-  if (m->struct_bytes != (int32_t)sizeof(ZbModel))
-    return fail(ZB_EARG, "model struct_bytes %d != %zu (layout mismatch)", m->struct_bytes, sizeof(ZbModel));
-  if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
-    return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
-  if (m->ngeom * ZB_CON_PER_GEOM * 4 > 32)
-    return fail(ZB_EMODEL, "ngeom=%d: contact rows exceed the 32-lane team", m->ngeom);
-  if (m->max_depth > ZB_MAX_DEPTH) return fail(ZB_EMODEL, "dof depth %d > %d", m->max_depth, ZB_MAX_DEPTH);
-  if (m->nu != ZB_NJ || m->nbody != ZB_NBODY_TASK)
-    return fail(ZB_EMODEL, "task layout needs nu=%d nbody=%d (got %d, %d)", ZB_NJ, ZB_NBODY_TASK, m->nu, m->nbody);
-  if (m->body_jnttype[1] != ZB_JNT_FREE) return fail(ZB_EMODEL, "body 1 must carry the free joint");
-  int maxbd = 0;
-  for (int b = 0; b < m->nbody; b++) {
-    if (m->body_depth[b] > maxbd) maxbd = m->body_depth[b];
-    int nch = 0;
-    for (int c = 1; c < m->nbody; c++)
-      if (m->body_parent[c] == b) nch++;
-    if (nch > 8) return fail(ZB_EMODEL, "body %d has %d children (max 8)", b, nch);
-    /* subtree sums are chain suffix sums below the base (zb_engine.hip subtree_sum) */
-    if (b != 1 && nch > 1) return fail(ZB_EMODEL, "body %d branches (%d children): only the base may", b, nch);
-  }
-  if (maxbd > 15) return fail(ZB_EMODEL, "body depth %d > 15", maxbd);
-  /* dof tree shape the factorization relies on (zb_engine.hip factor_ldl):
-     a root chain 0..R-1 (R <= 6, one dof per top elimination level) and
-     unbranched limb chains of consecutive dofs hanging off dof R-1 */
-  int nroot = 0;
-  for (int k = 0; k < 6 && k < m->nlevel; k++) {
-    const int lv = m->nlevel - 1 - k;
-    if (m->level_nmem[lv] == 1 && m->level_mem[lv][0] == k && m->dof_depth[k] == k) nroot++;
-    else break;
-  }
-  if (nroot != 6) return fail(ZB_EMODEL, "dof tree: the free joint's 6 dofs must form the root chain (got %d)", nroot);
-  if (m->nv != 6 + ZB_NJ) return fail(ZB_EMODEL, "task layout needs nv=%d (got %d)", 6 + ZB_NJ, m->nv);
-  /* depths / counts the engine is compiled for (zb_engine.hip NGEOM, MAXBD, MAXDD, NLIMBLV) */
-  if (m->ngeom != 2 || maxbd != 8 || m->max_depth != 12 || m->nlevel != 12)
-    return fail(ZB_EMODEL, "engine compiled for ngeom 2, body depth 8, dof depth 12, 12 levels (got %d, %d, %d, %d)",
-                m->ngeom, maxbd, m->max_depth, m->nlevel);
-  for (int k = nroot; k < m->nv; k++) {
-    const int p = m->dof_parent[k];
-    int nchild_prev = 0;
-    for (int j = nroot; j < m->nv; j++) nchild_prev += (m->dof_parent[j] == k - 1);
-    const bool head = p == nroot - 1;
-    const bool cont = p == k - 1 && k - 1 >= nroot && nchild_prev == 1;
-    if (!head && !cont)
-      return fail(ZB_EMODEL, "dof %d: limbs must be unbranched chains of consecutive dofs off dof %d", k, nroot - 1);
-  }
-  return ZB_OK;
-}
-
-static int check_cfg(const ZbEnvConfig* c) {
-  if (c->struct_bytes != (int32_t)sizeof(ZbEnvConfig))
-    return fail(ZB_EARG, "config struct_bytes %d != %zu", c->struct_bytes, sizeof(ZbEnvConfig));
-  if (c->n_substeps < 1 || c->iterations < 0 || c->ls_iterations < 0 || !(c->dt > 0.f))
-    return fail(ZB_EARG, "invalid solver/timestep configuration");
-  return ZB_OK;
-}
-
-/* The per-lane roles of a 32-lane team (body lane, dof lane, limb-chain position, contact
-   rows holding the dof, actuator), computed once here instead of by every wave at the top
-   of every launch. Field-major [TP_NF][32]; the checks of check_model hold. */
-static void build_topology(const ZbModel* m, int32_t t[zb::TP_NF][zb::TOPO_LANES]) {
-  using namespace zb;
-  const int NB = ZB_NBODY_TASK, NV = 6 + ZB_NJ;
-  memset(t, 0, sizeof(int32_t) * TP_NF * TOPO_LANES);
-  int nch_of[TOPO_LANES], bdep_of[TOPO_LANES];
-  for (int l = 0; l < TOPO_LANES; l++) {
-    const bool isb = l < NB;
-    t[TP_BPAR][l] = isb ? m->body_parent[l] : 0;
-    t[TP_BDEP][l] = bdep_of[l] = isb ? m->body_depth[l] : 1000;
-    t[TP_BJT][l] = isb ? m->body_jnttype[l] : ZB_JNT_NONE;
-    t[TP_BDOFADR][l] = isb ? m->body_dofadr[l] : -1;
-    t[TP_BLAST][l] = isb ? m->body_lastdof[l] : -1;
-    int nch = 0;
-    uint32_t ch0 = 0, ch1 = 0;
-    for (int b = 1; b < NB; b++)
-      if (isb && m->body_parent[b] == l && nch < 8) {
-        if (nch < 4) ch0 |= (uint32_t)b << (8 * nch);
-        else ch1 |= (uint32_t)b << (8 * (nch - 4));
-        nch++;
-      }
-    t[TP_NCH][l] = nch_of[l] = nch;
-    t[TP_CH0][l] = (int32_t)ch0;
-    t[TP_CH1][l] = (int32_t)ch1;
-  }
-  /* per body depth: the largest child count among the bodies at that depth (4 bits each) */
-  uint64_t lv = 0;
-  for (int d = 0; d <= TOPO_MAXBD && d < 16; d++) {
-    int mx = 0;
-    for (int l = 0; l < TOPO_LANES; l++)
-      if (bdep_of[l] == d && nch_of[l] > mx) mx = nch_of[l];
-    lv |= (uint64_t)(mx & 0xf) << (4 * d);
-  }
-  for (int l = 0; l < TOPO_LANES; l++) {
-    t[TP_LVL_LO][l] = (int32_t)(uint32_t)lv;
-    t[TP_LVL_HI][l] = (int32_t)(uint32_t)(lv >> 32);
-    const bool isd = l < NV;
-    const int ddep = isd ? m->dof_depth[l] : 0;
-    const int dbody = isd ? m->dof_body[l] : 0;
-    t[TP_DDEP][l] = ddep;
-    t[TP_DBODY][l] = dbody;
-    t[TP_QADR][l] = isd ? m->dof_qposadr[l] : -1;
-    int act = -1;
-    for (int a = 0; a < m->nu; a++)
-      if (isd && m->act_dof[a] == l) act = a;
-    t[TP_ACT][l] = act;
-    uint32_t desc = 0;
-    for (int k = 0; k < NV; k++)
-      if (isd && k != l && m->dof_depth[k] > ddep && m->dof_anc[k][ddep] == l) desc |= 1u << k;
-    uint32_t rm = 0;
-    for (int g = 0; g < TOPO_NGEOM; g++) {
-      const int kd = m->body_lastdof[m->geom_body[g]];
-      if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm |= 0xFFFFu << (16 * g);
-    }
-    t[TP_ROWMASK][l] = (int32_t)rm;
-    t[TP_DK0][l] = isd ? l - m->body_dofadr[dbody] : 0;
-    t[TP_DFREE][l] = (isd && m->body_jnttype[dbody] == ZB_JNT_FREE) ? 1 : 0;
-    int hd = -1, ln = 0;
-    if (isd && l >= TOPO_NROOT) {
-      hd = l;
-      while (m->dof_parent[hd] >= TOPO_NROOT) hd = m->dof_parent[hd];
-      int k = hd;
-      while (k + 1 < NV && m->dof_parent[k + 1] == k) k++;
-      ln = k - hd + 1;
-    }
-    t[TP_CHD][l] = hd;
-    t[TP_CPS][l] = hd >= 0 ? l - hd : 0;
-    t[TP_CLN][l] = ln;
-  }
-}
 
 int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_offset, int device, uint64_t seed,
               ZbHandle** out) {
@@ -313,13 +129,19 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMemset(h->rnd, 0, n * ZB_RAND_STRIDE * sizeof(float));
   if (e == hipSuccess) e = hipMemset(h->stats, 0, n * ZB_NUM_STATS * sizeof(float));
   if (e == hipSuccess) e = hipMemset(h->iters, 0, n * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc(&h->sched, (2 + (n + 1) / 2) * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemset(h->sched, 0, (2 + (n + 1) / 2) * sizeof(uint32_t));
+  /* [0] units taken, [1] pairs finished, [2 + pair] per-pair progress, [2 + npair] sticky error */
+  if (e == hipSuccess) e = hipMalloc(&h->sched, (3 + (n + 1) / 2) * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(h->sched, 0, (3 + (n + 1) / 2) * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&h->itpart, n * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(h->itpart, 0, n * sizeof(int32_t));
   h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device));
 #if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
-  if (e == hipSuccess) e = hipMalloc(&h->stamps, n * ZB_NSTAMP * sizeof(unsigned long long));
+  {
+    /* phase stamps: ZB_NSTAMP per env; wave times: 4 words per (chunk, pair), up to one chunk per
+       substep (zb_set_step_chunks clamps to n_substeps) */
+    size_t words = n * ZB_NSTAMP, wt = 4 * (size_t)cfg->n_substeps * ((n + 1) / 2);
+    if (e == hipSuccess) e = hipMalloc(&h->stamps, (words > wt ? words : wt) * sizeof(unsigned long long));
+  }
 #endif
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
@@ -402,8 +224,11 @@ int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_criti
   a.success = success;
   a.curriculum = curriculum_level;
   a.nchunk = h->nchunk;
+  a.air_mark = h->air_mark;
   hipError_t e = zb::launch_step(a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_step launch: %s", hipGetErrorString(e));
+  if (h->air_mark) h->air_marked = 1;
+  h->air_mark = 0;
   return ZB_OK;
 }
 
@@ -421,8 +246,36 @@ int zb_rollout(ZbHandle* h, const float* actions, int n_steps, float* obs_actor,
   a.done = done;
   a.success = success;
   a.curriculum = curriculum_level;
+  a.air_mark = h->air_mark;
   hipError_t e = zb::launch_step(a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_rollout launch: %s", hipGetErrorString(e));
+  if (h->air_mark) h->air_marked = 1;
+  h->air_mark = 0;
+  return ZB_OK;
+}
+
+int zb_mark_rollout_start(ZbHandle* h) {
+  if (!h) return fail(ZB_EARG, "zb_mark_rollout_start: null handle");
+  h->air_mark = 1;
+  h->air_marked = 0;
+  return ZB_OK;
+}
+
+int zb_feet_airtime_exact(ZbHandle* h, float* reward0, float* reward_terms0, float curriculum_level, void* stream) {
+  if (!h) return fail(ZB_EARG, "zb_feet_airtime_exact: null handle");
+  if (!h->air_marked)
+    return fail(ZB_EARG, "zb_feet_airtime_exact: no step of a marked rollout since zb_mark_rollout_start "
+                         "(or already patched)");
+  if (!(curriculum_level == curriculum_level)) return fail(ZB_EARG, "zb_feet_airtime_exact: curriculum is NaN");
+  int rc = use_device(h);
+  if (rc) return rc;
+  zb::StepArgs a = base_args(h);
+  a.reward = reward0;
+  a.reward_terms = reward_terms0;
+  a.curriculum = curriculum_level;
+  hipError_t e = zb::launch_airtime_exact(a, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_feet_airtime_exact launch: %s", hipGetErrorString(e));
+  h->air_marked = 0;
   return ZB_OK;
 }
 
@@ -466,6 +319,23 @@ int zb_set_step_chunks(ZbHandle* h, int k) {
     h->nchunk = choose_chunks(h->n, h->cfg.n_substeps, zb::step_resident_blocks(h->device));
   } else {
     h->nchunk = k > h->cfg.n_substeps ? h->cfg.n_substeps : k;
+  }
+  return ZB_OK;
+}
+
+int zb_check(ZbHandle* h) {
+  if (!h) return fail(ZB_EARG, "zb_check: null handle");
+  int rc = use_device(h);
+  if (rc) return rc;
+  const size_t npair = ((size_t)(h->n > 0 ? h->n : 1) + 1) / 2;
+  uint32_t err = 0;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(&err, h->sched + 2 + npair, sizeof err, hipMemcpyDeviceToHost));
+  if (err) {
+    /* the chunk counters may be left mid-protocol: clear them so the next launch starts clean */
+    HIPCHK(hipMemset(h->sched, 0, (3 + npair) * sizeof(uint32_t)));
+    return fail(ZB_ESTATE, "a chunked zb_step timed out waiting for a predecessor chunk: the state of the "
+                           "launches since the last zb_check is invalid (zb_set_state / zb_reset to recover)");
   }
   return ZB_OK;
 }

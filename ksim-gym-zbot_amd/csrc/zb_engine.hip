@@ -484,6 +484,9 @@ __device__ __forceinline__ void stu_cg(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ uint32_t addu_cg(uint32_t* p, uint32_t v) {
   return __hip_atomic_fetch_add((guint_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void maxu_cg(uint32_t* p, uint32_t v) {
+  (void)__hip_atomic_fetch_max((guint_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 /* ------------------------ RNG: threefry2x32-20 (Random123) ------------------ */
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -2360,7 +2363,7 @@ __device__ __forceinline__ void quat_roll_pitch(const float q_[4], float& roll, 
 
 /* terminations + reward terms (train.py:1546-1593) ; returns done */
 __device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, const BodyK& B, float cur, float* terms_out,
-                        float& total, bool& fail) {
+                        float& total, bool& fail, float& airtime_term) {
   MP m = c.m;
   CP cfg = c.cfg;
   const int l = c.l;
@@ -2400,6 +2403,7 @@ __device__ __forceinline__ bool rewards(const Ctx& c, EnvS& s, const LaneS& ls, 
       s.prev_cont[sd] = cont[sd] ? 1.f : 0.f;
     }
     t[ZB_T_FEET_AIRTIME] = rr;
+    airtime_term = rr;
   }
   {
     float ql[4], qr[4];
@@ -2649,13 +2653,22 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
     ch = (int)(u / (uint32_t)npair);
     pair = (int)(u - (uint32_t)ch * (uint32_t)npair);
     if (ch > 0) {
-      /* bounded: a wait that outlives ~2 s gives up and marks the env's iteration count */
+      /* bounded: a wait that outlives ~2 s gives up. That is fatal for the launch: the sticky
+         error word sched[2 + npair] is raised (zb_check reports it to the host), the env's
+         iteration count is marked, and this unit stores no state (it would have run on the
+         predecessor's unpublished row) */
       for (uint32_t spins = 0; ldu_cg(a.sched + 2 + pair) < (uint32_t)ch; spins++) {
         if (spins > (1u << 23)) {
           timed_out = true;
           break;
         }
         __builtin_amdgcn_s_sleep(4);
+      }
+      if (timed_out) {
+        if (threadIdx.x == 0) stu_cg(a.sched + 2 + npair, 1u);
+      } else {
+        /* the predecessor's state stores happen-before the loads below */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
     }
   }
@@ -2737,8 +2750,17 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
         }
         bool fail;
         float* terms = (live && a.reward_terms && !rollout) ? a.reward_terms + (size_t)vopq(e) * ZB_NUM_TERMS : nullptr;
-        done = rewards(c, s, ls, B, a.curriculum, terms, total, fail);
+        float air_term;
+        done = rewards(c, s, ls, B, a.curriculum, terms, total, fail, air_term);
         success = done && !fail;
+        if (a.air_mark && t == 0 && live && c.l == 0) {
+          /* first step of a rollout: its contact flags and causal FeetAirtime term, for the
+             exact ksim form patched in after the rollout (airtime_exact_kernel) */
+          float* st = state_row();
+          const uint32_t bits = (s.prev_cont[0] > 0.5f ? 1u : 0u) | (s.prev_cont[1] > 0.5f ? 2u : 0u);
+          st_cg<true>(st + ZB_S_AIR0_CONT, bitsf(bits));
+          st_cg<true>(st + ZB_S_AIR0_TERM, air_term);
+        }
         rsum += total;
         if (live && a.stats && c.l == 0) {
           float* sp = a.stats + (size_t)vopq(e) * ZB_NUM_STATS;
@@ -2784,16 +2806,17 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   } else if (live && a.iters && c.l == 0) {
     a.iters[vopq(e)] = iters;
   }
-  if (live) {
+  if (live && !timed_out) {
     if (K > 1) store_state<true>(c, s, ls, state_row());
     else store_state<false>(c, s, ls, state_row());
   }
   if (K > 1) {
-    /* publish: every store of this wave has completed before lane 0's flag store */
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    /* publish: every state store of this wave happens-before lane 0's flag store */
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (threadIdx.x == 0) {
       if (partial) {
-        stu_cg(a.sched + 2 + pair, (uint32_t)(ch + 1));
+        /* atomic max: a late publish never lowers a flag a later chunk already advanced */
+        maxu_cg(a.sched + 2 + pair, (uint32_t)(ch + 1));
       } else {
         /* last chunk: leave the pair's flag and (after the last pair's last chunk, when every
            unit has been taken) both counters at zero for the next launch */
@@ -2951,6 +2974,39 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(step_kernel, grid, block, 0, s, b);
   return hipGetLastError();
 }
+/* ksim's FeetAirtimeReward over one trajectory (train.py:503-546), row 0. The fused step
+   computes the causal form, Σ_feet (air[t-1] - penalty) · [c_t ∧ ¬c_{t-1}], which is ksim's term
+   for every t ≥ 1: the airtime scan (contact-or-done zeroes it, else + ctrl_dt) and the touchdown
+   test are the same recurrences. Row 0 differs: ksim's touchdown takes prev = False at t = 0
+   (`concatenate([False], c[:-1])`) and its airtime is `roll(air, 1)`, which reads air[T-1], the
+   airtime after the trajectory's last step. The first step of a marked rollout saved c_0 and its
+   causal term in the state row (ZB_S_AIR0_*); the state row now holds air[T-1]. One lane per env:
+   term0 = Σ_feet c_0 · (air[T-1] - penalty), added to reward0 as scale · (term0 - causal0) and
+   written over reward_terms0's FeetAirtime slot. */
+__global__ __launch_bounds__(256) void airtime_exact_kernel(const float* __restrict__ state, const ZbEnvConfig* cfg,
+                                                            int n, float curriculum, float* reward0, float* terms0) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float* st = state + (size_t)e * ZB_STATE_STRIDE;
+  const uint32_t bits = fbits(st[ZB_S_AIR0_CONT]);
+  const float causal = st[ZB_S_AIR0_TERM];
+  const float pen = cfg->feet_airtime_touchdown_penalty;
+  float term = 0.f;
+  term += (st[ZB_S_AIRTIME] - pen) * ((bits & 1u) ? 1.f : 0.f);
+  term += (st[ZB_S_AIRTIME + 1] - pen) * ((bits & 2u) ? 1.f : 0.f);
+  const float sc = cfg->reward_scale[ZB_T_FEET_AIRTIME] * (cfg->reward_by_curriculum[ZB_T_FEET_AIRTIME] ? curriculum : 1.f);
+  if (reward0) reward0[e] += sc * (term - causal);
+  if (terms0) terms0[(size_t)e * ZB_NUM_TERMS + ZB_T_FEET_AIRTIME] = term;
+}
+
+hipError_t launch_airtime_exact(const StepArgs& a, hipStream_t s) {
+  if (a.n_envs <= 0) return hipSuccess;
+  dim3 grid((unsigned)((a.n_envs + 255) / 256)), block(256);
+  hipLaunchKernelGGL(airtime_exact_kernel, grid, block, 0, s, (const float*)a.state, a.cfg, a.n_envs, a.curriculum,
+                     a.reward, a.reward_terms);
+  return hipGetLastError();
+}
+
 hipError_t launch_reset(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);

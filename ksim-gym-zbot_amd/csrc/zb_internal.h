@@ -11,6 +11,7 @@
 #include "zbot.h"
 #include "zbot_policy.h"
 #include "zbot_ppo.h"
+#include "zb_host.h"
 
 /* debug forward dump layout (zb_debug_forward), fp32 words per env */
 #define ZB_DBG_QM      0     /* [nv*nv] dense symmetric mass matrix */
@@ -25,18 +26,6 @@
 #define ZB_NSTAMP      20    /* phase-stamp slots of the -DZB_STAMPS build (zb_engine.hip S_*) */
 
 namespace zb {
-
-/* per-lane topology of a team (32 lanes), built once by zb_create from the model
-   (zb_capi.cpp build_topology) and read by the kernels' make_ctx: field-major
-   [TP_NF][32] int32 */
-enum {
-  TP_BPAR, TP_BDEP, TP_BJT, TP_BDOFADR, TP_BLAST, TP_NCH, TP_CH0, TP_CH1, TP_LVL_LO, TP_LVL_HI,
-  TP_DDEP, TP_DBODY, TP_QADR, TP_ACT, TP_ROWMASK, TP_DK0, TP_DFREE, TP_CHD, TP_CPS, TP_CLN, TP_NF
-};
-constexpr int TOPO_LANES = 32;
-constexpr int TOPO_NROOT = 6;  /* root dof chain (the free joint), zb_engine.hip NROOT */
-constexpr int TOPO_NGEOM = 2;  /* foot geoms, zb_engine.hip NGEOM */
-constexpr int TOPO_MAXBD = 8;  /* deepest body, zb_engine.hip MAXBD */
 
 struct StepArgs {
   const ZbModel* model;     /* device copy */
@@ -66,6 +55,7 @@ struct StepArgs {
   int nchunk;               /* 1: one workgroup per pair runs all substeps */
   uint32_t* sched;          /* [2 + npair]: units taken, pairs finished, per-pair chunks done */
   int32_t* itpart;          /* [n] Newton iterations of the chunks so far */
+  int air_mark;             /* first step of a rollout: save its contacts + causal airtime term */
 };
 
 /* workgroups of step_kernel resident on the device at once (occupancy x CUs) */
@@ -74,6 +64,9 @@ int step_resident_blocks(int device);
 hipError_t launch_step(const StepArgs& a, hipStream_t s);
 hipError_t launch_reset(const StepArgs& a, hipStream_t s);
 hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s);
+/* exact ksim FeetAirtime row 0 of a marked rollout (a.state, a.cfg, a.n_envs, a.curriculum,
+   a.reward = reward row 0 or null, a.reward_terms = terms row 0 or null) */
+hipError_t launch_airtime_exact(const StepArgs& a, hipStream_t s);
 
 /* post-rollout PPO inputs (zb_ppo.hip, include/zbot_ppo.h) */
 struct GaeArgs {

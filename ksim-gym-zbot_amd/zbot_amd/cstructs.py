@@ -51,7 +51,9 @@ S_RNG_STEP = 169
 S_PREV_CONT = 170
 S_EPISODE = 172
 S_NAN = 173
-S_END = 174
+S_AIR0_CONT = 174
+S_AIR0_TERM = 175
+S_END = 176
 
 RAND_STRIDE = 160
 R_MASS = 0

@@ -21,12 +21,13 @@ def shard(global_envs: int, world: int, rank: int) -> tuple[int, int]:
     return rank * n, n
 
 
-def reduce_episode_stats(stats_local, group=None):
-    """[n_local, 4] per-env statistics -> [4] float64 global sums (every rank)."""
+def reduce_fixed_order(part, group=None):
+    """A per-rank float64 partial -> the sum over ranks, the same bits on every rank: all_gather
+    (RCCL over xGMI on GPUs, gloo on CPU) and a rank-order sum, whatever algorithm the collective
+    picks. Without an initialised process group: the partial itself."""
     import torch  # noqa: PLC0415
     import torch.distributed as dist  # noqa: PLC0415
 
-    part = stats_local.double().sum(0)
     if not dist.is_available() or not dist.is_initialized():
         return part
     world = dist.get_world_size(group)
@@ -36,6 +37,11 @@ def reduce_episode_stats(stats_local, group=None):
     for p in parts[1:]:
         total += p
     return total
+
+
+def reduce_episode_stats(stats_local, group=None):
+    """[n_local, 4] per-env statistics -> [4] float64 global sums (every rank)."""
+    return reduce_fixed_order(stats_local.double().sum(0), group=group)
 
 
 def dist_env() -> tuple[int, int, int]:

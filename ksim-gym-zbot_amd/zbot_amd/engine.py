@@ -13,7 +13,7 @@ import os
 from . import cstructs as cs
 
 LIB_NAME = "libzbot_hip.so"
-ABI_VERSION = 2  # include/zbot.h: version 2 added zb_step / zb_rollout's `success` output
+ABI_VERSION = 3  # include/zbot.h: 2 added zb_step / zb_rollout's `success`, 3 the exact FeetAirtime patch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 CSRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 
@@ -65,9 +65,12 @@ def load_library(path: str | None = None) -> C.CDLL:
     L.zb_get_stats.argtypes = [vp, vp, C.c_int, vp]
     L.zb_set_step_chunks.argtypes = [vp, C.c_int]
     L.zb_debug_forward.argtypes = [vp, vp, vp, vp, vp]
+    L.zb_mark_rollout_start.argtypes = [vp]
+    L.zb_check.argtypes = [vp]
+    L.zb_feet_airtime_exact.argtypes = [vp, vp, vp, C.c_float, vp]
     for f in ("zb_create", "zb_destroy", "zb_reset", "zb_step", "zb_rollout", "zb_get_state", "zb_set_state",
               "zb_get_rand", "zb_set_rand", "zb_get_stats", "zb_get_solver_iters", "zb_debug_forward",
-              "zb_set_step_chunks"):
+              "zb_set_step_chunks", "zb_mark_rollout_start", "zb_feet_airtime_exact", "zb_check"):
         getattr(L, f).restype = C.c_int
     # post-rollout PPO inputs (include/zbot_ppo.h)
     L.zb_gae_partials_words.argtypes = [C.c_int]
@@ -165,15 +168,23 @@ class HipEngine:
                                _ptr(self.obs_extra) if extras else None, self._stream()))
         return self.outputs()
 
-    def step(self, action, curriculum: float = 1.0, extras: bool = True, terms: bool = True) -> dict:
+    def step(self, action, curriculum: float = 1.0, extras: bool = True, terms: bool = True, reward=None,
+             done=None) -> dict:
+        """One control step of every env. reward [n] / done [n] (optional): write those two outputs
+        there instead of the engine's buffers (a row of a [T, n] rollout buffer, no copy)."""
         a = action
         if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
             a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
         if tuple(a.shape) != (self.n, cs.NJ):
             raise ZbError(f"action must be [{self.n}, {cs.NJ}], got {tuple(a.shape)}")
+        if reward is not None:
+            self._check_out(reward, "reward", (self.n,), self.torch.float32)
+        if done is not None:
+            self._check_out(done, "done", (self.n,), self.torch.uint8)
         _check(self.L.zb_step(self.h, _ptr(a), _ptr(self.obs_actor), _ptr(self.obs_critic),
                               _ptr(self.obs_extra) if extras else None, _ptr(self.reward_terms) if terms else None,
-                              _ptr(self.reward), _ptr(self.done), _ptr(self.success), float(curriculum),
+                              _ptr(self.reward if reward is None else reward),
+                              _ptr(self.done if done is None else done), _ptr(self.success), float(curriculum),
                               self._stream()))
         return self.outputs()
 
@@ -193,6 +204,22 @@ class HipEngine:
         _check(self.L.zb_rollout(self.h, _ptr(a), T, _ptr(self.obs_actor), _ptr(self.obs_critic), _ptr(reward_sum),
                                  _ptr(self.done), _ptr(self.success), float(curriculum), self._stream()))
         return self.outputs()
+
+    def mark_rollout_start(self) -> None:
+        """The next step() / rollout() is step 0 of a rollout (zb_mark_rollout_start): it saves what
+        feet_airtime_exact() needs to give ksim's FeetAirtime row 0."""
+        _check(self.L.zb_mark_rollout_start(self.h))
+
+    def feet_airtime_exact(self, reward0=None, terms0=None, curriculum: float = 1.0) -> None:
+        """After the last step of a marked rollout: patch row 0 to ksim's FeetAirtimeReward
+        (prev contact False at t = 0, airtime roll(air, 1) -> air[T-1]; train.py:515-546).
+        reward0 [n] gets scale * (ksim term - causal term) added, terms0 [n, 12] (nullable) its
+        FeetAirtime slot overwritten. Rows t >= 1 of the fused step are already ksim's."""
+        if reward0 is not None:
+            self._check_out(reward0, "reward0", (self.n,), self.torch.float32)
+        if terms0 is not None:
+            self._check_out(terms0, "terms0", (self.n, cs.NUM_TERMS), self.torch.float32)
+        _check(self.L.zb_feet_airtime_exact(self.h, _ptr(reward0), _ptr(terms0), float(curriculum), self._stream()))
 
     def get_state(self):
         out = self.torch.empty(self.n, cs.STATE_STRIDE, dtype=self.torch.float32, device=self.device)
@@ -227,6 +254,11 @@ class HipEngine:
         """Work units per pair of envs in step() (0: the automatic choice, 1: whole control steps;
         DESIGN.md §4e). The same bits for every k."""
         _check(self.L.zb_set_step_chunks(self.h, int(k)))
+
+    def check(self) -> None:
+        """Synchronise and raise ZbError if a launch since the last check flagged its results
+        invalid (zb_check: a chunked step's bounded hand-off wait timed out)."""
+        _check(self.L.zb_check(self.h))
 
     def solver_iters(self):
         out = self.torch.empty(self.n, dtype=self.torch.int32, device=self.device)
@@ -318,6 +350,11 @@ class EnvGroups:
         # priority < 0: high-priority group streams (torch.cuda.Stream priority)
         self.streams = group_streams(torch, self.device, groups, priority)
         self._tail = [None] * groups  # each group's last enqueued event
+        # events are re-recorded, not created per step: a stream wait captures the event's record
+        # at the time the wait is enqueued (CUDA / HIP semantics), so reuse is safe, and no
+        # hipEventCreate / Destroy pair runs per step and group
+        self._fork_ev = torch.cuda.Event()
+        self._mark_ev = [torch.cuda.Event() for _ in range(groups)]
 
     def groups(self):
         """(engine, stream, env range) of every group."""
@@ -328,14 +365,14 @@ class EnvGroups:
 
     def fork(self) -> None:
         """Order every group stream after the work enqueued so far on the current stream."""
-        ev = self.torch.cuda.Event()
+        ev = self._fork_ev
         ev.record(self.torch.cuda.current_stream(self.device))
         for s in self.streams:
             s.wait_event(ev)
 
     def mark(self, g: int) -> None:
         """Record group g's tail (after the work just enqueued on its stream)."""
-        ev = self.torch.cuda.Event()
+        ev = self._mark_ev[g]
         ev.record(self.streams[g])
         self._tail[g] = ev
 
@@ -346,20 +383,27 @@ class EnvGroups:
             if ev is not None:
                 cur.wait_event(ev)
 
-    def step(self, action, curriculum: float = 1.0, extras: bool = True, terms: bool = True, events=None) -> dict:
+    def step(self, action, curriculum: float = 1.0, extras: bool = True, terms: bool = True, events=None,
+             reward=None, done=None) -> dict:
         """events: optional per-group (start, end) torch.cuda.Event pairs recorded around each group's
-        launch on its stream (bench.py's per-launch timing)."""
+        launch on its stream (bench.py's per-launch timing). reward [n] / done [n]: as HipEngine.step
+        (each group writes its slice; pending until join())."""
         a = action
         if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
             a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
         if tuple(a.shape) != (self.n, cs.NJ):
             raise ZbError(f"action must be [{self.n}, {cs.NJ}], got {tuple(a.shape)}")
         self.fork()
+        for s in self.streams:
+            # the group streams read `a` after step() returns (no join): keep its block from being
+            # reused on the caller's stream before they are done with it
+            a.record_stream(s)
         for g, (e, s, (lo, hi)) in enumerate(self.groups()):
             with self.torch.cuda.stream(s):
                 if events is not None:
                     events[g][0].record(s)
-                e.step(a[lo:hi], curriculum=curriculum, extras=extras, terms=terms)
+                e.step(a[lo:hi], curriculum=curriculum, extras=extras, terms=terms,
+                       reward=None if reward is None else reward[lo:hi], done=None if done is None else done[lo:hi])
                 if events is not None:
                     events[g][1].record(s)
             self.mark(g)
@@ -374,10 +418,26 @@ class EnvGroups:
         self.fork()
         for g, (e, s, (lo, hi)) in enumerate(self.groups()):
             with self.torch.cuda.stream(s):
-                e.rollout(a[:, lo:hi].contiguous(), curriculum=curriculum,
+                part = a[:, lo:hi].contiguous()  # allocated on the group stream
+                a.record_stream(s)
+                e.rollout(part, curriculum=curriculum,
                           reward_sum=None if reward_sum is None else reward_sum[lo:hi])
             self.mark(g)
         return self.outputs()
+
+    def mark_rollout_start(self) -> None:
+        """Every group's next step is step 0 of a rollout (HipEngine.mark_rollout_start)."""
+        for e in self.engines:
+            e.mark_rollout_start()
+
+    def feet_airtime_exact(self, reward0=None, terms0=None, curriculum: float = 1.0) -> None:
+        """HipEngine.feet_airtime_exact per group, on the group's stream after its last step;
+        reward0 [n] / terms0 [n, 12] are the rollout's row-0 buffers (nullable). Pending like step()."""
+        for g, (e, s, (lo, hi)) in enumerate(self.groups()):
+            with self.torch.cuda.stream(s):
+                e.feet_airtime_exact(None if reward0 is None else reward0[lo:hi],
+                                     None if terms0 is None else terms0[lo:hi], curriculum=curriculum)
+            self.mark(g)
 
     def _each(self, fn):
         self.join()
@@ -411,3 +471,6 @@ class EnvGroups:
 
     def solver_iters(self):
         return self.torch.cat(self._each(lambda e, lo, hi: e.solver_iters()))
+
+    def check(self) -> None:
+        self._each(lambda e, lo, hi: e.check())

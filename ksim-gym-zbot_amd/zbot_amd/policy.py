@@ -198,13 +198,18 @@ class PolicyRollout:
     actor -> zb_step chain on their own stream (bit-identical: the actor's RNG is keyed by global
     env id)."""
 
-    def __init__(self, engine, actor: GruPolicy, seed: int = 0, curriculum: float = 1.0, stagger: bool = False):
+    def __init__(self, engine, actor: GruPolicy, seed: int = 0, curriculum: float = 1.0, stagger: bool = False,
+                 exact_airtime: bool = True):
         if actor.kind != ACTOR:
             raise ZbError("PolicyRollout needs an actor")
         self.eng = engine
         self.actor = actor
         self.seed = seed
         self.curriculum = curriculum
+        # each run() is one ksim trajectory: its FeetAirtime row 0 is patched to ksim's form
+        # (prev contact False at t = 0, airtime roll -> air[T-1]; include/zbot.h
+        # zb_feet_airtime_exact). False keeps the fused step's causal row 0.
+        self.exact_airtime = exact_airtime
         # with env groups: at the first step of a run(), group g's chain starts after group g-1's
         # first actor launch, offsetting the groups' phases (bit-identical either way)
         self.stagger = stagger
@@ -265,6 +270,9 @@ class PolicyRollout:
         parts = self.eng.groups() if grouped else [(self.eng, None, (0, n))]
         if grouped:
             self.eng.fork()
+        if self.exact_airtime:
+            for e, _, _ in parts:
+                _check(L.zb_mark_rollout_start(e.h))
         for t in range(T):
             for g, (e, s, (lo, hi)) in enumerate(parts):
                 with (torch.cuda.stream(s) if s is not None else contextlib.nullcontext()):
@@ -282,6 +290,9 @@ class PolicyRollout:
                                      crit[t + 1][lo:hi].data_ptr() if record_critic else None, None, None,
                                      rew[t][lo:hi].data_ptr(), done[t][lo:hi].data_ptr(),
                                      success[t][lo:hi].data_ptr(), float(self.curriculum), stream))
+                    if self.exact_airtime and t == T - 1:
+                        _check(L.zb_feet_airtime_exact(e.h, rew[0][lo:hi].data_ptr(), None, float(self.curriculum),
+                                                       stream))
                     if critic is not None:  # V(s_t): its input crit[t] is ready since step t-1
                         critic.critic(crit[t][lo:hi], critic_carry[lo:hi],
                                       reset=done[t - 1][lo:hi] if t > 0 else None, value=val[t][lo:hi])

@@ -22,6 +22,7 @@ from dataclasses import dataclass
 from . import cstructs as cs
 from .config import default_config
 from .constants import JOINT_BIASES, REWARDS
+from .curriculum import EpisodeLengthCurriculum, rollout_episode_length
 from .engine import HipEngine
 from .model import compile_model
 
@@ -97,15 +98,23 @@ class ZbotWalkingEnv:
 
     `num_envs`, `dt`, `ctrl_dt`, `iterations`, `ls_iterations` default to
     train.py:1768-1781 (512 envs, 0.001, 0.02, 8, 8).
+
+    `curriculum` is ksim's EpisodeLengthCurriculum of get_curriculum (train.py:1595-1602);
+    `curriculum_level` starts at its initial level and moves when update_curriculum() is called
+    once per rollout (a training step). Assigning `curriculum_level` directly overrides it.
     """
 
     def __init__(self, num_envs: int = 512, *, seed: int = 0, device: int = 0, env_offset: int = 0,
-                 push: bool = False, randomize: bool = False, obs_noise: bool = True, model=None, **cfg_kw):
+                 push: bool = False, randomize: bool = False, obs_noise: bool = True, model=None,
+                 curriculum: EpisodeLengthCurriculum | None = None, **cfg_kw):
         self.model = model or compile_model()
         self.cfg = default_config(push=push, randomize=randomize, obs_noise=obs_noise, **cfg_kw)
         self.engine = HipEngine(self.model, self.cfg, num_envs, env_offset=env_offset, device=device, seed=seed)
         self.num_envs = num_envs
-        self.curriculum_level = 1.0
+        self.curriculum = curriculum or EpisodeLengthCurriculum()
+        self.curriculum_state = self.curriculum.initial_state()
+        self.curriculum_level = self.curriculum_state.level
+        self._last_done = None
 
     def _result(self, out: dict, with_reward: bool) -> StepResult:
         terms = {}
@@ -127,7 +136,33 @@ class ZbotWalkingEnv:
 
     def step(self, action) -> StepResult:
         """One control step (20 physics substeps) for every env; done envs auto-reset."""
-        return self._result(self.engine.step(action, curriculum=self.curriculum_level), with_reward=True)
+        out = self.engine.step(action, curriculum=self.curriculum_level)
+        self._last_done = out["done"]
+        return self._result(out, with_reward=True)
+
+    def begin_rollout(self) -> None:
+        """Open a rollout (one ksim trajectory): clear the episode-statistics window that
+        update_curriculum() reads, and mark step 0 for the exact FeetAirtime row
+        (end_rollout; include/zbot.h zb_feet_airtime_exact)."""
+        self.engine.get_stats(clear=True)
+        self.engine.mark_rollout_start()
+
+    def end_rollout(self, reward0=None, terms0=None) -> None:
+        """Patch the rollout's row 0 (its reward [n] / reward terms [n, 12] buffers, as recorded from
+        the first step() after begin_rollout) to ksim's FeetAirtimeReward (train.py:515-546)."""
+        self.engine.feet_airtime_exact(reward0, terms0, curriculum=self.curriculum_level)
+
+    def update_curriculum(self) -> float:
+        """EpisodeLengthCurriculum update after a rollout (train.py:1595-1602; zbot_amd.curriculum):
+        the mean episode length of the rollout's window (begin_rollout) over every env of every rank
+        (RCCL all_gather when distributed), then the level law. Returns the new level."""
+        if self._last_done is None:
+            raise RuntimeError("update_curriculum() needs a rollout: step() first")
+        length = rollout_episode_length(self.engine.get_stats(), self.engine.get_state(), self._last_done,
+                                        self.cfg.ctrl_dt)
+        self.curriculum_state = self.curriculum.update(self.curriculum_state, length)
+        self.curriculum_level = self.curriculum_state.level
+        return self.curriculum_level
 
     def default_action(self):
         """FeetechActuators.get_default_action: current joint positions (train.py:1282-1283)."""

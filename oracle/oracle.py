@@ -108,6 +108,33 @@ def synthetic_actions(cmodel, seed: int, n: int, env_offset: int, t: int, std: f
     return a
 
 
+def feet_airtime_traj(contact, done, carry, ctrl_dt: float = 0.02, touchdown_penalty: float = 0.3):
+    """FeetAirtimeReward.get_reward_stateful over one trajectory, as ksim evaluates it after the
+    rollout (train.py:503-546; stand_still_threshold=None as registered at train.py:1559-1564).
+
+    contact [T, n, 2] bool (touch > 0.1, train.py:516-517), done [T, n] bool, carry [n, 2] float32
+    (the airtime carry, initial_carry zeros, train.py:499-501) -> (reward [T, n], carry' [n, 2]).
+    float32 throughout, the operations in the reference's order:
+      _airtime_sequence (:503-513): scan new = where(contact | done, 0, air + ctrl_dt)
+      touchdown (:526-528): c & ~concatenate([False], c[:-1])   -- prev = False at t = 0
+      (:533-539): (roll(air, 1) - penalty) * touchdown, left + right -- row 0 reads air[T-1]
+    """
+    f32 = np.float32
+    contact = np.asarray(contact, dtype=bool)
+    done = np.asarray(done, dtype=bool)
+    T, n = done.shape
+    a = np.asarray(carry, dtype=f32).copy()
+    air = np.empty((T, n, 2), dtype=f32)
+    for t in range(T):
+        a = np.where(contact[t] | done[t][:, None], f32(0.0), a + f32(ctrl_dt)).astype(f32)
+        air[t] = a
+    prev = np.concatenate([np.zeros((1, n, 2), dtype=bool), contact[:-1]], axis=0)
+    td = contact & ~prev
+    shifted = np.roll(air, 1, axis=0)
+    r = ((shifted - f32(touchdown_penalty)) * td.astype(f32)).astype(f32)
+    return (r[..., 0] + r[..., 1]).astype(f32), a
+
+
 class OracleEnv:
     """N environments simulated by the CPU oracle, same state layout as the engine."""
 

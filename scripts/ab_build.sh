@@ -15,5 +15,5 @@ elif [ "$REV" != cur ]; then SRC=$OUT/zb_engine_$NAME.hip; git -C "$ROOT" show "
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -I"$CSRC" -fno-signed-zeros \
   -freciprocal-math -fno-math-errno -fapprox-func ${SLP--fno-slp-vectorize} "$@" -c -o "$OUT/eng_$NAME.o" "$SRC"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libeng_$NAME.so" "$OUT/eng_$NAME.o" \
-  "$CSRC/build/zb_capi.o" "$CSRC/build/zb_ppo.o" "$CSRC/build/zb_policy.o"
+  "$CSRC/build/zb_capi.o" "$CSRC/build/zb_ppo.o" "$CSRC/build/zb_policy.o" "$CSRC/build/zb_host.o"
 echo "built $OUT/libeng_$NAME.so"

@@ -166,3 +166,29 @@ def test_set_step_chunks_same_bits(torch_gpu, cmodel):
         np.testing.assert_array_equal(_bits(st), _bits(states[0]))
     with pytest.raises(ZbError):
         e.set_step_chunks(-1)
+
+
+def test_converted_actions_outlive_step_without_join(torch_gpu, cmodel):
+    """A float64 action converted inside EnvGroups.step is read on the group streams after step()
+    returns; allocations right after step() (no join) must not reuse its block before the groups
+    are done with it (record_stream). Same bits as float32 actions on one handle."""
+    torch = torch_gpu
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    n = 256
+    cfg = default_config(push=True)
+    one = HipEngine(cmodel, cfg, n, seed=5)
+    grp = EnvGroups(cmodel, cfg, n, groups=2, seed=5)
+    one.reset()
+    grp.reset()
+    acts = _actions(torch, cmodel, 6, n, 9)
+    junk = []
+    for t in range(6):
+        one.step(acts[t])
+        grp.step(acts[t].double())  # converted copy, dropped when step() returns
+        # same-size allocations on the caller's stream, written at once
+        junk.append(torch.full((n, 20), float("nan"), dtype=torch.float32, device="cuda"))
+        junk.append(torch.full((n, 20), float("nan"), dtype=torch.float64, device="cuda"))
+    grp.join()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_bits(grp.get_state()), _bits(one.get_state()))

@@ -50,6 +50,25 @@ def close(a, b, scale):
     return np.abs(a - b) <= 1e-4 * np.maximum(np.abs(b), scale)
 
 
+class MaxErr:
+    """Max |gpu - oracle| per output over a test's steps: asserted against the test's stated
+    tolerance and printed, so a run's log shows how much headroom each bound has."""
+
+    def __init__(self, name):
+        self.name, self.err = name, {}
+
+    def add(self, key, got, ref, tol, rtol=0.0):
+        got = np.asarray(got, np.float64)
+        ref = np.asarray(ref, np.float64)
+        excess = np.abs(got - ref) - rtol * np.abs(ref)
+        e = float(excess.max()) if excess.size else 0.0
+        self.err[key] = max(self.err.get(key, 0.0), e)
+        assert e <= tol, f"{self.name}: {key} max error {e:.3e} > {tol:.1e}"
+
+    def report(self):
+        print(f"\n[{self.name}] max error: " + ", ".join(f"{k} {v:.2e}" for k, v in self.err.items()))
+
+
 def test_engine_loads_native_library(torch_gpu, cmodel):
     from zbot_amd import engine as E
 
@@ -94,6 +113,34 @@ def test_forward_stages_match_oracle(torch_gpu, cmodel, oracle_mod):
         np.testing.assert_allclose(g[DBG["misc"] + 2:DBG["misc"] + 4], ref["touch"], rtol=1e-3, atol=1e-3)
 
 
+# One env-step from identical state, fp32 engine vs fp32 oracle: (abs, rel) per output. The engine
+# is built with approximate reciprocals / transcendentals and hipcc's FMA contraction, the oracle
+# with -ffp-contract=off, so the bits differ; the constrained solve amplifies rounding in qvel.
+ONE_STEP_TOL = {
+    "qpos": (1e-4, 0.0),
+    "qvel": (1e-2, 0.0),
+    "planner": (1e-2, 0.0),
+    "obs_actor": (1e-3, 0.0),
+    "obs_critic": (2e-2, 1e-3),
+    "obs_extra": (5e-2, 1e-2),
+    "reward": (1e-3, 0.0),
+    "reward_terms": (1e-3, 0.0),
+}
+
+
+def one_step_outputs(gs, out, st_ref, ref):
+    yield "qpos", gs[:, :27], st_ref[:, :27]
+    yield "qvel", gs[:, 32:58], st_ref[:, 32:58]
+    yield "planner", gs[:, cs.S_PLAN_POS:cs.S_PLAN_TAU + 20], st_ref[:, cs.S_PLAN_POS:cs.S_PLAN_TAU + 20]
+    yield "obs_actor", out["obs_actor"].cpu().numpy(), ref["obs_actor"]
+    yield "obs_critic", out["obs_critic"].cpu().numpy(), ref["obs_critic"]
+    if out.get("obs_extra") is not None and "obs_extra" in ref:
+        yield "obs_extra", out["obs_extra"].cpu().numpy()[:, :67], ref["obs_extra"][:, :67]
+    yield "reward", out["reward"].cpu().numpy(), ref["reward"]
+    if "reward_terms" in ref:
+        yield "reward_terms", out["reward_terms"].cpu().numpy(), ref["reward_terms"]
+
+
 @pytest.mark.parametrize("push,randomize", [(False, False), (True, False), (False, True), (True, True)])
 def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize):
     torch = torch_gpu
@@ -101,6 +148,7 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize):
     n = 64
     env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
     eng = engine(cmodel, cfg, n, seed=7)
+    err = MaxErr(f"one-step push={push} randomize={randomize}")
     for t in range(3):
         eng.set_state(torch.from_numpy(env.state.copy()))
         eng.set_rand(torch.from_numpy(env.rand.copy()))
@@ -110,19 +158,17 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize):
         torch.cuda.synchronize()
         gs = eng.get_state().cpu().numpy()
         np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
-        np.testing.assert_allclose(gs[:, :27], env.state[:, :27], atol=1e-4)
-        np.testing.assert_allclose(gs[:, 32:58], env.state[:, 32:58], atol=1e-2)
-        np.testing.assert_allclose(gs[:, cs.S_PLAN_POS:cs.S_PLAN_TAU + 20], env.state[:, cs.S_PLAN_POS:cs.S_PLAN_TAU + 20],
-                                   atol=1e-2)
-        np.testing.assert_allclose(out["obs_actor"].cpu().numpy(), ref["obs_actor"], atol=1e-3)
-        np.testing.assert_allclose(out["obs_critic"].cpu().numpy(), ref["obs_critic"], atol=2e-2, rtol=1e-3)
-        np.testing.assert_allclose(out["obs_extra"].cpu().numpy()[:, :67], ref["obs_extra"][:, :67], atol=5e-2,
-                                   rtol=1e-2)
-        np.testing.assert_allclose(out["reward"].cpu().numpy(), ref["reward"], atol=1e-3)
-        np.testing.assert_allclose(out["reward_terms"].cpu().numpy(), ref["reward_terms"], atol=1e-3)
+        for key, got, want in one_step_outputs(gs, out, env.state, ref):
+            err.add(key, got, want, *ONE_STEP_TOL[key])
         # integer bookkeeping is exact
         for w in (cs.S_EP_STEPS, cs.S_RNG_STEP, cs.S_EPISODE):
             assert np.array_equal(gs[:, w].view(np.uint32), env.state[:, w].view(np.uint32))
+    err.report()
+
+
+# Multi-step rollouts from the same reset (contact dynamics are chaotic): the first 8 rewards and
+# the final base position of the committed oracle fixtures.
+GOLDEN_TOL = {"reward": 1e-2, "final_base_pos": 1e-2}
 
 
 @pytest.mark.parametrize("name", ["c1_seed0", "c5_push_seed1"])
@@ -143,10 +189,13 @@ def test_golden_rollout(torch_gpu, cmodel, name):
         done.append(o["done"].cpu().numpy().copy())
     rew, done = np.stack(rew), np.stack(done)
     np.testing.assert_array_equal(done, g["done"])
-    np.testing.assert_allclose(rew[:8], g["reward"][:8], atol=1e-2)
+    err = MaxErr(f"golden {name}")
+    for t in range(8):
+        err.add(f"reward[{t}]", rew[t], g["reward"][t], GOLDEN_TOL["reward"])
     gs = eng.get_state().cpu().numpy()
-    np.testing.assert_allclose(gs[:, :3], g["final_state"][:, :3], atol=1e-2)
-    np.testing.assert_allclose(eng.get_rand().cpu().numpy(), g["final_rand"], atol=1e-6)
+    err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], GOLDEN_TOL["final_base_pos"])
+    err.add("final_rand", eng.get_rand().cpu().numpy(), g["final_rand"], 1e-6)
+    err.report()
 
 
 def test_deterministic_and_shard_invariant(torch_gpu, cmodel, oracle_mod):
@@ -322,6 +371,7 @@ def test_mjcf_variant_model_parity(torch_gpu, cmodel_mjcf, oracle_mod):
         assert close(g[e, DBG["qM"]:DBG["qM"] + 26 * 26].reshape(26, 26), ref["qM"], 1e-3).all(), e
         assert close(g[e, DBG["bias"]:DBG["bias"] + 26], ref["qfrc_bias"], 1e-2).all(), e
         assert close(g[e, DBG["qacc_smooth"]:DBG["qacc_smooth"] + 26], ref["qacc_smooth"], 10.0).all(), e
+    err = MaxErr("mjcf variant one-step")
     for t in range(2):
         eng.set_state(torch.from_numpy(env.state.copy()))
         eng.set_rand(torch.from_numpy(env.rand.copy()))
@@ -331,10 +381,9 @@ def test_mjcf_variant_model_parity(torch_gpu, cmodel_mjcf, oracle_mod):
         torch.cuda.synchronize()
         gs = eng.get_state().cpu().numpy()
         np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
-        np.testing.assert_allclose(gs[:, :27], env.state[:, :27], atol=1e-4)
-        np.testing.assert_allclose(gs[:, 32:58], env.state[:, 32:58], atol=1e-2)
-        np.testing.assert_allclose(out["obs_actor"].cpu().numpy(), ref["obs_actor"], atol=1e-3)
-        np.testing.assert_allclose(out["reward"].cpu().numpy(), ref["reward"], atol=1e-3)
+        for key, got, want in one_step_outputs(gs, out, env.state, ref):
+            err.add(key, got, want, *ONE_STEP_TOL[key])
+    err.report()
 
 
 def test_team_divergence_is_exact(torch_gpu, cmodel, oracle_mod):

@@ -158,3 +158,58 @@ def test_observation_dims():
 
     assert NUM_ACTOR_INPUTS == 50  # train.py:53
     assert NUM_CRITIC_INPUTS == 484  # train.py:54
+
+
+# ---- FeetAirtimeReward over a trajectory, train.py:503-546 ----
+def test_feet_airtime_traj_hand_case(oracle_mod):
+    """Hand-derived: left contact [1,0,0,1,1], right always down, carry (0.1, 0), no dones.
+    air_l = [0, .02, .04, 0, 0]; touchdowns (prev = False at t = 0): left t0, t3; right t0.
+    Row 0 reads roll(air)[0] = air[T-1] = 0 for both feet: -0.3 - 0.3; row 3: .04 - .3."""
+    c = np.zeros((5, 1, 2), bool)
+    c[:, 0, 0] = [1, 0, 0, 1, 1]
+    c[:, 0, 1] = True
+    r, carry = oracle_mod.feet_airtime_traj(c, np.zeros((5, 1), bool), np.array([[0.1, 0.0]], np.float32))
+    np.testing.assert_allclose(r[:, 0], [-0.6, 0, 0, np.float32(0.04) - np.float32(0.3), 0], rtol=0, atol=1e-7)
+    assert carry.tolist() == [[0.0, 0.0]]
+
+
+def test_feet_airtime_traj_roll_wrap_and_done(oracle_mod):
+    """A touchdown at t = 0 only: row 0 is air[T-1] - 0.3 (jnp.roll wrap, train.py:533-534); a done
+    zeroes the airtime like a contact (contact_or_done, train.py:511)."""
+    c = np.zeros((5, 1, 2), bool)
+    c[0, 0, 0] = True
+    d = np.zeros((5, 1), bool)
+    r, carry = oracle_mod.feet_airtime_traj(c, d, np.zeros((1, 2), np.float32))
+    f = np.float32
+    air4 = f(f(f(f(0.02) + f(0.02)) + f(0.02)) + f(0.02))
+    assert r[0, 0] == f(air4 - f(0.3)) and (r[1:] == 0).all()
+    assert carry[0, 0] == air4 and carry[0, 1] == f(f(f(f(f(0.02) + f(0.02)) + f(0.02)) + f(0.02)) + f(0.02))
+    d[2, 0] = True
+    r, _ = oracle_mod.feet_airtime_traj(c, d, np.zeros((1, 2), np.float32))
+    assert r[0, 0] == f(f(f(0.02) + f(0.02)) - f(0.3))
+
+
+def test_feet_airtime_causal_form_equals_ksim_after_row0(oracle_mod):
+    """The fused step's causal per-step form (zb_engine.hip rewards(): touchdown against the
+    previous step's contact, airtime of the previous step) gives ksim's rows t >= 1 bit for bit on
+    random contact / done sequences; only row 0 differs (include/zbot.h zb_feet_airtime_exact)."""
+    f = np.float32
+    rng = np.random.default_rng(0)
+    T, n = 40, 64
+    c = rng.random((T, n, 2)) < 0.6
+    d = rng.random((T, n)) < 0.05
+    carry = rng.uniform(0, 0.3, (n, 2)).astype(f)
+    prev0 = rng.random((n, 2)) < 0.5
+    ref, _ = oracle_mod.feet_airtime_traj(c, d, carry)
+    air, prev = carry.copy(), prev0.copy()
+    causal = np.zeros((T, n), f)
+    for t in range(T):
+        rr = np.zeros(n, f)
+        for sd in range(2):
+            td = c[t, :, sd] & ~prev[:, sd]
+            rr = (rr + (air[:, sd] - f(0.3)) * td.astype(f)).astype(f)
+            air[:, sd] = np.where(c[t, :, sd] | d[t], f(0), air[:, sd] + f(0.02))
+            prev[:, sd] = c[t, :, sd]
+        causal[t] = rr
+    np.testing.assert_array_equal(causal[1:], ref[1:])
+    assert not np.array_equal(causal[0], ref[0])
