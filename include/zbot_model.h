@@ -147,7 +147,9 @@ typedef struct ZbModel {
      HIP engine so no per-launch scans are needed) */
   int32_t  max_body_depth;
   int32_t  mrow_size;                  /* packed depth-indexed row storage (floats) */
-  int32_t  pad_tab[2];
+  int32_t  nskip_geom;                 /* colliding geoms of the source model the engine cannot
+                                          collide (not box soles): zb_create rejects nskip_geom > 0 */
+  int32_t  pad_tab;
   int32_t  body_nchild[ZB_MAX_BODY];
   int32_t  body_child[ZB_MAX_BODY][8]; /* -1 padded */
   int32_t  depth_maxchild[16];         /* max #children over bodies at a depth */

@@ -67,6 +67,9 @@ struct EnvS {
   float ema[4], lag, air[2], push_timer, touch[2], feet_dist, ep_ret, prev_cont[2];
   uint32_t ep_steps, rng_step, episode, nanflag;
   float floor_mu, imu_q[4], imu_p[3];
+  /* the team's RNG identity (global env id, seed): read only at draw sites (observation noise,
+     pushes, resets), so kept here rather than in registers across the substep loop */
+  uint32_t env, seed_lo, seed_hi;
 };
 struct Sensors {
   float fq[4], gyro[3], acc[3], touch[2], force[6];
@@ -559,8 +562,6 @@ struct Ctx {
   MP m;
   CP cfg;
   EnvL* L;
-  uint64_t seed;
-  uint32_t env;
   int l;
   int nu;
   /* lane as a limb-chain dof (dofs >= nroot; each limb is an unbranched chain of
@@ -577,6 +578,12 @@ struct Ctx {
   int dfree;        /* dof l belongs to a free joint */
 };
 
+
+/* the team's RNG identity (EnvS.env / seed, written by make_ctx) */
+__device__ __forceinline__ uint64_t cseed(const Ctx& c) {
+  return (uint64_t)c.L->s.seed_lo | ((uint64_t)c.L->s.seed_hi << 32);
+}
+__device__ __forceinline__ uint32_t cenv(const Ctx& c) { return c.L->s.env; }
 
 /* ancestor dof at depth e of a dof whose limb chain starts at dof `head`
    (root dofs: head < 0): the tree shape makes ancestors dofs 0..NROOT-1
@@ -1804,12 +1811,19 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
   tsync();
   /* the full build runs with the whole wave (matrix-core Schur complement); a
      refactor inside the Newton loop may run for one team only (team reductions) */
+#ifndef ZB_UNIFORM_NEWTON
   return full ? factor_ldl<true>(c, H, Hd, L->Hs) : factor_ldl<false>(c, H, Hd, L->Hs);
+#else
+  /* the Newton loop is wave-uniform (solve_newton): every factorization of H runs the root Schur
+     complement on the matrix cores, so an unchanged team's refactor reproduces its last factor */
+  (void)full;
+  return factor_ldl<true>(c, H, Hd, L->Hs);
+#endif
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
 __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float grad,
-                                             float& Mv) {
+                                             float& Mv, bool active = true) {
   CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
@@ -1861,7 +1875,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
     d2 = c2 + gg[1];
   };
   float d1 = cc[2], d2 = c2 + cc[3];
-  if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
+  if (!active || !(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
   float gtol = cfg->ls_tolerance * (-d1);
   float lo = 0.f, hi = -1.f;
   float alpha = -d1 / d2;
@@ -1913,12 +1927,27 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
   int it = 0;
+#ifndef ZB_UNIFORM_NEWTON
   while (live && it < cfg->iterations) {
     float Mv;
     STAMP(S_CHECK);
     float alpha = line_search(c, r, search, Ma, fs, grad, Mv);
     STAMP(S_LS);
     if (alpha == 0.f) break;
+#else
+  /* Wave-uniform loop: it runs while either team of the wave iterates (a divergent loop issued
+     the same instructions for the slower team anyway). A team that has stopped is a ghost: its line
+     search returns alpha = 0, so every update below is an exact no-op on its state (same x, jar,
+     forces, gradient, cost; an unchanged H refactors to the same bits), and its counters stop. The
+     uniform control flow lets every refactor use the matrix-core root Schur complement. */
+  bool active = live && cfg->iterations > 0;
+  while (__ballot(active) != 0ull) {
+    float Mv;
+    STAMP(S_CHECK);
+    float alpha = line_search(c, r, search, Ma, fs, grad, Mv, active);
+    STAMP(S_LS);
+    if (alpha == 0.f) active = false;
+#endif
     x += alpha * search;
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
@@ -1935,6 +1964,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     tsum_n<3>(red);
     cost = red[0];
     STAMP(S_UPD);
+#ifndef ZB_UNIFORM_NEWTON
     it++;
     /* mj_solNewton's termination test. MuJoCo runs it after the Hessian update and the new
        search direction; both only feed the next iteration, so a terminating iteration skips
@@ -1946,6 +1976,22 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = red[2] > 0.f;
     if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo);
+#else
+    if (active) {
+      it++;
+      /* mj_solNewton's termination test. MuJoCo runs it after the Hessian update and the new
+         search direction; both only feed the next iteration, so a terminating iteration skips
+         them here (qacc, forces and costs are the same bits either way). */
+      const float improvement = scale * (oldcost - cost);
+      const float gradient = scale * sqrtf(red[1]);
+      if (improvement < cfg->tolerance || gradient < cfg->tolerance || it >= cfg->iterations) active = false;
+    }
+    if (__ballot(active) == 0ull) break;
+    /* H depends only on the active set (M, D fixed within a substep): refactor only when it changed
+       (MuJoCo's Newton does the same); a team whose set did not change refactors to the same bits */
+    const bool changed = active && red[2] > 0.f;
+    if (__ballot(changed) != 0ull) Dinv = hessian_factor(c, r, false, pa, pf, plo);
+#endif
     STAMP(S_HESS);
     const float mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
@@ -2198,11 +2244,15 @@ __device__ __forceinline__ void load_params(const Ctx& c, EnvS& s, LaneS& ls, co
 
 /* randomizer sampling (must match oracle/zb_oracle.c sample_rand) */
 __device__ __forceinline__ void sample_rand(const Ctx& c, uint32_t episode, float* rnd) {
-  CP cfg = c.cfg;
-  const int l = c.l;
+  /* re-derived here: hoisted out of the substep loop, the per-k field addresses were live for the
+     whole launch and spilled to scratch (only this rare path reads them) */
+  CP cfg = opaque(c.cfg);
+  /* opaque lane id: the per-k selections and keys below depend on the lane only, and hoisted to the
+     kernel entry they were live (spilled) for the whole launch though only this rare path reads them */
+  const int l = vopq(c.l);
   for (int k = l; k < 75; k += TEAM) {
     float u0, u1;
-    uniform2(c.seed, P_RAND, (uint32_t)k, c.env, episode, u0, u1);
+    uniform2(cseed(c), P_RAND, (uint32_t)k, cenv(c), episode, u0, u1);
     float lo, hi;
     int base;
     if (k < 16) { lo = cfg->rand_mass[0]; hi = cfg->rand_mass[1]; base = ZB_R_MASS + 2 * k; }
@@ -2216,9 +2266,9 @@ __device__ __forceinline__ void sample_rand(const Ctx& c, uint32_t episode, floa
   }
   if (l == 0) {
     float z00, z01, z10, z11, z20, z21;
-    normal2(c.seed, P_RAND, 75u, c.env, episode, z00, z01);
-    normal2(c.seed, P_RAND, 76u, c.env, episode, z10, z11);
-    normal2(c.seed, P_RAND, 77u, c.env, episode, z20, z21);
+    normal2(cseed(c), P_RAND, 75u, cenv(c), episode, z00, z01);
+    normal2(cseed(c), P_RAND, 76u, cenv(c), episode, z10, z11);
+    normal2(cseed(c), P_RAND, 77u, cenv(c), episode, z20, z21);
     float rv[3] = {cfg->rand_imu_tilt_std * z00, cfg->rand_imu_tilt_std * z01, cfg->rand_imu_yaw_std * z10};
     float ang = sqrtf(dot3(rv, rv)), q[4] = {1.f, 0.f, 0.f, 0.f};
     if (ang > MINVAL) {
@@ -2229,8 +2279,8 @@ __device__ __forceinline__ void sample_rand(const Ctx& c, uint32_t episode, floa
     rnd[ZB_R_IMU_POS + 0] = cfg->rand_imu_pos_std * z11;
     rnd[ZB_R_IMU_POS + 1] = cfg->rand_imu_pos_std * z20;
     rnd[ZB_R_IMU_POS + 2] = cfg->rand_imu_pos_std * z21;
-    for (int k = ZB_R_END; k < ZB_RAND_STRIDE; k++) rnd[k] = 0.f;
   }
+  for (int k = ZB_R_END + l; k < ZB_RAND_STRIDE; k += TEAM) rnd[k] = 0.f;
 }
 
 /* rotate_quat_by_quat (train.py:751-787) */
@@ -2266,7 +2316,7 @@ __device__ __forceinline__ void observe(const Ctx& c, EnvS& s, const LaneS& ls, 
   float acc[3] = {sen.acc[0], sen.acc[1], sen.acc[2]};
   if (cfg->flags & ZB_F_OBS_NOISE) {
     float z0 = 0.f, z1 = 0.f;
-    if (l < 4) normal2(c.seed, P_OBS, (uint32_t)l, c.env, s.rng_step, z0, z1);
+    if (l < 4) normal2(cseed(c), P_OBS, (uint32_t)l, cenv(c), s.rng_step, z0, z1);
     float a0 = tsh(z0, 0), a1 = tsh(z1, 0), b0 = tsh(z0, 1), b1 = tsh(z1, 1);
     float c0 = tsh(z0, 2), c1 = tsh(z1, 2), d0 = tsh(z0, 3);
     imu[0] += cfg->imu_noise_std * a0; imu[1] += cfg->imu_noise_std * a1;
@@ -2540,7 +2590,7 @@ __device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, 
     int qa = c.qadr;
     ls.q = m->joint_bias[c.act] + (c.L->par[P_Q0][c.l] - m->qpos0[qa]);
     float u0, u1;
-    uniform2(c.seed, P_RESET, (uint32_t)(c.act / 2), c.env, episode, u0, u1);
+    uniform2(cseed(c), P_RESET, (uint32_t)(vopq(c.act) / 2), cenv(c), episode, u0, u1);
     float u = (c.act & 1) ? u1 : u0;
     ls.v = cfg->reset_qvel_scale * (2.f * u - 1.f);
   } else if (l < NV && c.qadr >= 0) {
@@ -2548,7 +2598,7 @@ __device__ __forceinline__ void reset_prepare(const Ctx& c, EnvS& s, LaneS& ls, 
   }
   {
     float u0, u1;
-    uniform2(c.seed, P_RESET, 15u, c.env, episode, u0, u1);
+    uniform2(cseed(c), P_RESET, 15u, cenv(c), episode, u0, u1);
     s.lag = cfg->lag_range[0] + (cfg->lag_range[1] - cfg->lag_range[0]) * u0;
     s.push_timer = cfg->push_interval[0] + (cfg->push_interval[1] - cfg->push_interval[0]) * u1;
   }
@@ -2568,8 +2618,8 @@ __device__ __forceinline__ void push_event(const Ctx& c, EnvS& s, LaneS& ls, flo
   float timer = s.push_timer - cfg->ctrl_dt;
   if (timer <= 0.f) {
     float u0, u1, w0, w1;
-    uniform2(c.seed, P_PUSH, 0u, c.env, s.rng_step, u0, u1);
-    uniform2(c.seed, P_PUSH, 1u, c.env, s.rng_step, w0, w1);
+    uniform2(cseed(c), P_PUSH, 0u, cenv(c), s.rng_step, u0, u1);
+    uniform2(cseed(c), P_PUSH, 1u, cenv(c), s.rng_step, w0, w1);
     float mag = (cfg->push_vel_range[0] + (cfg->push_vel_range[1] - cfg->push_vel_range[0]) * w1) / cfg->push_vel_range[1];
     if (c.l == 0) ls.v += cur * mag * cfg->push_linvel[0] * (2.f * u0 - 1.f);
     if (c.l == 1) ls.v += cur * mag * cfg->push_linvel[1] * (2.f * u1 - 1.f);
@@ -2587,8 +2637,9 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.m = (MP)m;
   c.cfg = (CP)cfg;
   c.L = L;
-  c.seed = seed;
-  c.env = env;
+  L->s.env = env;
+  L->s.seed_lo = (uint32_t)seed;
+  L->s.seed_hi = (uint32_t)(seed >> 32);
   const int l = threadIdx.x & (TEAM - 1);
   c.l = l;
   c.nu = m->nu;
@@ -2716,7 +2767,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   bool partial = false;                               /* a chunk before the last one */
   for (int t = 0; t < nsteps; t++) {
     const bool last_t = t == nsteps - 1;
-    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + vopq(ee)) * ZB_NJ + c.act];
+    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + vopq(ee)) * ZB_NJ + vopq(c.act)];
     if (ch == 0 && (cfg->flags & ZB_F_PUSH)) push_event(c, s, ls, a.curriculum);
     float total = 0.f;
     int ss = ch * cfg->n_substeps / K;

@@ -90,6 +90,10 @@ int check_model(const ZbModel* m) {
   if (m->struct_bytes != (int32_t)sizeof(ZbModel))
     return fail(ZB_EARG, "model struct_bytes %d != %zu (layout mismatch)", m->struct_bytes, sizeof(ZbModel));
   if (int rc = check_indices(m)) return rc;
+  if (m->nskip_geom != 0)
+    return fail(ZB_EMODEL, "the source model has %d colliding geoms the engine does not collide with the floor (it "
+                           "collides the 2 box soles): compile_model(..., drop_colliders=True) to simulate without "
+                           "them knowingly", m->nskip_geom);
   if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
   if (m->ngeom * ZB_CON_PER_GEOM * 4 > 32)

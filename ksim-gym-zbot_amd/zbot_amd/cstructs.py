@@ -194,7 +194,8 @@ class ZbModel(C.Structure):
         ("geom_right_foot", C.c_int32),
         ("max_body_depth", C.c_int32),
         ("mrow_size", C.c_int32),
-        ("pad_tab", _i(2)),
+        ("nskip_geom", C.c_int32),
+        ("pad_tab", C.c_int32),
         ("body_nchild", _i(MAX_BODY)),
         ("body_child", _i(MAX_BODY, 8)),
         ("depth_maxchild", _i(16)),

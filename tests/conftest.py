@@ -32,7 +32,7 @@ def mjcf_variant_desc():
     from zbot_amd.model import load_description
 
     root = ET.fromstring(to_mjcf(load_description()))
-    root.find("default").append(ET.fromstring('<default class="arm"><geom type="capsule" density="1200"/></default>'))
+    root.find("default").append(ET.fromstring('<default class="arm"><geom type="capsule" density="1200" contype="0" conaffinity="0"/></default>'))
     axes = [(1, 2, 3, 25.0), (0, 1, 1, -40.0), (3, -1, 2, 70.0), (1, 0, 0, 90.0)]
     k = 0
     for b in root.iter("body"):

@@ -113,6 +113,7 @@ def test_policy_rollout_rows_are_ksim_feet_airtime(oracle_mod):
         eng = HipEngine(cm, default_config(), 64, seed=3)
         ro = P.PolicyRollout(eng, P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=4)), seed=6, exact_airtime=exact)
         ro.reset()
+        ro.run(12)  # from the reset pose the feet touch down during the first steps: warm up first
         air0 = eng.get_state()[:, cs.S_AIRTIME:cs.S_AIRTIME + 2].clone()
         out = ro.run(12)
         st = eng.get_state()

@@ -2,10 +2,11 @@
 
 Tolerances (fp32 engine vs fp32/fp64 oracle; the reference computes in fp32):
   * per-stage forward quantities: |gpu - oracle_f64| <= 1e-4 * max(|ref|, scale)
-  * one env-step from identical state: qpos 1e-4 abs, qvel 1e-2 abs,
-    observations/reward 1e-3 abs, done exact
-  * multi-step rollouts (contact dynamics are chaotic): rewards 1e-2 abs over
-    the first 8 steps, done flags equal
+  * one env-step from identical state: ONE_STEP_TOL below (qpos 1e-6, qvel 2e-5,
+    reward 4e-6 abs, ...: ~5x the measured max error), done exact
+  * multi-step rollouts from the same reset: GOLDEN_TOL (rewards 1e-5 abs over the
+    first 8 steps, final base position 1e-5), done flags equal
+  * every test prints its measured max |error| per output (run with -s)
   * integer/bookkeeping outputs (done, counters, RNG-driven resets): exact
 """
 
@@ -58,15 +59,17 @@ class MaxErr:
         self.name, self.err = name, {}
 
     def add(self, key, got, ref, tol, rtol=0.0):
+        """|got - ref| <= tol + rtol |ref| elementwise; records the max absolute error."""
         got = np.asarray(got, np.float64)
         ref = np.asarray(ref, np.float64)
-        excess = np.abs(got - ref) - rtol * np.abs(ref)
-        e = float(excess.max()) if excess.size else 0.0
+        d = np.abs(got - ref)
+        e = float(d.max()) if d.size else 0.0
         self.err[key] = max(self.err.get(key, 0.0), e)
-        assert e <= tol, f"{self.name}: {key} max error {e:.3e} > {tol:.1e}"
+        excess = float((d - rtol * np.abs(ref)).max()) if d.size else 0.0
+        assert excess <= tol, f"{self.name}: {key} max error {e:.3e} (excess {excess:.3e}) > {tol:.1e} + {rtol:.0e} |ref|"
 
     def report(self):
-        print(f"\n[{self.name}] max error: " + ", ".join(f"{k} {v:.2e}" for k, v in self.err.items()))
+        print(f"\n[{self.name}] max |error|: " + ", ".join(f"{k} {v:.2e}" for k, v in self.err.items()))
 
 
 def test_engine_loads_native_library(torch_gpu, cmodel):
@@ -115,16 +118,19 @@ def test_forward_stages_match_oracle(torch_gpu, cmodel, oracle_mod):
 
 # One env-step from identical state, fp32 engine vs fp32 oracle: (abs, rel) per output. The engine
 # is built with approximate reciprocals / transcendentals and hipcc's FMA contraction, the oracle
-# with -ffp-contract=off, so the bits differ; the constrained solve amplifies rounding in qvel.
+# with -ffp-contract=off, so the bits differ. The bounds are the contract: about 5x the max error
+# measured on MI355X over the four configurations (round 3, profiles/r03_v1_gpu_tests.log: qpos
+# 1.2e-7, qvel 3.3e-6, planner 2.1e-6, obs_actor 3.3e-6, obs_critic 9.3e-5, obs_extra 1.9e-3 (the
+# accelerations), reward 7.2e-7, terms 1.0e-6).
 ONE_STEP_TOL = {
-    "qpos": (1e-4, 0.0),
-    "qvel": (1e-2, 0.0),
-    "planner": (1e-2, 0.0),
-    "obs_actor": (1e-3, 0.0),
-    "obs_critic": (2e-2, 1e-3),
-    "obs_extra": (5e-2, 1e-2),
-    "reward": (1e-3, 0.0),
-    "reward_terms": (1e-3, 0.0),
+    "qpos": (1e-6, 0.0),
+    "qvel": (2e-5, 0.0),
+    "planner": (1e-5, 0.0),
+    "obs_actor": (2e-5, 0.0),
+    "obs_critic": (5e-4, 0.0),
+    "obs_extra": (1e-2, 0.0),
+    "reward": (4e-6, 0.0),
+    "reward_terms": (5e-6, 0.0),
 }
 
 
@@ -168,7 +174,8 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize):
 
 # Multi-step rollouts from the same reset (contact dynamics are chaotic): the first 8 rewards and
 # the final base position of the committed oracle fixtures.
-GOLDEN_TOL = {"reward": 1e-2, "final_base_pos": 1e-2}
+# Measured (round 3): rewards <= 1.8e-6 over the 8 steps, final base position <= 2.0e-6.
+GOLDEN_TOL = {"reward": 1e-5, "final_base_pos": 1e-5}
 
 
 @pytest.mark.parametrize("name", ["c1_seed0", "c5_push_seed1"])

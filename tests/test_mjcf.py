@@ -415,3 +415,36 @@ def test_command_line_round_trip(tmp_path):
 def test_missing_file_is_reported():
     with pytest.raises(FileNotFoundError):
         load_mjcf("/nonexistent/zbot.xml")
+
+
+def test_skipped_colliders_are_rejected_by_zb_create():
+    """A real MJCF whose shins / hands collide (capsules) cannot be simulated by this engine, which
+    collides the two box soles with the floor: zb_create rejects it (ZB_EMODEL, nskip_geom) instead
+    of dropping those contacts silently; compile_model(..., drop_colliders=True) drops them
+    knowingly (missing item 3)."""
+    import ctypes as C
+    import xml.etree.ElementTree as ET
+
+    from zbot_amd import compile_model, default_config
+    from zbot_amd import engine as E
+
+    root = ET.fromstring(to_mjcf(load_description()))
+    for b in root.iter("body"):
+        if "knee" in b.get("name"):
+            b.append(ET.fromstring('<geom name="shin_col" type="capsule" size="0.015" fromto="0 0 0 0 0 -0.08" '
+                                   'mass="0"/>'))
+            break
+    desc = load_mjcf(ET.tostring(root, encoding="unicode"))
+    assert [g["name"] for g in desc["skipped_geoms"]] == ["shin_col"]
+    L = E.load_library()
+    h = C.c_void_p()
+    cm = compile_model(desc)
+    assert cm.cmodel.nskip_geom == 1
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc == -4 and b"colliding geoms" in L.zb_last_error()
+    cm = compile_model(desc, drop_colliders=True)
+    assert cm.cmodel.nskip_geom == 0
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc != -4  # validation passes (no device here: -2)
+    if rc == 0:
+        L.zb_destroy(h)
