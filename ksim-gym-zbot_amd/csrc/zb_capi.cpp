@@ -209,7 +209,7 @@ int zb_reset(ZbHandle* h, const uint8_t* env_mask_dev, float* obs_actor, float* 
 int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_critic, float* obs_extra,
             float* reward_terms, float* reward, uint8_t* done, uint8_t* success, float curriculum_level,
             void* stream) {
-  if (!h || !action) return fail(ZB_EARG, "zb_step: null handle or action");
+  if (!h || (!action && h->n > 0)) return fail(ZB_EARG, "zb_step: null handle or action");
   if (!(curriculum_level == curriculum_level)) return fail(ZB_EARG, "zb_step: curriculum is NaN");
   int rc = use_device(h);
   if (rc) return rc;
@@ -234,7 +234,7 @@ int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_criti
 
 int zb_rollout(ZbHandle* h, const float* actions, int n_steps, float* obs_actor, float* obs_critic, float* reward_sum,
                uint8_t* done, uint8_t* success, float curriculum_level, void* stream) {
-  if (!h || !actions || n_steps < 1) return fail(ZB_EARG, "zb_rollout: bad argument");
+  if (!h || (!actions && h->n > 0) || n_steps < 1) return fail(ZB_EARG, "zb_rollout: bad argument");
   int rc = use_device(h);
   if (rc) return rc;
   zb::StepArgs a = base_args(h);
@@ -280,6 +280,7 @@ int zb_feet_airtime_exact(ZbHandle* h, float* reward0, float* reward_terms0, flo
 }
 
 static int copy_rows(ZbHandle* h, void* dst, const void* src, size_t bytes, void* stream) {
+  if (h && bytes == 0) return ZB_OK; /* a handle over zero envs (an empty shard) */
   if (!h || !dst || !src) return fail(ZB_EARG, "null pointer");
   int rc = use_device(h);
   if (rc) return rc;

@@ -1811,19 +1811,12 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
   tsync();
   /* the full build runs with the whole wave (matrix-core Schur complement); a
      refactor inside the Newton loop may run for one team only (team reductions) */
-#ifndef ZB_UNIFORM_NEWTON
   return full ? factor_ldl<true>(c, H, Hd, L->Hs) : factor_ldl<false>(c, H, Hd, L->Hs);
-#else
-  /* the Newton loop is wave-uniform (solve_newton): every factorization of H runs the root Schur
-     complement on the matrix cores, so an unchanged team's refactor reproduces its last factor */
-  (void)full;
-  return factor_ldl<true>(c, H, Hd, L->Hs);
-#endif
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
 __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float grad,
-                                             float& Mv, bool active = true) {
+                                             float& Mv) {
   CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
@@ -1875,7 +1868,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
     d2 = c2 + gg[1];
   };
   float d1 = cc[2], d2 = c2 + cc[3];
-  if (!active || !(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
+  if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
   float gtol = cfg->ls_tolerance * (-d1);
   float lo = 0.f, hi = -1.f;
   float alpha = -d1 / d2;
@@ -1927,27 +1920,12 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
   int it = 0;
-#ifndef ZB_UNIFORM_NEWTON
   while (live && it < cfg->iterations) {
     float Mv;
     STAMP(S_CHECK);
     float alpha = line_search(c, r, search, Ma, fs, grad, Mv);
     STAMP(S_LS);
     if (alpha == 0.f) break;
-#else
-  /* Wave-uniform loop: it runs while either team of the wave iterates (a divergent loop issued
-     the same instructions for the slower team anyway). A team that has stopped is a ghost: its line
-     search returns alpha = 0, so every update below is an exact no-op on its state (same x, jar,
-     forces, gradient, cost; an unchanged H refactors to the same bits), and its counters stop. The
-     uniform control flow lets every refactor use the matrix-core root Schur complement. */
-  bool active = live && cfg->iterations > 0;
-  while (__ballot(active) != 0ull) {
-    float Mv;
-    STAMP(S_CHECK);
-    float alpha = line_search(c, r, search, Ma, fs, grad, Mv, active);
-    STAMP(S_LS);
-    if (alpha == 0.f) active = false;
-#endif
     x += alpha * search;
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
@@ -1964,7 +1942,6 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     tsum_n<3>(red);
     cost = red[0];
     STAMP(S_UPD);
-#ifndef ZB_UNIFORM_NEWTON
     it++;
     /* mj_solNewton's termination test. MuJoCo runs it after the Hessian update and the new
        search direction; both only feed the next iteration, so a terminating iteration skips
@@ -1976,22 +1953,6 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = red[2] > 0.f;
     if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo);
-#else
-    if (active) {
-      it++;
-      /* mj_solNewton's termination test. MuJoCo runs it after the Hessian update and the new
-         search direction; both only feed the next iteration, so a terminating iteration skips
-         them here (qacc, forces and costs are the same bits either way). */
-      const float improvement = scale * (oldcost - cost);
-      const float gradient = scale * sqrtf(red[1]);
-      if (improvement < cfg->tolerance || gradient < cfg->tolerance || it >= cfg->iterations) active = false;
-    }
-    if (__ballot(active) == 0ull) break;
-    /* H depends only on the active set (M, D fixed within a substep): refactor only when it changed
-       (MuJoCo's Newton does the same); a team whose set did not change refactors to the same bits */
-    const bool changed = active && red[2] > 0.f;
-    if (__ballot(changed) != 0ull) Dinv = hessian_factor(c, r, false, pa, pf, plo);
-#endif
     STAMP(S_HESS);
     const float mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);

@@ -301,7 +301,8 @@ def test_full_size_properties(torch_gpu, cmodel):
     assert (z > 0.2).float().mean().item() > 0.95
 
 
-@pytest.mark.parametrize("n,push,randomize", [(32768, True, False), (16384, False, True)], ids=["c3", "c5"])
+@pytest.mark.parametrize("n,push,randomize", [(32768, True, False), (16384, False, True), (65536, True, True)],
+                         ids=["c3", "c5", "c4_65536_one_gpu"])
 def test_full_size_configs(torch_gpu, cmodel, n, push, randomize):
     """BASELINE configs C3 (32768 envs, push curriculum) and C5 (16384 envs, per-env
     randomization) at full size, through size-independent properties: bit-reproducible,
@@ -442,3 +443,30 @@ def test_team_divergence_is_exact(torch_gpu, cmodel, oracle_mod):
     gs = eng.get_state().cpu().numpy()
     np.testing.assert_allclose(gs[:, cs.S_QACCW:cs.S_QACCW + 26], env.state[:, cs.S_QACCW:cs.S_QACCW + 26],
                                atol=5e-2, rtol=1e-2)
+
+
+def test_empty_and_single_env_handles(torch_gpu, cmodel, oracle_mod):
+    """Edge sizes through the C ABI: a handle over zero envs accepts every call as a no-op (a rank
+    whose shard is empty), and a single env (one team of a wave, the other a ghost) steps like
+    the oracle."""
+    torch = torch_gpu
+    cfg = default_config(push=True)
+    e0 = engine(cmodel, cfg, 0, seed=1)
+    out = e0.reset()
+    out = e0.step(torch.zeros(0, 20, device="cuda"))
+    assert out["obs_actor"].shape == (0, 50) and e0.get_state().shape == (0, cs.STATE_STRIDE)
+    e0.mark_rollout_start()
+    e0.step(torch.zeros(0, 20, device="cuda"))
+    e0.feet_airtime_exact(torch.zeros(0, device="cuda"))
+    e0.check()
+    env = warm_states(oracle_mod, cmodel, cfg, 1, steps=6)
+    e1 = engine(cmodel, cfg, 1, seed=7)
+    e1.set_state(torch.from_numpy(env.state.copy()))
+    a = oracle_mod.synthetic_actions(cmodel.cmodel, 7, 1, 0, 50)
+    ref = env.step(a)
+    o = e1.step(torch.from_numpy(a).cuda())
+    torch.cuda.synchronize()
+    err = MaxErr("single env one-step")
+    for key, got, want in one_step_outputs(e1.get_state().cpu().numpy(), o, env.state, ref):
+        err.add(key, got, want, *ONE_STEP_TOL[key])
+    err.report()
