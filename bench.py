@@ -358,6 +358,9 @@ def main() -> None:
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default: the config's)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--solver", default="newton", choices=["newton", "cg"],
+                    help="constraint solver (ZbEnvConfig.solver): MuJoCo's Newton (default) or CG; which one "
+                         "ksim sets is [U] (DESIGN.md §8)")
     ap.add_argument("--groups", type=int, default=2,
                     help="env groups per GPU, each stepping on its own HIP stream (zbot_amd.EnvGroups, "
                          "DESIGN.md §4f); 1 = one handle on the current stream")
@@ -401,7 +404,7 @@ def main() -> None:
     conf = CONFIGS[args.config]
     n = args.envs or conf["envs"]
     cm = compile_model()
-    cfg = default_config(push=conf["push"], randomize=conf["randomize"])
+    cfg = default_config(push=conf["push"], randomize=conf["randomize"], solver=args.solver)
     G = max(1, args.groups)
     if G > 1:
         eng = EnvGroups(cm, cfg, n, groups=G, env_offset=rank * n, device=dev.index, seed=args.seed)
@@ -425,6 +428,25 @@ def main() -> None:
             dist.all_gather(allp, part)
             return torch.stack(allp).sum(0)
         return part
+
+    # The other legs run first: their work (about two seconds of GPU time) brings the GPU to its
+    # steady clocks before the headline's own W warm-up steps and K timed steps; in a fresh
+    # process the first timed window otherwise ran ~4 % slower kernels (profiles/r03_v3_probe20_g*.json)
+    c2_leg = None if args.no_c2_rollout else bench_c2_rollout(eng, n, 256, dev, rank, world)
+    ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
+    # the actor-in-the-loop legs: one handle on the current stream for the actor's kernel time, and
+    # args.policy_groups env groups with the slot-sized two-wave actor (DESIGN.md §4f)
+    eng1 = eng if G == 1 else None
+    engp = None
+    if not (args.no_policy and args.no_pipeline):
+        if G > 1:
+            eng1 = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
+        if args.policy_groups > 1:
+            engp = EnvGroups(cm, cfg, n, groups=args.policy_groups, env_offset=rank * n, device=dev.index,
+                             seed=args.seed)
+    policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, engp)
+    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(engp or eng1, n, 32, 2, dev, world,
+                                                                     args.inloop_critic)
 
     eng.reset()
     for t in range(args.warmup):
@@ -488,32 +510,16 @@ def main() -> None:
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("envs") == n:
+        if tj.get("envs") == n and args.solver == "newton":
             traffic = tj.get("hbm_bytes_per_launch")
             flop_per_env_step = tj.get("issued_fp32_flop_per_env_step")
     # algorithmic FLOPs per env-step, counted by the instrumented CPU twin on the C2 workload
     # (scripts/count_flops.py)
     algo_flop = None
     fpath = os.path.join(ROOT, "profiles", "r02_flops_count.json")
-    if os.path.exists(fpath):
+    if os.path.exists(fpath) and args.solver == "newton":  # the count is of the Newton solver
         with open(fpath) as f:
             algo_flop = json.load(f)["as_run"]["flops_per_env_step"]
-
-    c2_leg = None if args.no_c2_rollout else bench_c2_rollout(eng, n, 256, dev, rank, world)
-    ppo_leg = None if args.no_ppo else bench_ppo_inputs(n, 256, 20, dev, world)
-    # the actor-in-the-loop legs: one handle on the current stream for the actor's kernel time, and
-    # args.policy_groups env groups with the slot-sized two-wave actor (DESIGN.md §4f)
-    eng1 = eng if G == 1 else None
-    engp = None
-    if not (args.no_policy and args.no_pipeline):
-        if G > 1:
-            eng1 = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=args.seed)
-        if args.policy_groups > 1:
-            engp = EnvGroups(cm, cfg, n, groups=args.policy_groups, env_offset=rank * n, device=dev.index,
-                             seed=args.seed)
-    policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, engp)
-    pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(engp or eng1, n, 32, 2, dev, world,
-                                                                     args.inloop_critic)
 
     if rank == 0:
         value = world * n * args.steps / elapsed
@@ -538,7 +544,7 @@ def main() -> None:
                 "envs_per_gpu": n,
                 "global_envs": world * n,
                 "substeps_per_step": cfg.n_substeps,
-                "solver": f"newton, {cfg.iterations} iters / {cfg.ls_iterations} ls iters",
+                "solver": f"{args.solver}, {cfg.iterations} iters / {cfg.ls_iterations} ls iters",
                 "parallelism": f"env-shard x{world} (one process per GPU)" + (
                     "" if world == 1 or args.dist_backend == "nccl" else f", {args.dist_backend} rehearsal")
                 + (f"; {G} env groups of {n // G} per GPU, each zb_step-ing on its own HIP stream" if G > 1 else ""),

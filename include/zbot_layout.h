@@ -104,6 +104,10 @@ extern "C" {
 #define ZB_ST_DONE     2   /* number of finished episodes */
 #define ZB_ST_REWARD   3   /* sum of per-step total reward */
 
+/* ZbEnvConfig.solver (mjtSolver order: mjSOL_CG = 1, mjSOL_NEWTON = 2; here 0 is the default) */
+#define ZB_SOLVER_NEWTON 0u  /* primal Newton, Hessian M + J'DJ (mj_solNewton) */
+#define ZB_SOLVER_CG     1u  /* primal nonlinear CG, M^-1 preconditioned, Polak-Ribiere (mj_solCG) */
+
 /* flag bits of ZbEnvConfig.flags */
 #define ZB_F_OBS_NOISE   1u   /* ksim observation noise (train.py:1497,1503) */
 #define ZB_F_PUSH        2u   /* PushEvent (train.py:1459-1468), config 3 */
@@ -148,7 +152,9 @@ typedef struct ZbEnvConfig {
   float    rand_imu_tilt_std;   /* radians(5)  train.py:1453 */
   float    rand_imu_yaw_std;    /* radians(1)  */
   float    rand_imu_pos_std;    /* 0.005 m     */
-  float    pad[3];
+  int32_t  solver;             /* ZB_SOLVER_NEWTON (default) or ZB_SOLVER_CG: the [U] solver type
+                                  ksim sets on the MJX model */
+  float    pad[2];
 } ZbEnvConfig;
 
 #ifdef __cplusplus

@@ -188,6 +188,7 @@ static zb::StepArgs base_args(ZbHandle* h) {
   a.nchunk = 1;
   a.sched = h->sched;
   a.itpart = h->itpart;
+  a.solver = h->cfg.solver;
   return a;
 }
 

@@ -1962,6 +1962,70 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   return x;
 }
 
+/* constrained acceleration by the primal nonlinear conjugate gradient (mj_solCG; MJX solver.py
+   with SolverType.CG; oracle solve_cg). The same warmstart, cost, exact line search and
+   termination test as solve_newton; the direction is the M^-1-preconditioned gradient, solved with
+   the smooth factor of M that forward() left in L[] / Dk / Di (DinvM: this lane's 1/D), with
+   Polak-Ribiere beta = max(0, g . (Mg - Mg_prev) / max(MINVAL, g_prev . Mg_prev)). No Hessian is
+   built or factored. Returns qacc (dof lane). */
+__device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters, bool live,
+                                          float DinvM) {
+  CP cfg = c.cfg;
+  MP m = c.m;
+  EnvL* L = c.L;
+  float x = w;
+  if (c.l < 32) L->vec[V_TMP2][c.l] = qs;
+  float Ma = mul_m(c, x, V_TMP);
+  float jw = row_dot(c, r, V_TMP) - r.aref;
+  float js = row_dot(c, r, V_TMP2) - r.aref;
+  tsync();
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, r.sl * x - r.al),
+                  rows_cost(c, r, js, qs - r.af, r.sl * qs - r.al)};
+  tsum_n<2>(cws);
+  if (cws[0] > cws[1]) {
+    x = qs;
+    Ma = mul_m(c, x, V_TMP);
+    r.jar = js;
+  } else {
+    r.jar = jw;
+  }
+  r.jf = x - r.af;
+  r.jl = r.sl * x - r.al;
+  const float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
+  float grad;
+  float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
+  float mg = solve_ldl(c, grad, DinvM);
+  float search = -mg;
+  int it = 0;
+  while (live && it < cfg->iterations) {
+    float Mv;
+    const float alpha = line_search(c, r, search, Ma, fs, grad, Mv);
+    if (alpha == 0.f) break;
+    x += alpha * search;
+    Ma += alpha * Mv;
+    r.jar += alpha * r.Jv;
+    r.jf += alpha * search;
+    r.jl += alpha * (r.sl * search);
+    const float oldcost = cost, gold = grad, mgold = mg;
+    float red[2];
+    red[0] = update_constraint_lane(c, r, x, qs, fs, Ma, grad);
+    red[1] = c.l < NV ? grad * grad : 0.f;
+    tsum_n<2>(red);
+    cost = red[0];
+    it++;
+    const float improvement = scale * (oldcost - cost);
+    const float gradient = scale * sqrtf(red[1]);
+    if (improvement < cfg->tolerance || gradient < cfg->tolerance || it >= cfg->iterations) break;
+    mg = solve_ldl(c, grad, DinvM);
+    float pr[2] = {c.l < NV ? grad * (mg - mgold) : 0.f, c.l < NV ? gold * mgold : 0.f};
+    tsum_n<2>(pr);
+    const float beta = fmaxf(pr[0] / fmaxf(pr[1], MINVAL), 0.f);
+    search = -mg + beta * search;
+  }
+  iters += it;
+  return x;
+}
+
 /* ----------------------------- Feetech actuator ---------------------------- */
 /* trapezoidal_step (train.py:1137-1196) + duty/torque (train.py:1260-1269) */
 __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
@@ -1998,6 +2062,7 @@ __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
 
 /* ------------------------------- full forward ------------------------------ */
 /* mj_forward (+ sensors if requested). Leaves qacc in ls.qacc, kinematics in B. */
+template <int SOLVER>
 __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
                                         Sensors& sen, int& iters) {
   MP m = c.m;
@@ -2047,7 +2112,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   qacc = qs;
   if (__ballot(nrows > 0) != 0ull) {
     int it2 = 0;
-    const float qn = solve_newton(c, r, qs, fs, ls.w, it2, nrows > 0);
+    const float qn = SOLVER == ZB_SOLVER_CG ? solve_cg(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM)
+                                            : solve_newton(c, r, qs, fs, ls.w, it2, nrows > 0);
     if (nrows > 0) {
       qacc = qn;
       iters += it2;
@@ -2644,6 +2710,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 #ifndef ZB_WAVES_PER_EU
 #define ZB_WAVES_PER_EU 2
 #endif
+template <int SOLVER>
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   /* Chunked step (a.nchunk > 1, one control step): the launch has npair * nchunk workgroups, each
@@ -2746,7 +2813,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       if (!resetting && !ghost) feetech(c, ls);
       STAMP(S_FEETECH);
       int it_pass = 0;
-      forward(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, it_pass);
+      forward<SOLVER>(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, it_pass);
       if (!ghost) iters += it_pass;
       if (!resetting && !ghost) {
         integrate(c, s, ls);
@@ -2856,6 +2923,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
 #endif
 }
 
+template <int SOLVER>
 __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
@@ -2880,7 +2948,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   int it = 0;
   if (live) reset_prepare(c, s, ls, rnd);
   else load_params(c, s, ls, nullptr);
-  forward(c, s, ls, B, r, live, sen, it);
+  forward<SOLVER>(c, s, ls, B, r, live, sen, it);
   if (!live) return;
   observe(c, s, ls, B, sen, a.obs_actor ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
           a.obs_critic ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
@@ -2889,6 +2957,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
 }
 
 /* single forward on the stored (qpos, qvel), ctrl = action row; dumps internals */
+template <int SOLVER>
 __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
@@ -2908,7 +2977,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   Rows r;
   Sensors& sen = c.L->sen;
   int it = 0;
-  forward(c, s, ls, B, r, true, sen, it);
+  forward<SOLVER>(c, s, ls, B, r, true, sen, it);
   if (!live) return;
   float* d = a.dbg + (size_t)e * ZB_DBG_STRIDE;
   const int l = c.l;
@@ -2968,7 +3037,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
 
 int step_resident_blocks(int device) {
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel, 64, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON>, 64, 0) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
   return per_cu * cus;
 }
@@ -2983,7 +3052,8 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   const StepArgs& b = a;
 #endif
   dim3 grid((unsigned)((b.n_envs + NTEAM - 1) / NTEAM * b.nchunk)), block(64);
-  hipLaunchKernelGGL(step_kernel, grid, block, 0, s, b);
+  if (b.solver == ZB_SOLVER_CG) hipLaunchKernelGGL(step_kernel<ZB_SOLVER_CG>, grid, block, 0, s, b);
+  else hipLaunchKernelGGL(step_kernel<ZB_SOLVER_NEWTON>, grid, block, 0, s, b);
   return hipGetLastError();
 }
 /* ksim's FeetAirtimeReward over one trajectory (train.py:503-546), row 0. The fused step
@@ -3022,13 +3092,15 @@ hipError_t launch_airtime_exact(const StepArgs& a, hipStream_t s) {
 hipError_t launch_reset(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  hipLaunchKernelGGL(reset_kernel, grid, block, 0, s, a);
+  if (a.solver == ZB_SOLVER_CG) hipLaunchKernelGGL(reset_kernel<ZB_SOLVER_CG>, grid, block, 0, s, a);
+  else hipLaunchKernelGGL(reset_kernel<ZB_SOLVER_NEWTON>, grid, block, 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  hipLaunchKernelGGL(debug_forward_kernel, grid, block, 0, s, a);
+  if (a.solver == ZB_SOLVER_CG) hipLaunchKernelGGL(debug_forward_kernel<ZB_SOLVER_CG>, grid, block, 0, s, a);
+  else hipLaunchKernelGGL(debug_forward_kernel<ZB_SOLVER_NEWTON>, grid, block, 0, s, a);
   return hipGetLastError();
 }
 

@@ -145,6 +145,8 @@ int check_cfg(const ZbEnvConfig* c) {
     return fail(ZB_EARG, "config struct_bytes %d != %zu", c->struct_bytes, sizeof(ZbEnvConfig));
   if (c->n_substeps < 1 || c->iterations < 0 || c->ls_iterations < 0 || !(c->dt > 0.f))
     return fail(ZB_EARG, "invalid solver/timestep configuration");
+  if (c->solver != (int32_t)ZB_SOLVER_NEWTON && c->solver != (int32_t)ZB_SOLVER_CG)
+    return fail(ZB_EARG, "unknown solver %d", c->solver);
   return ZB_OK;
 }
 

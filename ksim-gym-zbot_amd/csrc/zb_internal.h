@@ -56,6 +56,7 @@ struct StepArgs {
   uint32_t* sched;          /* [2 + npair]: units taken, pairs finished, per-pair chunks done */
   int32_t* itpart;          /* [n] Newton iterations of the chunks so far */
   int air_mark;             /* first step of a rollout: save its contacts + causal airtime term */
+  int solver;               /* ZB_SOLVER_NEWTON / ZB_SOLVER_CG: which kernel instantiation runs */
 };
 
 /* workgroups of step_kernel resident on the device at once (occupancy x CUs) */

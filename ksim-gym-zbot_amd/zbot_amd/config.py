@@ -26,7 +26,12 @@ def default_config(
     dt: float = DT,
     ctrl_dt: float = CTRL_DT,
     max_episode_sec: float = 80.0,
+    solver: str = "newton",
 ) -> cs.ZbEnvConfig:
+    """solver: "newton" (MuJoCo's default, mj_solNewton) or "cg" (mj_solCG, which MJX training setups
+    commonly select for speed); which one ksim 0.1.99 sets on the model is [U]."""
+    if solver not in ("newton", "cg"):
+        raise ValueError(f"solver must be 'newton' or 'cg', got {solver!r}")
     c = cs.ZbEnvConfig()
     c.struct_bytes = ctypes.sizeof(cs.ZbEnvConfig)
     flags = 0
@@ -74,6 +79,7 @@ def default_config(
     c.rand_imu_tilt_std = math.radians(5)  # train.py:1453
     c.rand_imu_yaw_std = math.radians(1.0)
     c.rand_imu_pos_std = 0.005
+    c.solver = cs.SOLVER_CG if solver == "cg" else cs.SOLVER_NEWTON
     return c
 
 

@@ -96,6 +96,8 @@ ST_LENGTH = 1
 ST_DONE = 2
 ST_REWARD = 3
 
+SOLVER_NEWTON = 0  # ZB_SOLVER_NEWTON
+SOLVER_CG = 1  # ZB_SOLVER_CG
 F_OBS_NOISE = 1
 F_PUSH = 2
 F_RANDOMIZE = 4
@@ -253,7 +255,8 @@ class ZbEnvConfig(C.Structure):
         ("rand_imu_tilt_std", C.c_float),
         ("rand_imu_yaw_std", C.c_float),
         ("rand_imu_pos_std", C.c_float),
-        ("pad", _f(3)),
+        ("solver", C.c_int32),
+        ("pad", _f(2)),
     ]
 
 

@@ -805,16 +805,17 @@ static real line_search(const ZbModel* m, const ZbData* d, Solver* s, const ZbEn
   return alpha;
 }
 
-static void solve_newton(const ZbModel* m, ZbData* d, const ZbEnvConfig* cfg) {
+/* warmstart: qacc_warmstart vs qacc_smooth, keep the cheaper (mj_fwdConstraint); sets qacc,
+   s->Ma and efc_jar */
+static void warmstart(const ZbModel* m, ZbData* d, Solver* sp) {
   int nv = m->nv;
-  Solver s;
-  /* warmstart: qacc_warmstart vs qacc_smooth, keep the cheaper (mj_fwdConstraint) */
+  Solver* s = sp;
   {
     real jar_w[MAXEFC], cost_w = 0, cost_s = 0, f;
     int act;
     for (int i = 0; i < nv; i++) d->qacc[i] = d->qacc_warm[i];
-    mul_m(m, d->qM, d->qacc, s.Ma);
-    for (int i = 0; i < nv; i++) cost_w += (real)0.5 * (s.Ma[i] - d->qfrc_smooth[i]) * (d->qacc[i] - d->qacc_smooth[i]);
+    mul_m(m, d->qM, d->qacc, s->Ma);
+    for (int i = 0; i < nv; i++) cost_w += (real)0.5 * (s->Ma[i] - d->qfrc_smooth[i]) * (d->qacc[i] - d->qacc_smooth[i]);
     for (int r = 0; r < d->nefc; r++) {
       real v = 0, v2 = 0;
       for (int j = 0; j < nv; j++) {
@@ -827,7 +828,7 @@ static void solve_newton(const ZbModel* m, ZbData* d, const ZbEnvConfig* cfg) {
     }
     if (cost_w > cost_s) {
       for (int i = 0; i < nv; i++) d->qacc[i] = d->qacc_smooth[i];
-      mul_m(m, d->qM, d->qacc, s.Ma);
+      mul_m(m, d->qM, d->qacc, s->Ma);
       for (int r = 0; r < d->nefc; r++) {
         real v = 0;
         for (int j = 0; j < nv; j++) v += d->efc_J[r][j] * d->qacc[j];
@@ -837,6 +838,12 @@ static void solve_newton(const ZbModel* m, ZbData* d, const ZbEnvConfig* cfg) {
       for (int r = 0; r < d->nefc; r++) d->efc_jar[r] = jar_w[r];
     }
   }
+}
+
+static void solve_newton(const ZbModel* m, ZbData* d, const ZbEnvConfig* cfg) {
+  int nv = m->nv;
+  Solver s;
+  warmstart(m, d, &s);
   real scale = (real)1 / (m->meaninertia * (nv > 1 ? nv : 1));
   s.cost = update_constraint(m, d, &s);
   hessian_solve(m, d, &s);
@@ -864,6 +871,56 @@ static void solve_newton(const ZbModel* m, ZbData* d, const ZbEnvConfig* cfg) {
   d->solver_iters += iter;
 }
 
+/* Primal nonlinear conjugate gradient (mj_solCG; MJX solver.py with SolverType.CG): the same
+   warmstart, cost, exact line search and termination test as Newton; the direction is the
+   M^-1-preconditioned gradient (mj_solveM with the smooth factor qLD) with Polak-Ribiere
+   beta = max(0, grad . (Mgrad - Mgrad_prev) / max(MINVAL, grad_prev . Mgrad_prev)), and no
+   Hessian. As in solve_newton, an iteration that terminates skips the direction update, which
+   only feeds the next iteration. */
+static void solve_cg(const ZbModel* m, ZbData* d, const ZbEnvConfig* cfg) {
+  int nv = m->nv;
+  Solver s;
+  warmstart(m, d, &s);
+  real scale = (real)1 / (m->meaninertia * (nv > 1 ? nv : 1));
+  s.cost = update_constraint(m, d, &s);
+  for (int i = 0; i < nv; i++) s.Mgrad[i] = s.grad[i];
+  solve_m(m, d->qLD, d->qLDinv, s.Mgrad);
+  for (int i = 0; i < nv; i++) s.search[i] = -s.Mgrad[i];
+  int iter = 0;
+  while (iter < cfg->iterations) {
+    real alpha = line_search(m, d, &s, cfg);
+    if (alpha == 0) break;
+    for (int i = 0; i < nv; i++) {
+      d->qacc[i] += alpha * s.search[i];
+      s.Ma[i] += alpha * s.Mv[i];
+    }
+    for (int r = 0; r < d->nefc; r++) d->efc_jar[r] += alpha * s.Jv[r];
+    real oldcost = s.cost, gold[NDOF], mgold[NDOF];
+    for (int i = 0; i < nv; i++) {
+      gold[i] = s.grad[i];
+      mgold[i] = s.Mgrad[i];
+    }
+    s.cost = update_constraint(m, d, &s);
+    iter++;
+    real improvement = scale * (oldcost - s.cost);
+    real gn = 0;
+    for (int i = 0; i < nv; i++) gn += s.grad[i] * s.grad[i];
+    real gradient = scale * SQRT(gn);
+    if (improvement < cfg->tolerance || gradient < cfg->tolerance) break;
+    for (int i = 0; i < nv; i++) s.Mgrad[i] = s.grad[i];
+    solve_m(m, d->qLD, d->qLDinv, s.Mgrad);
+    real num = 0, den = 0;
+    for (int i = 0; i < nv; i++) {
+      num += s.grad[i] * (s.Mgrad[i] - mgold[i]);
+      den += gold[i] * mgold[i];
+    }
+    real beta = num / (den > MINVAL ? den : MINVAL);
+    if (!(beta > 0)) beta = 0;
+    for (int i = 0; i < nv; i++) s.search[i] = -s.Mgrad[i] + beta * s.search[i];
+  }
+  d->solver_iters += iter;
+}
+
 /* --------------------------- full forward pass ----------------------------- */
 static void forward(const ZbModel* m, ZbData* d, real dt, const ZbEnvConfig* cfg) {
   kinematics(m, d);
@@ -877,6 +934,8 @@ static void forward(const ZbModel* m, ZbData* d, real dt, const ZbEnvConfig* cfg
   smooth_forces(m, d);
   if (d->nefc == 0) {
     for (int i = 0; i < m->nv; i++) d->qacc[i] = d->qacc_smooth[i];
+  } else if (cfg->solver == ZB_SOLVER_CG) {
+    solve_cg(m, d, cfg);
   } else {
     solve_newton(m, d, cfg);
   }
@@ -1619,7 +1678,7 @@ static const FieldOff config_fields[] = {
     OFF(ZbEnvConfig, stay_alive_balance), OFF(ZbEnvConfig, rand_mass), OFF(ZbEnvConfig, rand_armature),
     OFF(ZbEnvConfig, rand_damping), OFF(ZbEnvConfig, rand_friction), OFF(ZbEnvConfig, rand_qpos0),
     OFF(ZbEnvConfig, rand_floor_mu), OFF(ZbEnvConfig, rand_imu_tilt_std), OFF(ZbEnvConfig, rand_imu_yaw_std),
-    OFF(ZbEnvConfig, rand_imu_pos_std), OFF(ZbEnvConfig, pad),
+    OFF(ZbEnvConfig, rand_imu_pos_std), OFF(ZbEnvConfig, solver), OFF(ZbEnvConfig, pad),
 };
 long zbo_field_offset(int which, const char* name) {
   const FieldOff* f = which == 0 ? model_fields : config_fields;

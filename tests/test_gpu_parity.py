@@ -147,14 +147,15 @@ def one_step_outputs(gs, out, st_ref, ref):
         yield "reward_terms", out["reward_terms"].cpu().numpy(), ref["reward_terms"]
 
 
+@pytest.mark.parametrize("solver", ["newton", "cg"])
 @pytest.mark.parametrize("push,randomize", [(False, False), (True, False), (False, True), (True, True)])
-def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize):
+def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize, solver):
     torch = torch_gpu
-    cfg = default_config(push=push, randomize=randomize)
+    cfg = default_config(push=push, randomize=randomize, solver=solver)
     n = 64
     env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
     eng = engine(cmodel, cfg, n, seed=7)
-    err = MaxErr(f"one-step push={push} randomize={randomize}")
+    err = MaxErr(f"one-step {solver} push={push} randomize={randomize}")
     for t in range(3):
         eng.set_state(torch.from_numpy(env.state.copy()))
         eng.set_rand(torch.from_numpy(env.rand.copy()))
@@ -225,9 +226,10 @@ def test_deterministic_and_shard_invariant(torch_gpu, cmodel, oracle_mod):
     assert np.array_equal(half.get_state().cpu().numpy(), states[0][n // 2:])
 
 
-def test_rollout_launch_equals_steps(torch_gpu, cmodel, oracle_mod):
+@pytest.mark.parametrize("solver", ["newton", "cg"])
+def test_rollout_launch_equals_steps(torch_gpu, cmodel, oracle_mod, solver):
     torch = torch_gpu
-    cfg = default_config()
+    cfg = default_config(solver=solver)
     n, T = 32, 5
     A = torch.from_numpy(np.stack([oracle_mod.synthetic_actions(cmodel.cmodel, 9, n, 0, t) for t in range(T)])).cuda()
     a = engine(cmodel, cfg, n, seed=9)

@@ -43,3 +43,32 @@ def test_primal_helper_known_answer():
     # minimize (a + 1)^2 + 3 a^2 for a < 0: a* = -1/4
     a = P.minimize(p)
     assert abs(a[0] + 0.25) < 1e-7
+
+
+def test_oracle_cg_solution_is_the_minimizer(oracle_mod, cmodel):
+    """The CG variant (mj_solCG: M^-1-preconditioned Polak-Ribiere, the same line search and
+    termination; solver type [U]) converges to the same minimizer when given
+    iterations (200 here; fp32 CG stalls a little above Newton's accuracy, hence 1e-3 / 1e-5), and
+    with train.py's 8 iterations it never ends above the cost it started from."""
+    cfg = default_config(solver="cg", iterations=200)
+    cfg8 = default_config(solver="cg")
+    st = P.states(oracle_mod, cmodel, cfg)
+    rng = np.random.default_rng(1)
+    gaps = []
+    for e in range(st.shape[0]):
+        ctrl = (rng.normal(size=20) * 1.5).astype(np.float32)
+        p = oracle_mod.constraint_problem(cmodel.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl=ctrl,
+                                          qaccw=st[e, 64:90])
+        a_star = P.minimize(p)
+        cg = P.cost_grad_fn(p)
+        c_star = cg(a_star)[0]
+        a = p["qacc"].astype(np.float64)
+        assert np.abs(a - a_star).max() <= 1e-3 * max(1.0, np.abs(a_star).max()), e
+        assert cg(a)[0] - c_star <= 1e-5 * abs(c_star), e
+        p8 = oracle_mod.constraint_problem(cmodel.cmodel, cfg8, st[e, :27], st[e, 32:58], ctrl=ctrl,
+                                           qaccw=st[e, 64:90])
+        c8 = cg(p8["qacc"].astype(np.float64))[0]
+        c_ws = min(cg(st[e, 64:90].astype(np.float64))[0], cg(p["qacc_smooth"].astype(np.float64))[0])
+        assert c8 <= c_ws + 1e-6 * abs(c_ws), e
+        gaps.append((c8 - c_star) / abs(c_star))
+    print(f"CG (8 iterations) cost above the minimum: median {np.median(gaps):.2e}, max {np.max(gaps):.2e}")
