@@ -516,8 +516,9 @@ def main() -> None:
     # algorithmic FLOPs per env-step, counted by the instrumented CPU twin on the C2 workload
     # (scripts/count_flops.py)
     algo_flop = None
-    fpath = os.path.join(ROOT, "profiles", "r02_flops_count.json")
-    if os.path.exists(fpath) and args.solver == "newton":  # the count is of the Newton solver
+    fpath = os.path.join(ROOT, "profiles", "r02_flops_count.json" if args.solver == "newton" else
+                         f"r03_flops_count_{args.solver}.json")
+    if os.path.exists(fpath):
         with open(fpath) as f:
             algo_flop = json.load(f)["as_run"]["flops_per_env_step"]
 
@@ -581,7 +582,8 @@ def main() -> None:
                 "issued_achieved": None if flop_per_env_step is None else
                 flop_per_env_step * n / (rate_ms * 1e-3) / 1e12,
                 "note": "achieved = algorithmic FLOPs per env-step (counted by the instrumented CPU twin on the C2 "
-                        "workload, FMA=2, profiles/r02_flops_count.json) x envs / rate_ms (as roofline); issued = PMC "
+                        f"workload with this solver, FMA=2, {os.path.relpath(fpath, ROOT)}) x envs / rate_ms (as "
+                        "roofline); issued = PMC "
                         "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 lane-FLOP; the binding resource of this "
                         "latency/VALU-bound kernel",
             },

@@ -55,13 +55,15 @@ def main():
     ap.add_argument("--envs", type=int, default=64)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--out", default="")
+    ap.add_argument("--solver", default="newton", choices=["newton", "cg"])
     args = ap.parse_args()
     cm = compile_model()
     res = {"workload": f"C2 standing task, {args.envs} envs x {args.steps} env-steps after 20 warm-up steps, "
-                       "JOINT_BIASES + 0.05 N(0,1) actions (zbo_synthetic_actions), Newton 8 / 8",
-           "note": "FMA counted as a multiply and an add; compares listed apart and not in the FLOPs"}
-    res["as_run"] = count(cm, default_config(), args.envs, args.steps)
-    fixed = default_config()
+                       f"JOINT_BIASES + 0.05 N(0,1) actions (zbo_synthetic_actions), {args.solver} 8 / 8",
+           "note": "FMA counted as a multiply and an add; compares listed apart and not in the FLOPs",
+           "solver": args.solver}
+    res["as_run"] = count(cm, default_config(solver=args.solver), args.envs, args.steps)
+    fixed = default_config(solver=args.solver)
     fixed.tolerance = -1.0
     fixed.ls_tolerance = -1.0
     res["fixed_iterations"] = count(cm, fixed, args.envs, args.steps)

@@ -56,20 +56,23 @@ class MaxErr:
     tolerance and printed, so a run's log shows how much headroom each bound has."""
 
     def __init__(self, name):
-        self.name, self.err = name, {}
+        self.name, self.err, self.bad = name, {}, []
 
     def add(self, key, got, ref, tol, rtol=0.0):
-        """|got - ref| <= tol + rtol |ref| elementwise; records the max absolute error."""
+        """|got - ref| <= tol + rtol |ref| elementwise; records the max absolute error (asserted in
+        report(), after every output has been measured)."""
         got = np.asarray(got, np.float64)
         ref = np.asarray(ref, np.float64)
         d = np.abs(got - ref)
         e = float(d.max()) if d.size else 0.0
         self.err[key] = max(self.err.get(key, 0.0), e)
         excess = float((d - rtol * np.abs(ref)).max()) if d.size else 0.0
-        assert excess <= tol, f"{self.name}: {key} max error {e:.3e} (excess {excess:.3e}) > {tol:.1e} + {rtol:.0e} |ref|"
+        if not excess <= tol:
+            self.bad.append(f"{key} max error {e:.3e} (excess {excess:.3e}) > {tol:.1e} + {rtol:.0e} |ref|")
 
     def report(self):
         print(f"\n[{self.name}] max |error|: " + ", ".join(f"{k} {v:.2e}" for k, v in self.err.items()))
+        assert not self.bad, f"{self.name}: " + "; ".join(self.bad)
 
 
 def test_engine_loads_native_library(torch_gpu, cmodel):
@@ -133,6 +136,22 @@ ONE_STEP_TOL = {
     "reward_terms": (5e-6, 0.0),
 }
 
+# The CG solver stops after train.py's 8 iterations well before convergence (tests/
+# test_solver_optimality.py: 0.5 % median cost gap), so the two implementations' rounding
+# differences ride along its unconverged path: a wider contract, ~5x the measured error (round 3,
+# profiles/r03_v4_gpu_tests.log: qpos 1.8e-5, qvel 5.1e-4, planner 3.8e-4, obs_critic 3.8e-3,
+# obs_extra 0.12 (the accelerations), reward 2.8e-4, terms 8.9e-5).
+ONE_STEP_TOL_CG = {
+    "qpos": (1e-4, 0.0),
+    "qvel": (2.5e-3, 0.0),
+    "planner": (2e-3, 0.0),
+    "obs_actor": (2.5e-3, 0.0),
+    "obs_critic": (2e-2, 0.0),
+    "obs_extra": (5e-1, 0.0),
+    "reward": (1.5e-3, 0.0),
+    "reward_terms": (5e-4, 0.0),
+}
+
 
 def one_step_outputs(gs, out, st_ref, ref):
     yield "qpos", gs[:, :27], st_ref[:, :27]
@@ -165,8 +184,9 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize, solver)
         torch.cuda.synchronize()
         gs = eng.get_state().cpu().numpy()
         np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
+        tol = ONE_STEP_TOL_CG if solver == "cg" else ONE_STEP_TOL
         for key, got, want in one_step_outputs(gs, out, env.state, ref):
-            err.add(key, got, want, *ONE_STEP_TOL[key])
+            err.add(key, got, want, *tol[key])
         # integer bookkeeping is exact
         for w in (cs.S_EP_STEPS, cs.S_RNG_STEP, cs.S_EPISODE):
             assert np.array_equal(gs[:, w].view(np.uint32), env.state[:, w].view(np.uint32))
