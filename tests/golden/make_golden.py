@@ -25,12 +25,14 @@ from zbot_amd import compile_model, default_config  # noqa: E402
 CASES = {
     "c1_seed0": dict(n=32, steps=16, seed=0, push=False, randomize=False, std=0.05),
     "c5_push_seed1": dict(n=16, steps=16, seed=1, push=True, randomize=True, std=0.1),
+    # round 3: the CG solver variant (ZbEnvConfig.solver)
+    "c2_cg_seed2": dict(n=16, steps=16, seed=2, push=False, randomize=False, std=0.05, solver="cg"),
 }
 
 
-def run_case(name, n, steps, seed, push, randomize, std):
+def run_case(name, n, steps, seed, push, randomize, std, solver="newton"):
     cm = compile_model()
-    cfg = default_config(push=push, randomize=randomize)
+    cfg = default_config(push=push, randomize=randomize, solver=solver)
     env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
     oa0, oc0, _ = env.reset()
     rewards, dones, actions = [], [], []
@@ -49,7 +51,10 @@ def run_case(name, n, steps, seed, push, randomize, std):
 
 
 def main():
+    only = sys.argv[1:]  # case names to (re)generate; default: all
     for name, kw in CASES.items():
+        if only and name not in only:
+            continue
         data = run_case(name, **kw)
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **data, **{f"cfg_{k}": v for k, v in kw.items()})
         print(name, {k: v.shape for k, v in data.items()})

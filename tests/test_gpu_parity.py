@@ -197,14 +197,17 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize, solver)
 # the final base position of the committed oracle fixtures.
 # Measured (round 3): rewards <= 1.8e-6 over the 8 steps, final base position <= 2.0e-6.
 GOLDEN_TOL = {"reward": 1e-5, "final_base_pos": 1e-5}
+# CG (unconverged 8 iterations, ONE_STEP_TOL_CG): the one-step reward error 2.8e-4 compounds over steps
+GOLDEN_TOL_CG = {"reward": 5e-3, "final_base_pos": 2e-3}
 
 
-@pytest.mark.parametrize("name", ["c1_seed0", "c5_push_seed1"])
+@pytest.mark.parametrize("name", ["c1_seed0", "c5_push_seed1", "c2_cg_seed2"])
 def test_golden_rollout(torch_gpu, cmodel, name):
     torch = torch_gpu
     g = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
     n, steps, seed = int(g["cfg_n"]), int(g["cfg_steps"]), int(g["cfg_seed"])
-    cfg = default_config(push=bool(g["cfg_push"]), randomize=bool(g["cfg_randomize"]))
+    solver = str(g["cfg_solver"]) if "cfg_solver" in g else "newton"
+    cfg = default_config(push=bool(g["cfg_push"]), randomize=bool(g["cfg_randomize"]), solver=solver)
     eng = engine(cmodel, cfg, n, seed=seed)
     out = eng.reset()
     torch.cuda.synchronize()
@@ -218,10 +221,11 @@ def test_golden_rollout(torch_gpu, cmodel, name):
     rew, done = np.stack(rew), np.stack(done)
     np.testing.assert_array_equal(done, g["done"])
     err = MaxErr(f"golden {name}")
+    tol = GOLDEN_TOL_CG if solver == "cg" else GOLDEN_TOL
     for t in range(8):
-        err.add(f"reward[{t}]", rew[t], g["reward"][t], GOLDEN_TOL["reward"])
+        err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"])
     gs = eng.get_state().cpu().numpy()
-    err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], GOLDEN_TOL["final_base_pos"])
+    err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], tol["final_base_pos"])
     err.add("final_rand", eng.get_rand().cpu().numpy(), g["final_rand"], 1e-6)
     err.report()
 
