@@ -373,6 +373,10 @@ def main() -> None:
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (default: the config's)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--model", default=None,
+                    help="robot: an MJCF (.xml) or descriptor (.json) file instead of the default Z-Bot-like "
+                         "descriptor, e.g. ksim-gym-zbot_amd/assets/zbot_like_limbs.xml (colliders beyond the "
+                         "soles: the general-collider kernels); roofline FLOP / traffic stay the default model's")
     ap.add_argument("--solver", default="newton", choices=["newton", "cg"],
                     help="constraint solver (ZbEnvConfig.solver): MuJoCo's Newton (default) or CG; which one "
                          "ksim sets is [U] (DESIGN.md §8)")
@@ -418,7 +422,14 @@ def main() -> None:
 
     conf = CONFIGS[args.config]
     n = args.envs or conf["envs"]
-    cm = compile_model()
+    if args.model is None:
+        cm = compile_model()
+    elif args.model.endswith(".xml"):
+        from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
+
+        cm = compile_model(load_mjcf(args.model))
+    else:
+        cm = compile_model(args.model)
     cfg = default_config(push=conf["push"], randomize=conf["randomize"], solver=args.solver)
     G = max(1, args.groups)
     if G > 1:
@@ -531,7 +542,7 @@ def main() -> None:
     # algorithmic FLOPs per env-step, counted by the instrumented CPU twin on the C2 workload
     # (scripts/count_flops.py)
     algo_flop = None
-    fpath = os.path.join(ROOT, "profiles", "r02_flops_count.json" if args.solver == "newton" else
+    fpath = os.path.join(ROOT, "profiles", "r03_flops_count.json" if args.solver == "newton" else
                          f"r03_flops_count_{args.solver}.json")
     if os.path.exists(fpath):
         with open(fpath) as f:
@@ -566,6 +577,7 @@ def main() -> None:
                 + (f"; {G} env groups of {n // G} per GPU, each zb_step-ing on its own HIP stream" if G > 1 else ""),
                 "groups_per_gpu": G,
                 "avg_solver_iters_per_env_step": iters,
+                **({"model": args.model, "colliders": cm.geom_names} if args.model else {}),
             },
             "roofline": {
                 "bound": "hbm",

@@ -65,8 +65,11 @@ void zb_default_config(ZbEnvConfig* cfg);
  * against it (ZB_EMODEL otherwise): 26 bodies of which only the floating base
  * (body 1, free joint) branches; nu = 20 hinge actuators, nv = 26; the free
  * joint's 6 dofs form the root of the dof tree and every limb is an
- * unbranched chain of consecutive dofs; 2 foot sole boxes; body depth 8,
- * dof depth 12.
+ * unbranched chain of consecutive dofs of at most 6 (dof depth <= 12); body
+ * depth <= 8; 1 to 4 floor colliders (boxes, capsules, spheres; model
+ * nskip_geom = 0). Exactly two box colliders (the soles) run the two-sole
+ * kernels; any other collider set runs the general-collider instantiation
+ * (a second bank of 32 contact rows, larger LDS).
  *
  * Create a handle simulating `n_envs` environments whose global ids are
  * [env_offset, env_offset + n_envs) — RNG streams are keyed by global id, so

@@ -14,7 +14,8 @@
  *   - a kinematic tree with at most one joint per body; joint types: free
  *     (root only) or hinge; other bodies are welded (no joint);
  *   - nbody <= ZB_MAX_BODY, nv <= ZB_MAX_DOF, dof-chain depth <= ZB_MAX_DEPTH;
- *   - collision = floor plane (world geom) vs per-body boxes (foot soles);
+ *   - collision = floor plane (world geom) vs up to ZB_MAX_GEOM per-body boxes,
+ *     capsules or spheres (the two foot soles first by convention);
  *   - actuators = motors on hinge joints (joint transmission, gear).
  * All floats are fp32; all vectors are padded to 4 so rows are 16-B aligned.
  */
@@ -28,22 +29,27 @@ extern "C" {
 #endif
 
 #define ZB_MODEL_MAGIC   0x5A424F54u /* 'ZBOT' */
-#define ZB_MODEL_VERSION 5
+#define ZB_MODEL_VERSION 6
 
 #define ZB_MAX_BODY  32
 #define ZB_MAX_DOF   32
 #define ZB_MAX_QPOS  40
 #define ZB_MAX_DEPTH 12
-#define ZB_MAX_GEOM  4   /* colliding boxes */
+#define ZB_MAX_GEOM  4   /* floor colliders */
 #define ZB_MAX_SITE  8
 #define ZB_MAX_ACT   32
-#define ZB_CON_PER_GEOM 4 /* plane-box: the 4 sole corners */
+#define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-capsule 2, plane-sphere 1 */
 #define ZB_MAX_CON  (ZB_MAX_GEOM * ZB_CON_PER_GEOM)
 
 /* joint types (mjtJoint values where they exist) */
 #define ZB_JNT_NONE  -1
 #define ZB_JNT_FREE   0
 #define ZB_JNT_HINGE  3
+
+/* collider types (mjtGeom values) */
+#define ZB_GEOM_SPHERE  2
+#define ZB_GEOM_CAPSULE 3
+#define ZB_GEOM_BOX     6
 
 typedef struct ZbModel {
   /* header */
@@ -116,11 +122,13 @@ typedef struct ZbModel {
   float    fe_max_torque[ZB_MAX_ACT];    /* stored, never applied (train.py:1221) */
   float    fe_max_velocity[ZB_MAX_ACT];
 
-  /* collision geoms: boxes colliding with the floor plane z=0 */
+  /* collision geoms colliding with the floor plane z=0 */
   int32_t  geom_body[ZB_MAX_GEOM];
+  int32_t  geom_type[ZB_MAX_GEOM];      /* ZB_GEOM_* */
   float    geom_pos[ZB_MAX_GEOM][4];
   float    geom_quat[ZB_MAX_GEOM][4];
-  float    geom_size[ZB_MAX_GEOM][4];    /* box half sizes */
+  float    geom_size[ZB_MAX_GEOM][4];    /* mjModel.geom_size: box half sizes; capsule radius,
+                                           half-length (local z); sphere radius */
   /* floor: geom_priority=2 (train.py:1330) -> floor friction/solref/solimp win */
   float    floor_friction[4];            /* sliding, torsional, rolling */
   float    floor_solref[4];
@@ -148,14 +156,15 @@ typedef struct ZbModel {
   int32_t  max_body_depth;
   int32_t  mrow_size;                  /* packed depth-indexed row storage (floats) */
   int32_t  nskip_geom;                 /* colliding geoms of the source model the engine cannot
-                                          collide (not box soles): zb_create rejects nskip_geom > 0 */
+                                          collide (other types, or past ZB_MAX_GEOM): zb_create
+                                          rejects nskip_geom > 0 */
   int32_t  pad_tab;
   int32_t  body_nchild[ZB_MAX_BODY];
   int32_t  body_child[ZB_MAX_BODY][8]; /* -1 padded */
   int32_t  depth_maxchild[16];         /* max #children over bodies at a depth */
   uint32_t dof_desc[ZB_MAX_DOF];       /* bitmask of strict descendant dofs */
   uint32_t dof_ancpk[ZB_MAX_DOF][4];   /* dof_anc as bytes: byte (e&3) of word e>>2 */
-  uint32_t dof_rowmask[ZB_MAX_DOF];    /* contact rows (16 per geom) whose chain holds the dof */
+  uint32_t dof_rowmask[ZB_MAX_DOF];    /* contact rows (16 per geom, geoms 0-1) whose chain holds the dof */
   int32_t  dof_act[ZB_MAX_DOF];        /* actuator driving the dof or -1 */
   int32_t  dof_rowoff[ZB_MAX_DOF];     /* offset of the dof's row in packed storage */
   int32_t  geom_lastdof[ZB_MAX_GEOM];

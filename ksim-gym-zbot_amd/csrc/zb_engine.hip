@@ -48,7 +48,7 @@ constexpr int RMAX = 6;  /* root dof chain factored as one dense block: the free
 constexpr int NB = ZB_NBODY_TASK;
 constexpr int NV = 6 + ZB_NJ;
 constexpr int NROOT = RMAX;
-constexpr int NGEOM = 2;      /* foot sole boxes */
+constexpr int NGEOM = 2;      /* geoms per contact-row bank (bank 0: the two foot soles) */
 constexpr int MAXBD = 8;      /* deepest body (world 0, base 1, ..., foot 8) */
 constexpr int MAXDD = 12;     /* dof chain depth: 6 root + 6 leg */
 constexpr int NLIMBLV = 6;    /* elimination levels inside the limbs (longest limb) */
@@ -107,6 +107,17 @@ struct __align__(16) EnvL {
 
 /* the block's two team working sets (one wave = two teams) */
 __shared__ EnvL g_lds[NTEAM];
+
+/* The second contact-row bank of the general-collider kernels (XG: geoms 2-3, or any model that is
+   not exactly two box soles): its Jacobian rows. Its J'DJ blocks are staged in the Hessian rows'
+   space and its per-row scratch reuses rowDA / rowF after the first bank's (hessian_factor), so a
+   block of the XG kernels needs 3 KB more LDS, not 6: 7 blocks per CU instead of 6. Only the XG
+   instantiations reference it, so the LDS of the two-sole kernels is unchanged. */
+struct __align__(16) EnvX {
+  float J[32][CAP];
+};
+__shared__ EnvX g_ldsx[NTEAM];
+__device__ __forceinline__ EnvX* envx() { return &g_ldsx[(threadIdx.x & 63) / TEAM]; }
 
 /* ----------------------------- team primitives ----------------------------- */
 __device__ __forceinline__ float tsh(float v, int src) { return __shfl(v, src, TEAM); }
@@ -573,7 +584,8 @@ struct Ctx {
   uint64_t lvlch; /* per body depth: max #children among bodies at that depth (4 bits each) */
   /* lane as dof */
   int ddep, dbody, qadr, act;
-  uint32_t rowmask; /* contact rows whose Jacobian chain contains dof l */
+  uint32_t rowmask;  /* contact rows whose Jacobian chain contains dof l */
+  uint32_t rowmask2; /* the same in the second bank (XG) */
   int dk0;          /* index of dof l within its body's joint (free joint: 0..5) */
   int dfree;        /* dof l belongs to a free joint */
 };
@@ -608,6 +620,16 @@ struct BodyK {
   float xp[3], xq[4]; /* rotation matrices are recomputed from xq where needed */
   float cv[6];
 };
+/* a contact row of the second bank (XG), held by the lane like Rows' own */
+struct XRow {
+  bool any; /* wave-uniform: some row of the bank exists in either env of the wave */
+  bool ex;
+  int chd; int kdep;
+  float aref, D, jar, Jv, f;
+  int act;
+  int nrow;
+  uint32_t exmask;
+};
 /* constraint rows held by the lane */
 struct Rows {
   /* contact row (lane = row) */
@@ -623,6 +645,7 @@ struct Rows {
   float sl, al, Dl, jl, flim; int actl;
   int nrow;
   uint32_t exmask; /* team-uniform: existing contact rows */
+  XRow x;          /* second bank (XG kernels only) */
 };
 
 /* 16-byte LDS row access (rows are 12 floats = 48 B, 16-B aligned) */
@@ -1276,18 +1299,23 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
   return y;
 }
 
-/* chain gather: sum_e Jc[e] * vec[slot][anc_e] for a contact row */
-__device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) {
-  const int kdep = vopq(r.kdep);
+/* chain gather: sum_e Jc[e] * vec[slot][anc_e] for a contact row (Jrow: the row in bank 0's or
+   bank 1's J, chd: the row's chain head) */
+__device__ __forceinline__ float row_dot(const Ctx& c, const float* Jrow, int chd, int slot) {
   float jr[CAP], vv[CAP];
-  ld_row(&c.L->u.J[c.l][0], jr);
+  ld_row(Jrow, jr);
 #pragma unroll
-  for (int e = 0; e < CAP; e++) vv[e] = c.L->vec[slot][anc_lin(r.chd, e)];
+  for (int e = 0; e < CAP; e++) vv[e] = c.L->vec[slot][anc_lin(chd, e)];
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < CAP; e++) v += jr[e] * vv[e]; /* zero past the row's depth */
-  (void)kdep;
   return v;
+}
+__device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) {
+  return row_dot(c, &c.L->u.J[c.l][0], r.chd, slot);
+}
+__device__ __forceinline__ float row_dot_x(const Ctx& c, const Rows& r, int slot) {
+  return row_dot(c, &envx()->J[c.l][0], r.x.chd, slot);
 }
 
 /* ----------------------------------- RNE ----------------------------------- */
@@ -1440,54 +1468,111 @@ __device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, floa
   aref = -bb * vel - kk * imp * pos;
 }
 
-/* Plane-box contact of team lane l = 16*geom + 4*corner + edge: the sole corner
- * (mid-penetration point, as mj_collidePlaneBox), the pyramid edge direction
- * n +- mu t (frame of mju_makeFrame(+z): t1 = +y, t2 = -x) and the friction
- * coefficient; returns the signed distance (> margin: no contact). Recomputed
- * by the sensors instead of being held in registers through the solver. */
-__device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, const BodyK& B, float pos[3], float dir[3],
-                                               float& mu) {
+/* The collider of team lane l in contact-row bank `bank`: geom 2 bank + l / 16 (XG), or sole l / 16
+   of the two-sole kernels. gb: its body; false when the model has no such geom. */
+template <bool XG>
+__device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& gb) {
+  MP m = c.m;
+  const int gl = c.l >> 4;
+  g = XG ? 2 * bank + gl : gl;
+  const bool gvalid = XG ? g < m->ngeom : gl < NGEOM;
+  if (!gvalid) g = 0;
+  gb = gvalid ? m->geom_body[g] : 0;
+  return gvalid;
+}
+
+/* Floor contact of team lane l = 16*geom + 4*slot + edge (MuJoCo's primitive colliders,
+ * engine_collision_primitive.c; oracle collision()):
+ *   box (mjc_PlaneBox): contact slot k holds the corner of the pair (k, 7-k) that lies below the
+ *     box centre along the normal: corner k = (+-x, +-y, -z) by the bits of k, or its mirror
+ *     7-k = -corner k. Exactly those four corners pass MuJoCo's "offset along the normal <= 0"
+ *     test (an offset of exactly zero aside), so the set is MuJoCo's; only the row order differs.
+ *   capsule (mjc_PlaneCapsule, XG): slots 0 / 1 = the sphere at the +/- half-length end, tangent
+ *     frame along the axis projected on the plane (mjx plane_capsule: +y when that projection is
+ *     shorter than 0.5);
+ *   sphere (mjc_PlaneSphere, XG): slot 0.
+ * Sets the contact point (the deepest point moved back by half the distance), the pyramid edge
+ * direction n +- mu t (t1 = +y, t2 = n x t1 = -x for boxes and spheres: mju_makeFrame(+z)) and the
+ * friction; returns the signed distance, 1e30 where the slot holds no contact. Recomputed by the
+ * sensors instead of being held in registers through the solver. */
+template <bool XG>
+__device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, const BodyK& B, int bank, float pos[3],
+                                               float dir[3], float& mu) {
   MP m = c.m;
   const int l = c.l;
-  const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
-  const bool gvalid = g < NGEOM;
-  const int gg = gvalid ? g : 0;
-  const int gb = gvalid ? m->geom_body[g] : 0;
+  const int slot = (l >> 2) & 3, edge = l & 3;
+  int g, gb;
+  const bool gvalid = lane_geom<XG>(c, bank, g, gb);
   float xp[3], xqs[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) xqs[k] = tsh(B.xq[k], gb);
 #pragma unroll
   for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
-  /* corner in the body frame (geom_pos + geom_quat * local corner), then to the
-     world by the body's frame: two quaternion rotations */
-  float gq[4] = {m->geom_quat[gg][0], m->geom_quat[gg][1], m->geom_quat[gg][2], m->geom_quat[gg][3]}, t[3], gl[3];
-  float loc[3] = {(corner & 1) ? m->geom_size[gg][0] : -m->geom_size[gg][0],
-                  (corner & 2) ? m->geom_size[gg][1] : -m->geom_size[gg][1], -m->geom_size[gg][2]};
-  quat_rotate(t, gq, loc);
+  const int ty = XG ? m->geom_type[g] : ZB_GEOM_BOX;
+  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE;
+  /* the lane's point relative to the geom centre, geom frame -> body frame -> world */
+  float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
+  float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
+  const float s0 = m->geom_size[g][0], s1 = m->geom_size[g][1], s2 = m->geom_size[g][2];
+  float v[3];
+  if (box) {
+    v[0] = (slot & 1) ? s0 : -s0;
+    v[1] = (slot & 2) ? s1 : -s1;
+    v[2] = -s2;
+  } else {
+    v[0] = 0.f;
+    v[1] = 0.f;
+    v[2] = cap ? (slot == 0 ? s1 : -s1) : 0.f;
+  }
+  float w[3], t[3];
+  quat_rotate(w, gq, v);
+  if (box) {
+    /* the corner's offset along the normal: the z row of the body rotation times w */
+    const float rz0 = 2.f * (xqs[1] * xqs[3] - xqs[0] * xqs[2]), rz1 = 2.f * (xqs[2] * xqs[3] + xqs[0] * xqs[1]);
+    const float rz2 = 1.f - 2.f * (xqs[1] * xqs[1] + xqs[2] * xqs[2]);
+    if (rz0 * w[0] + rz1 * w[1] + rz2 * w[2] > 0.f) {
+      /* corner k lies above the centre: its mirror 7-k is the one MuJoCo keeps */
 #pragma unroll
-  for (int k = 0; k < 3; k++) gl[k] = m->geom_pos[gg][k] + t[k];
+      for (int k = 0; k < 3; k++) w[k] = -w[k];
+    }
+  }
+  float gl[3] = {gp[0] + w[0], gp[1] + w[1], gp[2] + w[2]};
   quat_rotate(t, xqs, gl);
-  float p[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2]};
-  float dist = p[2];
+  const float rad = box ? 0.f : s0;
+  float p[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2] - rad};
+  const float dist = p[2];
   pos[0] = p[0]; pos[1] = p[1]; pos[2] = p[2] - 0.5f * dist;
   mu = m->floor_friction[0] * s.floor_mu;
-  float sg = (edge & 1) ? -mu : mu;
-  if (edge < 2) { dir[0] = 0.f; dir[1] = sg; dir[2] = 1.f; }
-  else { dir[0] = -sg; dir[1] = 0.f; dir[2] = 1.f; }
-  return dist;
+  float t1x = 0.f, t1y = 1.f;
+  if (cap) {
+    /* the +z axis of the capsule in the world: the rotated offset / half-length, sign of the +end */
+    float u[3];
+    quat_rotate(u, xqs, w);
+    const float ax = slot == 0 ? u[0] : -u[0], ay = slot == 0 ? u[1] : -u[1];
+    const float bn = sqrtf(ax * ax + ay * ay) / s1;
+    const bool dflt = bn < 0.5f;
+    const float inv = dflt ? 0.f : 1.f / (bn * s1);
+    t1x = dflt ? 0.f : ax * inv;
+    t1y = dflt ? 1.f : ay * inv;
+  }
+  const float sg = (edge & 1) ? -mu : mu;
+  /* edges 0/1: n +- mu t1; 2/3: n +- mu t2, t2 = n x t1 = (-t1y, t1x, 0) */
+  dir[0] = edge < 2 ? sg * t1x : -sg * t1y;
+  dir[1] = edge < 2 ? sg * t1y : sg * t1x;
+  dir[2] = 1.f;
+  const bool slot_ok = box || (cap ? slot < 2 : slot == 0);
+  return (gvalid && slot_ok) ? dist : 1e30f;
 }
 
-/* collision + contact rows (lane r) + dof rows (lane j) */
-__device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
-                                 Rows& r) {
+/* the contact rows of one bank: collision, then the row of lane l (J at Jrow) */
+template <bool XG, typename CR>
+__device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const BodyK& B, const float cm[3], int bank,
+                                             CR& r, float* Jrow) {
   MP m = c.m;
   CP cfg = c.cfg;
   EnvL* L = c.L;
-  const int l = c.l;
-  /* ---- contact rows: lane = 16*geom + 4*corner + edge ---- */
-  const int g = l >> 4, corner = (l >> 2) & 3, edge = l & 3;
-  const bool gvalid = g < NGEOM;
-  const int gb = gvalid ? m->geom_body[g] : 0;
+  int g, gb;
+  const bool gvalid = lane_geom<XG>(c, bank, g, gb);
   int kd = gvalid ? m->body_lastdof[gb] : 0;
   if (kd < 0) kd = 0;
   r.chd = tshi(c.chd, kd);
@@ -1503,8 +1588,8 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
 #pragma unroll
   for (int e = 0; e < CAP; e++) Jc[e] = 0.f;
   float pos[3], dir[3], mu;
-  const float dist = contact_point(c, s, B, pos, dir, mu);
-  if (gvalid && dist < m->floor_margin) {
+  const float dist = contact_point<XG>(c, s, B, bank, pos, dir, mu);
+  if (dist <= m->floor_margin) {
     r.ex = true;
     float off[3] = {pos[0] - cm[0], pos[1] - cm[1], pos[2] - cm[2]}, sa[3];
     cross3(sa, off, dir);
@@ -1534,7 +1619,23 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   r.exmask = tb;
   /* every row is stored, zero where there is no contact (and past the row's
      depth), so the row products below need no per-entry masks */
-  st_row(&L->u.J[l][0], Jc);
+  st_row(Jrow, Jc);
+}
+
+/* collision + contact rows (lane r; XG: both banks) + dof rows (lane j) */
+template <bool XG>
+__device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
+                                 Rows& r) {
+  MP m = c.m;
+  CP cfg = c.cfg;
+  const int l = c.l;
+  contact_rows<XG>(c, s, B, cm, 0, r, &c.L->u.J[l][0]);
+  if constexpr (XG) {
+    contact_rows<XG>(c, s, B, cm, 1, r.x, &envx()->J[l][0]);
+    /* the second bank's work is skipped, bit for bit, while no row of it exists in the wave (the
+       usual case: shins and hands off the floor) */
+    r.x.any = __ballot(r.x.ex) != 0ull;
+  }
   /* ---- dof rows (lane j) ---- */
   r.hf = r.hl = false;
   r.actf = r.actl = 0;
@@ -1600,8 +1701,9 @@ __device__ __forceinline__ float eval_one(float jar, float D, float& force, int&
   return on ? 0.5f * D * jar * jar : 0.f;
 }
 
-/* row costs at given jar values (no state change) */
-__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jl_) {
+/* row costs at given jar values (no state change); jx: the second bank's contact row (XG) */
+template <bool XG>
+__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jl_, float jx) {
   float f;
   int a;
   const float k0 = eval_one(jc, r.D, f, a);
@@ -1611,12 +1713,49 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
   cost += r.ex ? k0 : 0.f;
   cost += r.hf ? k1 : 0.f;
   cost += r.hl ? k2 : 0.f;
+  if constexpr (XG) {
+    const float k3 = eval_one(jx, r.x.D, f, a);
+    cost += r.x.ex ? k3 : 0.f;
+  }
   return cost;
+}
+
+/* sum_r J_r[e] f_r over the 16 contact rows of a geom (one 16-lane DPP row; they share the geom's
+   dof chain): a transposing butterfly over the rows (pairings: row mirror, half-row mirror, quad
+   xor 2, quad xor 1). At each stage a lane keeps the half of its column sums on its side and adds
+   its partner's copy of them, so lane 16 f + e ends with the geom-f sum of column e (45 instead of
+   108 VALU instructions). */
+__device__ __forceinline__ float colsum16(const float* Jrow, float fr) {
+  float q[16];
+  {
+    float jr[CAP];
+    ld_row(Jrow, jr);
+#pragma unroll
+    for (int e = 0; e < CAP; e++) q[e] = jr[e] * fr; /* J rows are zero where no contact */
+#pragma unroll
+    for (int e = CAP; e < 16; e++) q[e] = 0.f;
+  }
+  const int li = threadIdx.x & 15;
+  float u8[8], u4[4], u2[2];
+  {
+    const bool s1 = li >= 8;
+#pragma unroll
+    for (int k = 0; k < 8; k++) u8[k] = (s1 ? q[8 + k] : q[k]) + dppf<0x140>(s1 ? q[k] : q[8 + k]);
+    const bool s2 = (li & 4) != 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) u4[k] = (s2 ? u8[4 + k] : u8[k]) + dppf<0x141>(s2 ? u8[k] : u8[4 + k]);
+    const bool s3 = (li & 2) != 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) u2[k] = (s3 ? u4[2 + k] : u4[k]) + dppf<0x4E>(s3 ? u4[k] : u4[2 + k]);
+  }
+  const bool s4 = (li & 1) != 0;
+  return (s4 ? u2[1] : u2[0]) + dppf<0xB1>(s4 ? u2[0] : u2[1]);
 }
 
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
 /* returns this lane's cost share; the caller reduces it over the team (alone, or together with
    the Newton loop's other per-iteration sums in one tsum_n) */
+template <bool XG>
 __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, float qacc, float qs, float fs,
                                                        float Ma, float& grad) {
   const int ddep = vopq(c.ddep);
@@ -1642,55 +1781,41 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, f
   }
   if (r.ex) L->rowF[c.l] = r.f;
   L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
-  /* J'f per dof: the 16 contact rows of a foot are one 16-lane DPP row and
-     share the foot's dof chain, so sum_r J_r[e] f_r (e = chain position) is
-     a row reduction for all 12 positions at once (interleaved DPP, no LDS);
-     a dof adds the sums of every foot whose chain holds it at its depth */
-  float q[16];
-  {
-    float jr[CAP];
-    ld_row(&L->u.J[c.l][0], jr);
-    const float fr = r.ex ? r.f : 0.f;
-#pragma unroll
-    for (int e = 0; e < CAP; e++) q[e] = jr[e] * fr; /* J rows are zero where no contact */
-#pragma unroll
-    for (int e = CAP; e < 16; e++) q[e] = 0.f;
+  float sx0 = 0.f, sx1 = 0.f;
+  if (XG && r.x.any) {
+    EnvX* X = envx();
+    float f3;
+    int a3;
+    const float k3 = eval_one(r.x.jar, r.x.D, f3, a3);
+    cost += r.x.ex ? k3 : 0.f;
+    r.x.f = r.x.ex ? f3 : r.x.f;
+    r.x.act = r.x.ex ? a3 : r.x.act;
+    const float cx = colsum16(&X->J[c.l][0], r.x.ex ? r.x.f : 0.f);
+    sx0 = tsh(cx, ddep);
+    sx1 = tsh(cx, 16 + ddep);
   }
-  /* transposing butterfly over the 16 rows of the foot (pairings: row mirror, half-row
-     mirror, quad xor 2, quad xor 1): at each stage a lane keeps the half of its column
-     sums on its side and adds its partner's copy of them, so lane 16f + e ends with
-     the foot-f sum of column e (45 instead of 108 VALU instructions) */
-  const int li = threadIdx.x & 15;
-  float u8[8], u4[4], u2[2];
-  {
-    const bool s1 = li >= 8;
-#pragma unroll
-    for (int k = 0; k < 8; k++) u8[k] = (s1 ? q[8 + k] : q[k]) + dppf<0x140>(s1 ? q[k] : q[8 + k]);
-    const bool s2 = (li & 4) != 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) u4[k] = (s2 ? u8[4 + k] : u8[k]) + dppf<0x141>(s2 ? u8[k] : u8[4 + k]);
-    const bool s3 = (li & 2) != 0;
-#pragma unroll
-    for (int k = 0; k < 2; k++) u2[k] = (s3 ? u4[2 + k] : u4[k]) + dppf<0x4E>(s3 ? u4[k] : u4[2 + k]);
-  }
-  const bool s4 = (li & 1) != 0;
-  const float colsum = (s4 ? u2[1] : u2[0]) + dppf<0xB1>(s4 ? u2[0] : u2[1]);
-  /* a dof adds the column sum at its depth of every foot whose chain holds it */
+  /* J'f per dof: a dof adds the column sum at its depth of every geom whose chain holds it */
+  const float colsum = colsum16(&L->u.J[c.l][0], r.ex ? r.f : 0.f);
   const float so = tsh(colsum, ddep), sx = tsh(colsum, 16 + ddep);
   tsync();
   float qc = 0.f;
   if (c.l < NV) {
     const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
     qc = (f0 ? so : 0.f) + (f1 ? sx : 0.f);
+    if constexpr (XG) {
+      const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
+      qc += (f2 ? sx0 : 0.f) + (f3 ? sx1 : 0.f);
+    }
     if (r.hf) qc += r.ff;
     if (r.hl) qc += r.sl * r.flim;
   }
   grad = Ma - fs - qc;
   return cost;
 }
+template <bool XG>
 __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float qacc, float qs, float fs, float Ma,
                                                   float& grad) {
-  return tsum(update_constraint_lane(c, r, qacc, qs, fs, Ma, grad));
+  return tsum(update_constraint_lane<XG>(c, r, qacc, qs, fs, Ma, grad));
 }
 
 /* G_f = sum_{r in foot f} D_r J_r J_r' (depth-indexed 12x12) for both feet of
@@ -1698,7 +1823,10 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
  * v_mfma_f32_16x16x4_f32 over the foot's 16 contact rows (K = 4 rows each;
  * lane l supplies row 4*chunk + l/16, entry l%16). Staged in the env's L[][]
  * as [foot][12][12]; L[][] is free until factor_ldl writes it. D is rowDA
- * (0 for absent / inactive rows). Wave-uniform: call with every lane active. */
+ * (0 for absent / inactive rows). Wave-uniform: call with every lane active.
+ * BANK2: the same for the second bank's geoms (EnvX J, rowDA holding that bank's D), staged in
+ * the Hessian rows Hs[][], free until hessian_factor stores the assembled rows. */
+template <bool BANK2>
 __device__ __forceinline__ void jdj_mfma() {
   const int l = threadIdx.x & 63;
   const int e = l & 15, k = l >> 4;
@@ -1717,8 +1845,8 @@ __device__ __forceinline__ void jdj_mfma() {
         const int r = 16 * f + 4 * ch + k;
         /* no masks: rowDA is zero for absent / inactive rows, and output rows or
            columns e >= CAP (lanes reading entry CAP-1) are never stored */
-        const float jv = g_lds[t].u.J[r][ec];
-        const float dv = g_lds[t].rowDA[r];
+        const float jv = BANK2 ? g_ldsx[t].J[r][ec] : g_lds[t].u.J[r][ec];
+        const float dv = g_lds[t].rowDA[r]; /* BANK2: the second bank's, written by hessian_factor */
         acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv * jv, jv, acc[t][f], 0, 0, 0);
       }
   /* lane l holds G[4*(l/16) + v][l%16], v = 0..3: G is symmetric (to rounding), so the
@@ -1729,24 +1857,59 @@ __device__ __forceinline__ void jdj_mfma() {
     for (int t = 0; t < NTEAM; t++)
 #pragma unroll
       for (int f = 0; f < NGEOM; f++)
-        *reinterpret_cast<v4f*>(&g_lds[t].L[0][0] + f * CAP * CAP + e * CAP + 4 * k) = acc[t][f];
+        *reinterpret_cast<v4f*>((BANK2 ? &g_lds[t].Hs[0][0] : &g_lds[t].L[0][0]) + f * CAP * CAP + e * CAP + 4 * k) =
+            acc[t][f];
 }
 
-/* H = M + J' D_active J rows (depth-indexed), then factor -> Dinv */
+/* H[e] += D_r J_r[e] J_r' over the rows of bitmask tb (pairs of rows per pass; da: the rows' D) */
+__device__ __forceinline__ void add_rows(uint32_t tb, const float (*J)[CAP], const float* da, int ddep, float H[CAP],
+                                         float& Hd) {
+  while (tb) {
+    const int k0 = __ffs(tb) - 1;
+    tb &= tb - 1u;
+    const bool h1 = tb != 0u;
+    const int k1 = h1 ? __ffs(tb) - 1 : k0;
+    tb &= tb - 1u;
+    float j0[CAP], j1[CAP];
+    ld_row(&J[k0][0], j0);
+    ld_row(&J[k1][0], j1);
+    const float jd0 = J[k0][ddep], jd1 = J[k1][ddep];
+    const float jj0 = da[k0] * jd0;
+    const float jj1 = (da[k1] * jd1) * (h1 ? 1.f : 0.f); /* a weight, not a select (loads) */
+    Hd += jj0 * jd0;
+    Hd += jj1 * jd1;
+#pragma unroll
+    for (int e = 0; e < CAP; e++) {
+      H[e] += jj0 * j0[e]; /* entries at or past the depth are never read */
+      H[e] += jj1 * j1[e];
+    }
+  }
+}
+
 /* H = M + J' D_active J (depth-indexed rows), then factor -> 1/D_j.
  * full: from M and every active contact row. Otherwise the stored unfactored
  * H of the previous build is updated with the rows whose activity changed
  * (+-D_r J_r J_r') -- MuJoCo's Newton also only re-assembles on a change of
- * the active set, and the change is usually a handful of rows. */
-__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo) {
+ * the active set, and the change is usually a handful of rows. XG: both banks. */
+template <bool XG>
+__device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo,
+                                                int pa2) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float H[CAP], Hd;
-  uint32_t tb;
+  uint32_t tb, tb2 = 0u;
+  float dl2 = 0.f;
   if (full) {
     Hd = load_mrow(c, H);
     tb = 0u;
-    jdj_mfma();
+    jdj_mfma<false>();
+    if (XG && r.x.any) {
+      /* the second bank's D (rowDA is free once the first bank's J'DJ has read it) */
+      tsync();
+      L->rowDA[c.l] = (r.x.ex && r.x.act) ? r.x.D : 0.f;
+      tsync();
+      jdj_mfma<true>();
+    }
     tsync();
     if (c.l < NV) {
       /* the G row of each foot whose chain holds the dof, else the zero row 31 of L
@@ -1765,6 +1928,18 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
          so they need no mask */
       for (int e = 0; e < CAP; e++) H[e] += g0[e] + g1[e];
       Hd += d0 + d1;
+      if (XG && r.x.any) {
+        const float* GX = &L->Hs[0][0] + ddep * CAP;
+        const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
+        const float* G2 = f2 ? GX : &L->L[31][0];
+        const float* G3 = f3 ? GX + CAP * CAP : &L->L[31][0];
+        ld_row(G2, g0);
+        ld_row(G3, g1);
+        const float d2 = G2[f2 ? ddep : 0], d3 = G3[f3 ? ddep : 0];
+#pragma unroll
+        for (int e = 0; e < CAP; e++) H[e] += g0[e] + g1[e];
+        Hd += d2 + d3;
+      }
     }
   } else {
     ld_row(&L->Hs[c.l][0], H);
@@ -1772,30 +1947,14 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     const float dl = r.ex ? ((r.act ? r.D : 0.f) - (pa ? r.D : 0.f)) : 0.f;
     L->rowF[c.l] = dl; /* rowF is free until the next update_constraint */
     tb = team_ballot(dl != 0.f) & c.rowmask;
+    if (XG && r.x.any) {
+      dl2 = r.x.ex ? ((r.x.act ? r.x.D : 0.f) - (pa2 ? r.x.D : 0.f)) : 0.f;
+      tb2 = team_ballot(dl2 != 0.f) & c.rowmask2;
+    }
     tsync();
   }
-  const float* da = full ? L->rowDA : L->rowF;
   if (c.l < NV) {
-    while (tb) {
-      const int k0 = __ffs(tb) - 1;
-      tb &= tb - 1u;
-      const bool h1 = tb != 0u;
-      const int k1 = h1 ? __ffs(tb) - 1 : k0;
-      tb &= tb - 1u;
-      float j0[CAP], j1[CAP];
-      ld_row(&L->u.J[k0][0], j0);
-      ld_row(&L->u.J[k1][0], j1);
-      const float jd0 = L->u.J[k0][ddep], jd1 = L->u.J[k1][ddep];
-      const float jj0 = da[k0] * jd0;
-      const float jj1 = (da[k1] * jd1) * (h1 ? 1.f : 0.f); /* a weight, not a select (loads) */
-      Hd += jj0 * jd0;
-      Hd += jj1 * jd1;
-#pragma unroll
-      for (int e = 0; e < CAP; e++) {
-        H[e] += jj0 * j0[e]; /* entries at or past the depth are never read */
-        H[e] += jj1 * j1[e];
-      }
-    }
+    add_rows(tb, L->u.J, full ? L->rowDA : L->rowF, ddep, H, Hd);
     float dd = 0.f;
     if (full) {
       if (r.hf && r.actf) dd += r.Df;
@@ -1806,6 +1965,14 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     }
     Hd += dd;
   }
+  if (XG && tb2 != 0u) {
+    /* the second bank's changed rows, their D through rowF after the first bank's (team-uniform) */
+    tsync();
+    L->rowF[c.l] = dl2;
+    tsync();
+    if (c.l < NV) add_rows(tb2, envx()->J, L->rowF, ddep, H, Hd);
+  }
+  if (XG && full && r.x.any) tsync(); /* the second bank's G rows in Hs[] are read before H is stored there */
   st_row(&L->Hs[c.l][0], H);
   L->Hsd[c.l] = Hd;
   tsync();
@@ -1815,12 +1982,14 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
+template <bool XG>
 __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float grad,
                                              float& Mv) {
   CP cfg = c.cfg;
   EnvL* L = c.L;
   Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
   r.Jv = row_dot(c, r, V_TMP); /* J rows are zero where no contact: no branch around the loads */
+  if constexpr (XG) r.x.Jv = r.x.any ? row_dot_x(c, r, V_TMP) : 0.f;
   tsync();
   /* the quadratic's coefficients and the slope/curvature at alpha = 0 in one reduction:
      d1(0) = search . grad (the gradient update_constraint left for the current active
@@ -1830,6 +1999,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   float g20 = (r.ex && r.act) ? r.D * r.Jv * r.Jv : 0.f;
   g20 += (r.hf && r.actf) ? r.Df * jv0 * jv0 : 0.f;
   g20 += (r.hl && r.actl) ? r.Dl * jv0 * jv0 : 0.f;
+  if constexpr (XG) g20 += (r.x.ex && r.x.act) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
   float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
   tsum_n<4>(cc);
   const float c1 = cc[0], c2 = cc[1];
@@ -1840,6 +2010,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
   const float Rf = r.Rf * r.fl, DfJ = r.hf ? r.Df * jv0 : 0.f, DfJ2 = DfJ * jv0;
   const float sv = r.sl * jv0, jl0 = r.jl;
   const float DlJ = r.hl ? r.Dl * sv : 0.f, DlJ2 = DlJ * sv;
+  const float DXJ = (XG && r.x.ex) ? r.x.D * r.x.Jv : 0.f, DXJ2 = DXJ * r.x.Jv;
   auto eval = [&](float alpha, float& d1, float& d2) {
     /* branch-free; rows that do not exist or are inactive add exact zeros */
     float g1, g2;
@@ -1861,6 +2032,12 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
       const float x = jl0 + alpha * sv;
       g1 += DlJ * fminf(x, 0.f);
       g2 += x < 0.f ? DlJ2 : 0.f;
+    }
+    if (XG && r.x.any) {
+      /* second-bank contact row */
+      const float x = r.x.jar + alpha * r.x.Jv;
+      g1 += DXJ * fminf(x, 0.f);
+      g2 += x < 0.f ? DXJ2 : 0.f;
     }
     float gg[2] = {g1, g2};
     tsum_n<2>(gg);
@@ -1884,6 +2061,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search
 }
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
+template <bool XG>
 __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters,
                                               bool live) {
   CP cfg = c.cfg;
@@ -1896,26 +2074,33 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   /* rows that do not exist have zero J and zero aref: no mask */
   float jw = row_dot(c, r, V_TMP) - r.aref;
   float js = row_dot(c, r, V_TMP2) - r.aref;
+  float jwx = 0.f, jsx = 0.f;
+  if (XG && r.x.any) {
+    jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
+    jsx = row_dot_x(c, r, V_TMP2) - r.x.aref;
+  }
   tsync();
-  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, r.sl * x - r.al),
-                  rows_cost(c, r, js, qs - r.af, r.sl * qs - r.al)};
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
+                  rows_cost<XG>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
   tsum_n<2>(cws);
   const float cw = cws[0], cs = cws[1];
   if (cw > cs) {
     x = qs;
     Ma = mul_m(c, x, V_TMP);
     r.jar = js;
+    r.x.jar = jsx;
   } else {
     r.jar = jw;
+    r.x.jar = jwx;
   }
   STAMP(S_WARM);
   r.jf = x - r.af;
   r.jl = r.sl * x - r.al;
   float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
-  float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
+  float cost = update_constraint<XG>(c, r, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
-  float Dinv = hessian_factor(c, r, true, 0, 0, 0);
+  float Dinv = hessian_factor<XG>(c, r, true, 0, 0, 0, 0);
   STAMP(S_HESS0);
   float search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
@@ -1923,22 +2108,23 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   while (live && it < cfg->iterations) {
     float Mv;
     STAMP(S_CHECK);
-    float alpha = line_search(c, r, search, Ma, fs, grad, Mv);
+    float alpha = line_search<XG>(c, r, search, Ma, fs, grad, Mv);
     STAMP(S_LS);
     if (alpha == 0.f) break;
     x += alpha * search;
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
+    if constexpr (XG) r.x.jar += alpha * r.x.Jv;
     r.jf += alpha * search;
     r.jl += alpha * (r.sl * search);
     float oldcost = cost;
-    const int pa = r.act, pf = r.actf, plo = r.actl;
+    const int pa = r.act, pf = r.actf, plo = r.actl, pa2 = XG ? r.x.act : 0;
     /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
        value, so the bits of separate tsum calls): cost, |grad|^2 and the active-set change */
     float red[3];
-    red[0] = update_constraint_lane(c, r, x, qs, fs, Ma, grad);
+    red[0] = update_constraint_lane<XG>(c, r, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
-    red[2] = (r.act != pa || r.actf != pf || r.actl != plo) ? 1.f : 0.f;
+    red[2] = (r.act != pa || r.actf != pf || r.actl != plo || (XG && r.x.act != pa2)) ? 1.f : 0.f;
     tsum_n<3>(red);
     cost = red[0];
     STAMP(S_UPD);
@@ -1952,7 +2138,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = red[2] > 0.f;
-    if (changed) Dinv = hessian_factor(c, r, false, pa, pf, plo);
+    if (changed) Dinv = hessian_factor<XG>(c, r, false, pa, pf, plo, pa2);
     STAMP(S_HESS);
     const float mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
@@ -1968,6 +2154,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
    the smooth factor of M that forward() left in L[] / Dk / Di (DinvM: this lane's 1/D), with
    Polak-Ribiere beta = max(0, g . (Mg - Mg_prev) / max(MINVAL, g_prev . Mg_prev)). No Hessian is
    built or factored. Returns qacc (dof lane). */
+template <bool XG>
 __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters, bool live,
                                           float DinvM) {
   CP cfg = c.cfg;
@@ -1978,37 +2165,45 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   float Ma = mul_m(c, x, V_TMP);
   float jw = row_dot(c, r, V_TMP) - r.aref;
   float js = row_dot(c, r, V_TMP2) - r.aref;
+  float jwx = 0.f, jsx = 0.f;
+  if (XG && r.x.any) {
+    jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
+    jsx = row_dot_x(c, r, V_TMP2) - r.x.aref;
+  }
   tsync();
-  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost(c, r, jw, x - r.af, r.sl * x - r.al),
-                  rows_cost(c, r, js, qs - r.af, r.sl * qs - r.al)};
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
+                  rows_cost<XG>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
   tsum_n<2>(cws);
   if (cws[0] > cws[1]) {
     x = qs;
     Ma = mul_m(c, x, V_TMP);
     r.jar = js;
+    r.x.jar = jsx;
   } else {
     r.jar = jw;
+    r.x.jar = jwx;
   }
   r.jf = x - r.af;
   r.jl = r.sl * x - r.al;
   const float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
-  float cost = update_constraint(c, r, x, qs, fs, Ma, grad);
+  float cost = update_constraint<XG>(c, r, x, qs, fs, Ma, grad);
   float mg = solve_ldl(c, grad, DinvM);
   float search = -mg;
   int it = 0;
   while (live && it < cfg->iterations) {
     float Mv;
-    const float alpha = line_search(c, r, search, Ma, fs, grad, Mv);
+    const float alpha = line_search<XG>(c, r, search, Ma, fs, grad, Mv);
     if (alpha == 0.f) break;
     x += alpha * search;
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
+    if constexpr (XG) r.x.jar += alpha * r.x.Jv;
     r.jf += alpha * search;
     r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
     float red[2];
-    red[0] = update_constraint_lane(c, r, x, qs, fs, Ma, grad);
+    red[0] = update_constraint_lane<XG>(c, r, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
     tsum_n<2>(red);
     cost = red[0];
@@ -2062,7 +2257,7 @@ __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
 
 /* ------------------------------- full forward ------------------------------ */
 /* mj_forward (+ sensors if requested). Leaves qacc in ls.qacc, kinematics in B. */
-template <int SOLVER>
+template <int SOLVER, bool XG>
 __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
                                         Sensors& sen, int& iters) {
   MP m = c.m;
@@ -2102,9 +2297,9 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   float qs = solve_ldl(c, fs, DinvM);
   STAMP(S_SOLVES);
   /* constraints */
-  make_constraints(c, s, ls, B, cm, r);
+  make_constraints<XG>(c, s, ls, B, cm, r);
   STAMP(S_CON);
-  int nrows = tmaxi(r.nrow + (r.hf || r.hl ? 1 : 0));
+  int nrows = tmaxi(r.nrow + (XG ? r.x.nrow : 0) + (r.hf || r.hl ? 1 : 0));
   float qacc;
   /* entered by the whole wave when either env has rows (the full Hessian
      build runs on the matrix cores and needs every lane); an env without
@@ -2112,8 +2307,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   qacc = qs;
   if (__ballot(nrows > 0) != 0ull) {
     int it2 = 0;
-    const float qn = SOLVER == ZB_SOLVER_CG ? solve_cg(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM)
-                                            : solve_newton(c, r, qs, fs, ls.w, it2, nrows > 0);
+    const float qn = SOLVER == ZB_SOLVER_CG ? solve_cg<XG>(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM)
+                                            : solve_newton<XG>(c, r, qs, fs, ls.w, it2, nrows > 0);
     if (nrows > 0) {
       qacc = qn;
       iters += it2;
@@ -2127,24 +2322,32 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   /* contact forces per geom -> cfrc_ext on the geom body, touch */
   float fext[6] = {0, 0, 0, 0, 0, 0};
   float cpos[3], cdir[3], cmu;
-  (void)contact_point(c, s, B, cpos, cdir, cmu);
+  (void)contact_point<XG>(c, s, B, 0, cpos, cdir, cmu);
+  float xpos[3], xdir[3];
+  if (XG && r.x.any) (void)contact_point<XG>(c, s, B, 1, xpos, xdir, cmu);
   const int rgeom = c.l >> 4;
   float tch0 = 0.f, tch1 = 0.f;
-  for (int g = 0; g < NGEOM; g++) {
-    bool mine = r.ex && rgeom == g;
+  for (int g = 0; g < (XG ? 2 * NGEOM : NGEOM); g++) {
+    /* geom g: bank g / 2, lanes 16 (g % 2) .. + 15 */
+    const bool b1 = XG && g >= NGEOM;
+    if (b1 && !r.x.any) continue; /* wave-uniform */
+    const bool mine = (b1 ? r.x.ex : r.ex) && rgeom == (g & 1);
+    const float rf = b1 ? r.x.f : r.f;
+    const float* pp = b1 ? xpos : cpos;
+    const float* dd = b1 ? xdir : cdir;
     float F[3] = {0, 0, 0}, tq[3] = {0, 0, 0};
     float fn = 0.f;
     if (mine) {
-      F[0] = r.f * cdir[0]; F[1] = r.f * cdir[1]; F[2] = r.f * cdir[2];
-      float off[3] = {cpos[0] - cm[0], cpos[1] - cm[1], cpos[2] - cm[2]};
+      F[0] = rf * dd[0]; F[1] = rf * dd[1]; F[2] = rf * dd[2];
+      float off[3] = {pp[0] - cm[0], pp[1] - cm[1], pp[2] - cm[2]};
       cross3(tq, off, F);
-      fn = r.f;
+      fn = rf;
     }
     float ex7[7] = {tq[0], tq[1], tq[2], F[0], F[1], F[2], fn};
     tsum_n<7>(ex7);
     float ext[6] = {ex7[0], ex7[1], ex7[2], ex7[3], ex7[4], ex7[5]};
     float fnt = ex7[6];
-    if (c.l == m->geom_body[g]) {
+    if (g < m->ngeom && c.l == m->geom_body[g]) {
 #pragma unroll
       for (int k = 0; k < 6; k++) fext[k] += ext[k];
     }
@@ -2686,6 +2889,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.qadr = t[TP_QADR * TEAM];
   c.act = t[TP_ACT * TEAM];
   c.rowmask = (uint32_t)t[TP_ROWMASK * TEAM];
+  c.rowmask2 = (uint32_t)t[TP_ROWMASK2 * TEAM];
   c.dk0 = t[TP_DK0 * TEAM];
   c.dfree = t[TP_DFREE * TEAM];
   c.chd = t[TP_CHD * TEAM];
@@ -2710,7 +2914,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 #ifndef ZB_WAVES_PER_EU
 #define ZB_WAVES_PER_EU 2
 #endif
-template <int SOLVER>
+template <int SOLVER, bool XG>
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   /* Chunked step (a.nchunk > 1, one control step): the launch has npair * nchunk workgroups, each
@@ -2813,7 +3017,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       if (!resetting && !ghost) feetech(c, ls);
       STAMP(S_FEETECH);
       int it_pass = 0;
-      forward<SOLVER>(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, it_pass);
+      forward<SOLVER, XG>(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, it_pass);
       if (!ghost) iters += it_pass;
       if (!resetting && !ghost) {
         integrate(c, s, ls);
@@ -2923,7 +3127,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
 #endif
 }
 
-template <int SOLVER>
+template <int SOLVER, bool XG>
 __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
@@ -2948,7 +3152,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   int it = 0;
   if (live) reset_prepare(c, s, ls, rnd);
   else load_params(c, s, ls, nullptr);
-  forward<SOLVER>(c, s, ls, B, r, live, sen, it);
+  forward<SOLVER, XG>(c, s, ls, B, r, live, sen, it);
   if (!live) return;
   observe(c, s, ls, B, sen, a.obs_actor ? a.obs_actor + (size_t)e * ZB_OBS_ACTOR : nullptr,
           a.obs_critic ? a.obs_critic + (size_t)e * ZB_OBS_CRITIC : nullptr,
@@ -2957,7 +3161,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
 }
 
 /* single forward on the stored (qpos, qvel), ctrl = action row; dumps internals */
-template <int SOLVER>
+template <int SOLVER, bool XG>
 __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
@@ -2977,7 +3181,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   Rows r;
   Sensors& sen = c.L->sen;
   int it = 0;
-  forward<SOLVER>(c, s, ls, B, r, true, sen, it);
+  forward<SOLVER, XG>(c, s, ls, B, r, true, sen, it);
   if (!live) return;
   float* d = a.dbg + (size_t)e * ZB_DBG_STRIDE;
   const int l = c.l;
@@ -3002,10 +3206,10 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = c.L->ci[l][k];
     for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
   }
-  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (r.hf ? 1 : 0) + (r.hl ? 1 : 0)));
+  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (XG && r.x.ex ? 1 : 0) + (r.hf ? 1 : 0) + (r.hl ? 1 : 0)));
   if (l == 0) {
     d[ZB_DBG_MISC + 0] = (float)nefc;
-    d[ZB_DBG_MISC + 1] = (float)(r.nrow / 4);
+    d[ZB_DBG_MISC + 1] = (float)((r.nrow + (XG ? r.x.nrow : 0)) / 4);
     d[ZB_DBG_MISC + 2] = sen.touch[0];
     d[ZB_DBG_MISC + 3] = sen.touch[1];
     for (int k = 0; k < 4; k++) d[ZB_DBG_MISC + 4 + k] = sen.fq[k];
@@ -3035,12 +3239,26 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   }
 }
 
-int step_resident_blocks(int device) {
+int step_resident_blocks(int device, int xg) {
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON>, 64, 0) != hipSuccess) return 0;
+  const hipError_t e = xg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, true>, 64, 0)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, false>, 64, 0);
+  if (e != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
   return per_cu * cus;
 }
+
+/* the instantiation for the handle's solver and collider set */
+#define ZB_LAUNCH_VARIANT(K, grid, block, s, args)                                                        \
+  do {                                                                                                    \
+    if ((args).solver == ZB_SOLVER_CG) {                                                                  \
+      if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_CG, true>), grid, block, 0, s, args);                \
+      else hipLaunchKernelGGL((K<ZB_SOLVER_CG, false>), grid, block, 0, s, args);                         \
+    } else {                                                                                              \
+      if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, true>), grid, block, 0, s, args);            \
+      else hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, false>), grid, block, 0, s, args);                     \
+    }                                                                                                     \
+  } while (0)
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
@@ -3052,8 +3270,7 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   const StepArgs& b = a;
 #endif
   dim3 grid((unsigned)((b.n_envs + NTEAM - 1) / NTEAM * b.nchunk)), block(64);
-  if (b.solver == ZB_SOLVER_CG) hipLaunchKernelGGL(step_kernel<ZB_SOLVER_CG>, grid, block, 0, s, b);
-  else hipLaunchKernelGGL(step_kernel<ZB_SOLVER_NEWTON>, grid, block, 0, s, b);
+  ZB_LAUNCH_VARIANT(step_kernel, grid, block, s, b);
   return hipGetLastError();
 }
 /* ksim's FeetAirtimeReward over one trajectory (train.py:503-546), row 0. The fused step
@@ -3092,15 +3309,13 @@ hipError_t launch_airtime_exact(const StepArgs& a, hipStream_t s) {
 hipError_t launch_reset(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  if (a.solver == ZB_SOLVER_CG) hipLaunchKernelGGL(reset_kernel<ZB_SOLVER_CG>, grid, block, 0, s, a);
-  else hipLaunchKernelGGL(reset_kernel<ZB_SOLVER_NEWTON>, grid, block, 0, s, a);
+  ZB_LAUNCH_VARIANT(reset_kernel, grid, block, s, a);
   return hipGetLastError();
 }
 hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  if (a.solver == ZB_SOLVER_CG) hipLaunchKernelGGL(debug_forward_kernel<ZB_SOLVER_CG>, grid, block, 0, s, a);
-  else hipLaunchKernelGGL(debug_forward_kernel<ZB_SOLVER_NEWTON>, grid, block, 0, s, a);
+  ZB_LAUNCH_VARIANT(debug_forward_kernel, grid, block, s, a);
   return hipGetLastError();
 }
 

@@ -64,7 +64,8 @@ static int check_indices(const ZbModel* m) {
   for (int a = 0; a < m->nu; a++)
     if (!in(m->act_dof[a], 0, NV)) return fail(ZB_EMODEL, "actuator %d: dof %d out of range", a, m->act_dof[a]);
   for (int g = 0; g < m->ngeom; g++)
-    if (!in(m->geom_body[g], 1, NB) || !in(m->geom_lastdof[g], -1, NV))
+    if (!in(m->geom_body[g], 1, NB) || !in(m->geom_lastdof[g], -1, NV) ||
+        m->geom_lastdof[g] != m->body_lastdof[m->geom_body[g]])
       return fail(ZB_EMODEL, "geom %d: body / dof out of range", g);
   for (int s = 0; s < m->nsite; s++)
     if (!in(m->site_body[s], 0, NB)) return fail(ZB_EMODEL, "site %d: body %d out of range", s, m->site_body[s]);
@@ -96,8 +97,16 @@ int check_model(const ZbModel* m) {
                            "them knowingly", m->nskip_geom);
   if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
-  if (m->ngeom * ZB_CON_PER_GEOM * 4 > 32)
-    return fail(ZB_EMODEL, "ngeom=%d: contact rows exceed the 32-lane team", m->ngeom);
+  /* colliders: two banks of 32 contact-row lanes, 16 rows (4 contacts x 4 pyramid edges) per geom */
+  if (m->ngeom < 1 || m->ngeom * ZB_CON_PER_GEOM * 4 > 2 * 32)
+    return fail(ZB_EMODEL, "ngeom=%d: 1 to %d floor colliders", m->ngeom, ZB_MAX_GEOM);
+  for (int g = 0; g < m->ngeom; g++) {
+    const int ty = m->geom_type[g];
+    const int nsz = ty == ZB_GEOM_BOX ? 3 : ty == ZB_GEOM_CAPSULE ? 2 : ty == ZB_GEOM_SPHERE ? 1 : 0;
+    if (nsz == 0) return fail(ZB_EMODEL, "geom %d: type %d (box 6, capsule 3, sphere 2)", g, ty);
+    for (int k = 0; k < nsz; k++)
+      if (!(m->geom_size[g][k] > 0.f)) return fail(ZB_EMODEL, "geom %d: size[%d] must be positive", g, k);
+  }
   if (m->max_depth > ZB_MAX_DEPTH) return fail(ZB_EMODEL, "dof depth %d > %d", m->max_depth, ZB_MAX_DEPTH);
   if (m->nu != ZB_NJ || m->nbody != ZB_NBODY_TASK)
     return fail(ZB_EMODEL, "task layout needs nu=%d nbody=%d (got %d, %d)", ZB_NJ, ZB_NBODY_TASK, m->nu, m->nbody);
@@ -124,10 +133,11 @@ int check_model(const ZbModel* m) {
   }
   if (nroot != 6) return fail(ZB_EMODEL, "dof tree: the free joint's 6 dofs must form the root chain (got %d)", nroot);
   if (m->nv != 6 + ZB_NJ) return fail(ZB_EMODEL, "task layout needs nv=%d (got %d)", 6 + ZB_NJ, m->nv);
-  /* depths / counts the engine is compiled for (zb_engine.hip NGEOM, MAXBD, MAXDD, NLIMBLV) */
-  if (m->ngeom != 2 || maxbd != 8 || m->max_depth != 12 || m->nlevel != 12)
-    return fail(ZB_EMODEL, "engine compiled for ngeom 2, body depth 8, dof depth 12, 12 levels (got %d, %d, %d, %d)",
-                m->ngeom, maxbd, m->max_depth, m->nlevel);
+  /* the depths the engine is compiled for (zb_engine.hip MAXBD, MAXDD / NLIMBLV): the pointer-jumping
+     passes cover bodies up to depth 8 and limb chains up to 6 dofs below the 6 root dofs */
+  if (maxbd > TOPO_MAXBD || m->max_depth > 12 || m->nlevel > 12)
+    return fail(ZB_EMODEL, "body depth %d (max %d), dof depth %d (max 12), %d levels (max 12)", maxbd, TOPO_MAXBD,
+                m->max_depth, m->nlevel);
   for (int k = nroot; k < m->nv; k++) {
     const int p = m->dof_parent[k];
     int nchild_prev = 0;
@@ -138,6 +148,10 @@ int check_model(const ZbModel* m) {
       return fail(ZB_EMODEL, "dof %d: limbs must be unbranched chains of consecutive dofs off dof %d", k, nroot - 1);
   }
   return ZB_OK;
+}
+
+bool needs_xg(const ZbModel* m) {
+  return !(m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX);
 }
 
 int check_cfg(const ZbEnvConfig* c) {
@@ -200,12 +214,14 @@ void build_topology(const ZbModel* m, int32_t t[zb::TP_NF][zb::TOPO_LANES]) {
     uint32_t desc = 0;
     for (int k = 0; k < NV; k++)
       if (isd && k != l && m->dof_depth[k] > ddep && m->dof_anc[k][ddep] == l) desc |= 1u << k;
-    uint32_t rm = 0;
-    for (int g = 0; g < TOPO_NGEOM; g++) {
+    /* contact rows of geom g: bank g / 2, lanes 16 (g % 2) .. + 15 */
+    uint32_t rm[2] = {0u, 0u};
+    for (int g = 0; g < m->ngeom && g < 2 * TOPO_NGEOM; g++) {
       const int kd = m->body_lastdof[m->geom_body[g]];
-      if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm |= 0xFFFFu << (16 * g);
+      if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm[g / 2] |= 0xFFFFu << (16 * (g % 2));
     }
-    t[TP_ROWMASK][l] = (int32_t)rm;
+    t[TP_ROWMASK][l] = (int32_t)rm[0];
+    t[TP_ROWMASK2][l] = (int32_t)rm[1];
     t[TP_DK0][l] = isd ? l - m->body_dofadr[dbody] : 0;
     t[TP_DFREE][l] = (isd && m->body_jnttype[dbody] == ZB_JNT_FREE) ? 1 : 0;
     int hd = -1, ln = 0;

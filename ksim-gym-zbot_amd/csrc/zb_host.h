@@ -18,11 +18,11 @@ namespace zb {
    [TP_NF][32] int32 */
 enum {
   TP_BPAR, TP_BDEP, TP_BJT, TP_BDOFADR, TP_BLAST, TP_NCH, TP_CH0, TP_CH1, TP_LVL_LO, TP_LVL_HI,
-  TP_DDEP, TP_DBODY, TP_QADR, TP_ACT, TP_ROWMASK, TP_DK0, TP_DFREE, TP_CHD, TP_CPS, TP_CLN, TP_NF
+  TP_DDEP, TP_DBODY, TP_QADR, TP_ACT, TP_ROWMASK, TP_ROWMASK2, TP_DK0, TP_DFREE, TP_CHD, TP_CPS, TP_CLN, TP_NF
 };
 constexpr int TOPO_LANES = 32;
 constexpr int TOPO_NROOT = 6;  /* root dof chain (the free joint), zb_engine.hip NROOT */
-constexpr int TOPO_NGEOM = 2;  /* foot geoms, zb_engine.hip NGEOM */
+constexpr int TOPO_NGEOM = 2;  /* geoms per contact-row bank, zb_engine.hip NGEOM */
 constexpr int TOPO_MAXBD = 8;  /* deepest body, zb_engine.hip MAXBD */
 
 /* fail(): record the message for zb_last_error() and return `code` */
@@ -30,6 +30,8 @@ int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 /* ZB_OK, or ZB_EARG / ZB_EMODEL with the reason in zb_last_error() */
 int check_model(const ZbModel* m);
 int check_cfg(const ZbEnvConfig* c);
+/* the model needs the general-collider kernels (anything but exactly two box soles) */
+bool needs_xg(const ZbModel* m);
 /* requires check_model(m) == ZB_OK */
 void build_topology(const ZbModel* m, int32_t t[TP_NF][TOPO_LANES]);
 

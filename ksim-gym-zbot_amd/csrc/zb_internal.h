@@ -57,10 +57,11 @@ struct StepArgs {
   int32_t* itpart;          /* [n] Newton iterations of the chunks so far */
   int air_mark;             /* first step of a rollout: save its contacts + causal airtime term */
   int solver;               /* ZB_SOLVER_NEWTON / ZB_SOLVER_CG: which kernel instantiation runs */
+  int xg;                   /* general colliders (zb_host.h needs_xg): the two-bank instantiation */
 };
 
 /* workgroups of step_kernel resident on the device at once (occupancy x CUs) */
-int step_resident_blocks(int device);
+int step_resident_blocks(int device, int xg);
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s);
 hipError_t launch_reset(const StepArgs& a, hipStream_t s);

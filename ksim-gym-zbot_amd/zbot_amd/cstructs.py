@@ -16,11 +16,12 @@ MAX_ACT = 32
 CON_PER_GEOM = 4
 
 MODEL_MAGIC = 0x5A424F54
-MODEL_VERSION = 5
+MODEL_VERSION = 6
 
 JNT_NONE = -1
 JNT_FREE = 0
 JNT_HINGE = 3
+GEOM_SPHERE, GEOM_CAPSULE, GEOM_BOX = 2, 3, 6
 
 # zbot_layout.h
 NJ = 20
@@ -175,6 +176,7 @@ class ZbModel(C.Structure):
         ("fe_max_torque", _f(MAX_ACT)),
         ("fe_max_velocity", _f(MAX_ACT)),
         ("geom_body", _i(MAX_GEOM)),
+        ("geom_type", _i(MAX_GEOM)),
         ("geom_pos", _f(MAX_GEOM, 4)),
         ("geom_quat", _f(MAX_GEOM, 4)),
         ("geom_size", _f(MAX_GEOM, 4)),

@@ -23,8 +23,10 @@ MJCF semantics (XML reference, MuJoCo 3.3.4 [U]):
     inertiafromgeom="true"), the mass and inertia of the body's box / sphere /
     capsule / cylinder / ellipsoid geoms (density or mass, fromto,
     inertiagrouprange), composed about their common centre of mass;
-  * box <geom>s with a nonzero contype/conaffinity as the foot-sole colliders
-    (other colliding geoms are listed in desc["skipped_geoms"]), the
+  * box / capsule (size or fromto) / sphere <geom>s with a nonzero contype or
+    conaffinity as floor colliders, up to 4 in document order (the engine's
+    plane-box / plane-capsule / plane-sphere contacts; other colliding geoms
+    are listed in desc["skipped_geoms"] and make zb_create refuse the model), the
     <geom type="plane"> of the worldbody as the floor (friction, solref,
     solimp, margin);
   * <motor> / plain <general> actuators (gear, ctrlrange, ctrllimited), one per
@@ -46,6 +48,10 @@ import xml.etree.ElementTree as ET
 import numpy as np
 
 from .model import load_description
+
+# floor colliders the engine has contacts for (type -> sizes) and how many (ZB_MAX_GEOM)
+COLLIDER_TYPES = {"box": 3, "capsule": 2, "sphere": 1}
+MAX_COLLIDERS = 4
 
 
 def _floats(s: str | None, n: int | None = None) -> list[float] | None:
@@ -109,6 +115,23 @@ def _principal(inertia: np.ndarray) -> tuple[list[float], list[float]]:
     return [float(x) for x in w], _mat_quat(V)
 
 
+def _fromto_frame(ft: list[float]) -> tuple[np.ndarray, np.ndarray, float]:
+    """Centre, rotation (local z along the segment) and half-length of a geom given by fromto,
+    as MuJoCo's compiler sets them (mjuu_frame from the z axis: the shortest rotation of +z)."""
+    ft = np.asarray(ft, dtype=np.float64)
+    d = ft[3:] - ft[:3]
+    L = float(np.linalg.norm(d))
+    pos = (ft[:3] + ft[3:]) / 2
+    z = d / L
+    axis = np.cross([0.0, 0.0, 1.0], z)
+    sn, cs_ = float(np.linalg.norm(axis)), float(z[2])
+    if sn > 1e-12:
+        R = np.array(_quat_mat(_axis_quat(axis, math.atan2(sn, cs_))))
+    else:
+        R = np.eye(3) if cs_ > 0 else np.diag([1.0, -1.0, -1.0])
+    return pos, R, L / 2
+
+
 def _geom_mass_inertia(ga: dict, quat: list[float]):
     """(mass, centre, rotation, principal moments) of one solid geom, as MuJoCo's compiler
     takes it for inertiafromgeom: uniform density (default 1000) or the geom's explicit mass."""
@@ -119,18 +142,8 @@ def _geom_mass_inertia(ga: dict, quat: list[float]):
     if "fromto" in ga:
         if gt not in ("capsule", "cylinder", "box", "ellipsoid"):
             raise ValueError(f"geom {ga.get('name')}: fromto on a {gt}")
-        ft = np.array(_floats(ga["fromto"], 6))
-        d = ft[3:] - ft[:3]
-        L = float(np.linalg.norm(d))
-        pos = (ft[:3] + ft[3:]) / 2
-        z = d / L
-        axis = np.cross([0.0, 0.0, 1.0], z)
-        sn, cs_ = float(np.linalg.norm(axis)), float(z[2])
-        if sn > 1e-12:
-            R = np.array(_quat_mat(_axis_quat(axis, math.atan2(sn, cs_))))
-        else:
-            R = np.eye(3) if cs_ > 0 else np.diag([1.0, -1.0, -1.0])
-        size = [size[0], L / 2] if gt in ("capsule", "cylinder") else [size[0], size[1], L / 2]
+        pos, R, hl = _fromto_frame(_floats(ga["fromto"], 6))
+        size = [size[0], hl] if gt in ("capsule", "cylinder") else [size[0], size[1], hl]
     if gt == "sphere":
         r = size[0]
         vol = 4.0 / 3.0 * math.pi * r ** 3
@@ -355,17 +368,26 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                 ga = defaults.attrs(c, cls)
                 if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
                     continue  # visual only
-                if ga.get("type", "sphere") != "box":
-                    # the engine collides box soles with the floor (plane-box); other colliding
-                    # geoms are listed so a caller can see what the model leaves out
-                    desc.setdefault("skipped_geoms", []).append(
-                        {"name": ga.get("name", ""), "body": name, "type": ga.get("type", "sphere")})
+                gt = ga.get("type", "sphere")
+                if gt not in COLLIDER_TYPES or len(desc["geoms"]) >= MAX_COLLIDERS:
+                    # the engine collides up to 4 boxes, capsules and spheres with the floor; other
+                    # colliding geoms are listed so a caller can see what the model leaves out
+                    desc.setdefault("skipped_geoms", []).append({"name": ga.get("name", ""), "body": name, "type": gt})
                     continue
-                gd = {"name": ga.get("name", f"{name}_geom{len(desc['geoms'])}"), "body": name, "type": "box",
-                      "size": _floats(ga["size"], 3)}
-                if "pos" in ga:
-                    gd["pos"] = _floats(ga["pos"], 3)
+                nsz = COLLIDER_TYPES[gt]
+                gd = {"name": ga.get("name", f"{name}_geom{len(desc['geoms'])}"), "body": name, "type": gt}
                 gq = orientation(c, ga)
+                if "fromto" in ga:
+                    if gt != "capsule":
+                        raise ValueError(f"geom {gd['name']}: fromto on a {gt} collider")
+                    fpos, fR, hl = _fromto_frame(_floats(ga["fromto"], 6))
+                    gd["size"] = [_floats(ga["size"])[0], hl]
+                    gd["pos"] = [float(v) for v in fpos]
+                    gq = _mat_quat(fR)
+                else:
+                    gd["size"] = _floats(ga["size"], nsz)[:nsz]
+                    if "pos" in ga:
+                        gd["pos"] = _floats(ga["pos"], 3)
                 if gq != [1.0, 0.0, 0.0, 0.0]:
                     gd["quat"] = gq
                 desc["geoms"].append(gd)
@@ -440,11 +462,11 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
     for sd in desc["sites"]:
         if touched is not None and sd["name"] not in touched:
             continue
-        box = next((g["name"] for g in desc["geoms"] if g["body"] == sd["body"]), None)
-        if box is not None:
-            sd["touch_geom"] = box
+        geom = next((g["name"] for g in desc["geoms"] if g["body"] == sd["body"]), None)
+        if geom is not None:
+            sd["touch_geom"] = geom
         elif touched is not None:
-            raise ValueError(f"touch sensor on site {sd['name']}: no collision box on body {sd['body']}")
+            raise ValueError(f"touch sensor on site {sd['name']}: no collider on body {sd['body']}")
     return desc
 
 
@@ -508,7 +530,7 @@ def to_mjcf(desc: dict) -> str:
         for g in geoms.get(b["name"], []):
             gp = f' pos="{_fmt(g["pos"])}"' if "pos" in g else ""
             gq = f' quat="{_fmt(g["quat"])}"' if "quat" in g else ""
-            lines.append(f'{ind}  <geom name="{g["name"]}" type="box" size="{_fmt(g["size"])}"{gp}{gq}/>')
+            lines.append(f'{ind}  <geom name="{g["name"]}" type="{g.get("type", "box")}" size="{_fmt(g["size"])}"{gp}{gq}/>')
         for s in sites.get(b["name"], []):
             sq = f' quat="{_fmt(s["quat"])}"' if "quat" in s else ""
             lines.append(f'{ind}  <site name="{s["name"]}" pos="{_fmt(s.get("pos", [0, 0, 0]))}"{sq}/>')

@@ -197,7 +197,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) 
     """Compile a JSON robot description into a ZbModel (+ host float64 view).
 
     A description from zbot_amd.mjcf.load_mjcf lists the source's colliding geoms the engine does
-    not collide with the floor (it collides the two box soles, plane-box) in
+    not collide with the floor (it collides up to 4 boxes, capsules and spheres) in
     desc["skipped_geoms"]. They are counted into ZbModel.nskip_geom, and zb_create rejects such a
     model (ZB_EMODEL) rather than simulating it without those contacts. drop_colliders=True
     compiles it without them, knowingly (nskip_geom 0)."""
@@ -335,11 +335,18 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) 
             size = np.array(g["size"])
             gpos = xpos[bi] + xmat[bi] @ np.array(g.get("pos", [0, 0, 0]))
             gmat = xmat[bi] @ quat_to_mat(np.array(g.get("quat", [1.0, 0, 0, 0])))
-            for sx in (-1, 1):
-                for sy in (-1, 1):
-                    for sz in (-1, 1):
-                        c = gpos + gmat @ (size * np.array([sx, sy, sz]))
-                        zmin = min(zmin, c[2])
+            gt = g.get("type", "box")
+            if gt == "box":
+                for sx in (-1, 1):
+                    for sy in (-1, 1):
+                        for sz in (-1, 1):
+                            c = gpos + gmat @ (size * np.array([sx, sy, sz]))
+                            zmin = min(zmin, c[2])
+            elif gt == "capsule":
+                for sg in (-1, 1):
+                    zmin = min(zmin, gpos[2] + sg * size[1] * gmat[2, 2] - size[0])
+            else:
+                zmin = min(zmin, gpos[2] - size[0])
         qpos0[2] = -zmin + float(desc.get("base_clearance", 0.0))
         root.pos[2] = qpos0[2]
 
@@ -459,14 +466,21 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) 
         m.joint_bias[a] = JOINT_BIASES[a][1]
         m.joint_weight[a] = JOINT_BIASES[a][2]
 
+    gtypes = {"box": (cs.GEOM_BOX, 3), "capsule": (cs.GEOM_CAPSULE, 2), "sphere": (cs.GEOM_SPHERE, 1)}
     for gi, gd in enumerate(geoms):
-        if gd.get("type", "box") != "box":
-            raise ValueError("only box collision geoms are supported")
+        gt = gd.get("type", "box")
+        if gt not in gtypes:
+            raise ValueError(f"geom {gd['name']}: type {gt!r} (box, capsule and sphere collide with the floor)")
+        code, nsize = gtypes[gt]
+        if len(gd["size"]) < nsize or any(not (v > 0) for v in gd["size"][:nsize]):
+            raise ValueError(f"geom {gd['name']}: a {gt} needs {nsize} positive sizes")
         m.geom_body[gi] = names[gd["body"]]
+        m.geom_type[gi] = code
         gp = gd.get("pos", [0, 0, 0])
         gq = gd.get("quat", [1.0, 0, 0, 0])
         for k in range(3):
             m.geom_pos[gi][k] = gp[k]
+        for k in range(nsize):
             m.geom_size[gi][k] = gd["size"][k]
         for k in range(4):
             m.geom_quat[gi][k] = gq[k]
@@ -557,7 +571,7 @@ def _fill_tables(m, bodies, nbody, nv, dof_depth, dof_anc, dof_parent, geom_body
                 v |= (a if a >= 0 else 0) << (8 * bb)
             m.dof_ancpk[d][w] = v
         rm = 0
-        for g, kd in enumerate(glast):
+        for g, kd in enumerate(glast[:2]):  # geoms 0-1 (the engine's first row bank)
             if kd >= 0 and (kd == d or (desc >> kd) & 1):
                 rm |= 0xFFFF << (16 * g)
         m.dof_rowmask[d] = rm

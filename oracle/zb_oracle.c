@@ -258,7 +258,7 @@ typedef struct {
   real site_xpos[ZB_MAX_SITE][3], site_xmat[ZB_MAX_SITE][9], site_xquat[ZB_MAX_SITE][4];
   /* contacts */
   int ncon;
-  real con_pos[ZB_MAX_CON][3], con_dist[ZB_MAX_CON], con_mu[ZB_MAX_CON];
+  real con_pos[ZB_MAX_CON][3], con_dist[ZB_MAX_CON], con_mu[ZB_MAX_CON], con_t1[ZB_MAX_CON][3];
   int con_geom[ZB_MAX_CON], con_efc[ZB_MAX_CON];
   /* constraints */
   int nefc;
@@ -550,26 +550,70 @@ static void smooth_forces(const ZbModel* m, ZbData* d) {
 }
 
 /* ------------------------------- collision -------------------------------- */
-/* floor plane (z = 0, normal +z) vs box: the 4 sole corners (-z face) */
+/* The floor plane (z = 0, normal +z, train.py:1326-1331 floor with geom_priority 2) against each
+ * collider, as MuJoCo's primitive colliders (engine_collision_primitive.c, MuJoCo 3.3):
+ *   box (mjc_PlaneBox): the 8 corners in index order (bit 0: +x, bit 1: +y, bit 2: +z half
+ *     size), a corner kept when its offset from the centre along the normal is <= 0 and its
+ *     distance is within the margin, at most 4;
+ *   capsule (mjc_PlaneCapsule): the end spheres, the +half-length end first; tangent frame along
+ *     the capsule axis projected on the plane (mjx plane_capsule: +y when that projection is
+ *     shorter than 0.5, i.e. the axis is within 30 degrees of the normal);
+ *   sphere (mjc_PlaneSphere): one contact.
+ * Contact point: the deepest point moved back along the normal by half the distance. Frames other
+ * than the capsule's are mju_makeFrame(+z): t1 = +y, t2 = n x t1 = -x. */
+static void add_contact(const ZbModel* m, ZbData* d, int g, const real p[3], real dist, const real t1[3]) {
+  if (d->ncon >= ZB_MAX_CON) return;
+  int n = d->ncon++;
+  d->con_pos[n][0] = p[0];
+  d->con_pos[n][1] = p[1];
+  d->con_pos[n][2] = p[2] - (real)0.5 * dist;
+  d->con_dist[n] = dist;
+  d->con_geom[n] = g;
+  d->con_mu[n] = m->floor_friction[0] * d->floor_mu;
+  for (int k = 0; k < 3; k++) d->con_t1[n][k] = t1[k];
+}
+
 static void collision(const ZbModel* m, ZbData* d) {
+  static const real ty[3] = {0, 1, 0};
   d->ncon = 0;
+  const real margin = m->floor_margin;
   for (int g = 0; g < m->ngeom; g++) {
-    for (int c = 0; c < ZB_CON_PER_GEOM; c++) {
-      real loc[3] = {(c & 1) ? m->geom_size[g][0] : -m->geom_size[g][0],
-                     (c & 2) ? m->geom_size[g][1] : -m->geom_size[g][1], -m->geom_size[g][2]};
-      real w[3];
-      mulmv3(w, d->geom_xmat[g], loc);
-      real p[3] = {d->geom_xpos[g][0] + w[0], d->geom_xpos[g][1] + w[1], d->geom_xpos[g][2] + w[2]};
-      real dist = p[2];
-      if (dist < m->floor_margin) {
-        int n = d->ncon++;
-        d->con_pos[n][0] = p[0];
-        d->con_pos[n][1] = p[1];
-        d->con_pos[n][2] = p[2] - (real)0.5 * dist;
-        d->con_dist[n] = dist;
-        d->con_geom[n] = g;
-        d->con_mu[n] = m->floor_friction[0] * d->floor_mu;
+    const real* R = d->geom_xmat[g];
+    const real* c = d->geom_xpos[g];
+    const float* sz = m->geom_size[g];
+    if (m->geom_type[g] == ZB_GEOM_BOX) {
+      int cnt = 0;
+      for (int i = 0; i < 8 && cnt < 4; i++) {
+        real loc[3] = {(i & 1) ? sz[0] : -sz[0], (i & 2) ? sz[1] : -sz[1], (i & 4) ? sz[2] : -sz[2]}, w[3];
+        mulmv3(w, R, loc);
+        const real dist = c[2] + w[2];
+        if (dist > margin || w[2] > 0) continue;
+        real p[3] = {c[0] + w[0], c[1] + w[1], c[2] + w[2]};
+        add_contact(m, d, g, p, dist, ty);
+        cnt++;
       }
+    } else if (m->geom_type[g] == ZB_GEOM_CAPSULE) {
+      /* axis = local z in the world; b = its projection on the plane, normalised */
+      real ax[3] = {R[2], R[5], R[8]};
+      real b[3] = {ax[0], ax[1], 0};
+      real bn = SQRT(b[0] * b[0] + b[1] * b[1]);
+      real t1[3];
+      if (bn < (real)0.5) {
+        t1[0] = 0; t1[1] = 1; t1[2] = 0;
+      } else {
+        t1[0] = b[0] / bn; t1[1] = b[1] / bn; t1[2] = 0;
+      }
+      for (int e = 0; e < 2; e++) {
+        const real sg = e == 0 ? 1 : -1;
+        real p[3] = {c[0] + sg * sz[1] * ax[0], c[1] + sg * sz[1] * ax[1], c[2] + sg * sz[1] * ax[2] - sz[0]};
+        const real dist = p[2];
+        if (dist > margin) continue;
+        add_contact(m, d, g, p, dist, t1);
+      }
+    } else if (m->geom_type[g] == ZB_GEOM_SPHERE) {
+      real p[3] = {c[0], c[1], c[2] - sz[0]};
+      const real dist = p[2];
+      if (dist <= margin) add_contact(m, d, g, p, dist, ty);
     }
   }
 }
@@ -658,9 +702,12 @@ static void make_constraint(const ZbModel* m, ZbData* d, real dt) {
     }
   }
   /* contacts: pyramidal cone, condim 3 -> 4 rows (+t1, -t1, +t2, -t2) */
-  static const real n[3] = {0, 0, 1}, t1[3] = {0, 1, 0}, t2[3] = {-1, 0, 0}; /* mju_makeFrame(+z) */
+  static const real n[3] = {0, 0, 1};
   for (int c = 0; c < d->ncon; c++) {
     int body = m->geom_body[d->con_geom[c]];
+    /* frame (n, t1, t2 = n x t1), collision() */
+    const real* t1 = d->con_t1[c];
+    const real t2[3] = {-t1[1], t1[0], 0};
     real Jn[NDOF], Jt1[NDOF], Jt2[NDOF];
     point_jac_row(m, d, body, d->con_pos[c], n, Jn);
     point_jac_row(m, d, body, d->con_pos[c], t1, Jt1);
@@ -952,8 +999,9 @@ static void sensors(const ZbModel* m, ZbData* d) {
     real f0 = d->efc_force[r], f1 = d->efc_force[r + 1], f2 = d->efc_force[r + 2], f3 = d->efc_force[r + 3];
     real fn = f0 + f1 + f2 + f3, mu = d->con_mu[k];
     real ft1 = mu * (f0 - f1), ft2 = mu * (f2 - f3);
-    /* world force = fn*n + ft1*t1 + ft2*t2, frame n=(0,0,1) t1=(0,1,0) t2=(-1,0,0) */
-    real F[3] = {-ft2, ft1, fn};
+    /* world force = fn*n + ft1*t1 + ft2*t2, n = (0,0,1), t2 = n x t1 = (-t1y, t1x, 0) */
+    const real* t1 = d->con_t1[k];
+    real F[3] = {ft1 * t1[0] - ft2 * t1[1], ft1 * t1[1] + ft2 * t1[0], fn};
     int g = d->con_geom[k];
     int body = m->geom_body[g];
     real off[3] = {d->con_pos[k][0] - c[0], d->con_pos[k][1] - c[1], d->con_pos[k][2] - c[2]}, tq[3];
@@ -1654,7 +1702,7 @@ static const FieldOff model_fields[] = {
     OFF(ZbModel, act_ctrlrange), OFF(ZbModel, fe_kp), OFF(ZbModel, fe_kd), OFF(ZbModel, fe_error_gain),
     OFF(ZbModel, fe_max_pwm), OFF(ZbModel, fe_vin), OFF(ZbModel, fe_kt), OFF(ZbModel, fe_R), OFF(ZbModel, fe_vmax),
     OFF(ZbModel, fe_amax), OFF(ZbModel, fe_max_torque), OFF(ZbModel, fe_max_velocity), OFF(ZbModel, geom_body),
-    OFF(ZbModel, geom_pos), OFF(ZbModel, geom_quat), OFF(ZbModel, geom_size), OFF(ZbModel, floor_friction),
+    OFF(ZbModel, geom_type), OFF(ZbModel, geom_pos), OFF(ZbModel, geom_quat), OFF(ZbModel, geom_size), OFF(ZbModel, floor_friction),
     OFF(ZbModel, floor_solref), OFF(ZbModel, floor_solimp), OFF(ZbModel, floor_margin), OFF(ZbModel, pad_floor),
     OFF(ZbModel, site_body), OFF(ZbModel, site_pos), OFF(ZbModel, site_quat), OFF(ZbModel, site_imu),
     OFF(ZbModel, site_left_foot), OFF(ZbModel, site_right_foot), OFF(ZbModel, body_base), OFF(ZbModel, body_left_foot),

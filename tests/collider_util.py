@@ -1,0 +1,163 @@
+"""Floor colliders for the tests: two model variants with colliders beyond the box soles, an
+independent numpy restatement of MuJoCo's plane-box / plane-capsule / plane-sphere contact sets
+(engine_collision_primitive.c mjc_PlaneBox, mjc_PlaneCapsule, mjc_PlaneSphere), and states whose
+colliders touch the floor. Test infrastructure only."""
+
+from __future__ import annotations
+
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+
+def _variant(edit) -> dict:
+    from zbot_amd.mjcf import load_mjcf, to_mjcf
+    from zbot_amd.model import load_description
+
+    root = ET.fromstring(to_mjcf(load_description()))
+    edit(root)
+    return load_mjcf(ET.tostring(root, encoding="unicode"))
+
+
+def limbs_desc() -> dict:
+    """The soles plus a box on the right shin and a capsule on the left hand (4 colliders)."""
+
+    def edit(root):
+        for b in root.iter("body"):
+            if b.get("name") == "right_knee_pitch_link":
+                b.append(ET.fromstring('<geom name="right_shin" type="box" size="0.015 0.02 0.05" pos="0 0 -0.05" '
+                                       'euler="0.2 0 0.1"/>'))
+            if b.get("name") == "left_gripper_roll_link":
+                b.append(ET.fromstring('<geom name="left_hand" type="capsule" size="0.012" '
+                                       'fromto="0 0 0 0.01 0.0 -0.06"/>'))
+
+    return _variant(edit)
+
+
+def round_desc() -> dict:
+    """Capsule feet (the touch sensors' zones) and a sphere on the head (3 colliders)."""
+
+    def edit(root):
+        for g in root.iter("geom"):
+            if g.get("name") in ("right_foot_sole", "left_foot_sole"):
+                g.set("type", "capsule")
+                g.set("size", "0.01 0.035")
+                g.set("pos", "0 0 0")
+                g.set("quat", "0.7071067811865476 0 0.7071067811865476 0")
+        for b in root.iter("body"):
+            if b.get("name") == "head":
+                b.append(ET.fromstring('<geom name="head_ball" type="sphere" size="0.05" pos="0 0 0.02"/>'))
+
+    return _variant(edit)
+
+
+def _qmat(q) -> np.ndarray:
+    w, x, y, z = np.asarray(q, np.float64) / np.linalg.norm(q)
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def geom_frames(cm, qpos) -> list[tuple[str, np.ndarray, np.ndarray, list[float]]]:
+    """(type, world centre, world rotation, size) of each collider at qpos (float64)."""
+    from zbot_amd.model import _kinematics
+
+    xpos, xmat = _kinematics(cm.bodies, np.asarray(qpos, np.float64))
+    names = cm.body_names
+    out = []
+    for g in cm.desc["geoms"]:
+        b = names.index(g["body"])
+        c = xpos[b] + xmat[b] @ np.asarray(g.get("pos", [0.0, 0.0, 0.0]))
+        R = xmat[b] @ _qmat(g.get("quat", [1.0, 0.0, 0.0, 0.0]))
+        out.append((g.get("type", "box"), c, R, list(g["size"])))
+    return out
+
+
+def _corner(sz, i) -> np.ndarray:
+    return np.array([sz[0] if i & 1 else -sz[0], sz[1] if i & 2 else -sz[1], sz[2] if i & 4 else -sz[2]])
+
+
+def box_corners(c, R, sz, margin=0.0) -> list[tuple[int, float]]:
+    """mjc_PlaneBox: (corner index, distance) of the corners in index order whose offset along the
+    normal is <= 0 and whose distance is within the margin, at most 4."""
+    out = []
+    for i in range(8):
+        w = R @ _corner(sz, i)
+        d = c[2] + w[2]
+        if d > margin or w[2] > 0:
+            continue
+        out.append((i, float(d)))
+        if len(out) == 4:
+            break
+    return out
+
+
+def contacts(cm, qpos, margin=0.0) -> list[list[tuple[np.ndarray, float]]]:
+    """Per collider, its floor contacts (point, distance) by MuJoCo's rules: box corners in index
+    order (bit 0 x, 1 y, 2 z) below the centre along the normal and within the margin, at most 4;
+    capsule end spheres (+end first); sphere."""
+    out = []
+    for ty, c, R, sz in geom_frames(cm, qpos):
+        cons = []
+        if ty == "box":
+            cons = [(c + R @ _corner(sz, i), d) for i, d in box_corners(c, R, sz, margin)]
+        elif ty == "capsule":
+            for sg in (1.0, -1.0):
+                e = c + sg * sz[1] * R[:, 2]
+                d = e[2] - sz[0]
+                if d <= margin:
+                    cons.append((e, d))
+        else:
+            d = c[2] - sz[0]
+            if d <= margin:
+                cons.append((c, d))
+        out.append(cons)
+    return out
+
+
+def lowest_point(cm, qpos) -> float:
+    """The lowest point of every collider at qpos (box corners, capsule / sphere surfaces)."""
+    z = np.inf
+    for ty, c, R, sz in geom_frames(cm, qpos):
+        if ty == "box":
+            for i in range(8):
+                loc = np.array([sz[0] if i & 1 else -sz[0], sz[1] if i & 2 else -sz[1], sz[2] if i & 4 else -sz[2]])
+                z = min(z, c[2] + (R @ loc)[2])
+        elif ty == "capsule":
+            z = min(z, c[2] - sz[1] * abs(R[2, 2]) - sz[0])
+        else:
+            z = min(z, c[2] - sz[0])
+    return float(z)
+
+
+def touching_states(cm, n, seed, depth=0.003) -> np.ndarray:
+    """[n, 27] qpos: a random base orientation (uniform over rotations, half the envs tipped onto a
+    side within 45 degrees of horizontal), the joints at JOINT_BIASES + N(0, 0.3) inside their
+    ranges, and the base height that puts the lowest collider point U(0, depth) below the floor."""
+    from zbot_amd.constants import JOINT_BIASES
+
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, 27))
+    lo, hi = np.full(20, -np.inf), np.full(20, np.inf)
+    for b in cm.bodies:
+        if b.jnt_type == 3 and b.jrange is not None:
+            lo[b.qposadr - 7], hi[b.qposadr - 7] = b.jrange
+    for e in range(n):
+        q = cm.reset_qpos().astype(np.float64)
+        if e % 2:
+            # lying: a random heading, pitched or rolled 45..135 degrees
+            yaw, tilt, ax = rng.uniform(-np.pi, np.pi), rng.uniform(np.pi / 4, 3 * np.pi / 4), rng.integers(2)
+            qy = np.array([np.cos(yaw / 2), 0, 0, np.sin(yaw / 2)])
+            qt = np.array([np.cos(tilt / 2), np.sin(tilt / 2) * (ax == 0), np.sin(tilt / 2) * (ax == 1), 0])
+            w1, x1, y1, z1 = qy
+            w2, x2, y2, z2 = qt
+            quat = np.array([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                             w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2])
+        else:
+            quat = rng.normal(size=4)
+        q[3:7] = quat / np.linalg.norm(quat)
+        q[7:] = np.clip(np.array([b for _, b, _ in JOINT_BIASES]) + rng.normal(scale=0.3, size=20), lo, hi)
+        q[2] = 0.0
+        q[2] = -lowest_point(cm, q) - rng.uniform(0.0, depth)
+        out[e] = q
+    return out

@@ -1,0 +1,144 @@
+"""Floor colliders beyond the two box soles on the GPU (the general-collider kernels, XG): a right
+shin box and a left hand capsule beside the soles ("limbs"), and capsule feet with a head sphere
+("round"), in states where the colliders touch the floor (tests/collider_util.py), against the
+oracle on the same model and state."""
+
+import numpy as np
+import pytest
+
+import collider_util as U
+from zbot_amd import compile_model, default_config
+from zbot_amd import cstructs as cs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module", params=["limbs", "round"])
+def variant(request):
+    return request.param, compile_model(U.limbs_desc() if request.param == "limbs" else U.round_desc())
+
+
+def contact_env(O, cm, cfg, n, seed):
+    """An oracle env whose qpos are touching_states (at rest, no warm start)."""
+    env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
+    env.reset()
+    env.state[:, :27] = U.touching_states(cm, n, seed).astype(np.float32)
+    env.state[:, 32:58] = 0.0
+    env.state[:, cs.S_QACCW:cs.S_QACCW + 32] = 0.0
+    return env
+
+
+def test_debug_forward_matches_oracle(torch_gpu, variant, oracle_mod):
+    """One forward pass: contact and constraint counts exact, constrained acceleration and touch
+    within the stage test's bounds (test_forward_stages_match_oracle)."""
+    torch = torch_gpu
+    from zbot_amd.engine import DBG, HipEngine
+
+    name, cm = variant
+    cfg = default_config()
+    n = 64
+    env = contact_env(oracle_mod, cm, cfg, n, seed=5)
+    st = env.state.copy()
+    ctrl = (np.random.default_rng(2).normal(size=(n, 20)) * 0.5).astype(np.float32)
+    eng = HipEngine(cm, cfg, n)
+    g = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()
+    worst = 0.0
+    for e in range(n):
+        ref = oracle_mod.forward_debug(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
+        assert int(g[e, DBG["misc"] + 1]) == ref["ncon"], (name, e)
+        assert int(g[e, DBG["misc"]]) == ref["nefc"], (name, e)
+        qa = g[e, DBG["qacc"]:DBG["qacc"] + 26]
+        err = np.abs(qa - ref["qacc"]).max() / max(1.0, np.abs(ref["qacc"]).max())
+        worst = max(worst, err)
+        assert err <= 1e-3, (name, e, err)
+        np.testing.assert_allclose(g[e, DBG["misc"] + 2:DBG["misc"] + 4], ref["touch"], rtol=1e-3, atol=1e-3)
+    print(f"\n[{name} debug forward] max relative qacc error {worst:.2e}")
+
+
+# One env-step from a touching state at rest (the contacts' first impulses), fp32 engine vs fp32
+# oracle, about 5x the max error measured on MI355X (round 3, profiles/r03_v7_gpu_colliders.log:
+# Newton qpos 3.0e-7, qvel 3.6e-5, planner 2.2e-5, obs_critic 1.4e-4, obs_extra 4.2e-3, reward
+# 1.6e-6, terms 9.0e-7).
+COLLIDER_TOL = {
+    "qpos": (2e-6, 0.0),
+    "qvel": (2e-4, 0.0),
+    "planner": (1e-4, 0.0),
+    "obs_actor": (2e-4, 0.0),
+    "obs_critic": (1e-3, 0.0),
+    "obs_extra": (2e-2, 0.0),
+    "reward": (1e-5, 0.0),
+    "reward_terms": (5e-6, 0.0),
+}
+# CG (8 unconverged iterations, as ONE_STEP_TOL_CG): ~5x the measured qpos 2.8e-6, qvel 3.4e-4,
+# planner 8.4e-5, obs_critic 1.6e-2, obs_extra 0.30, reward 4.9e-5, terms 1.2e-5.
+COLLIDER_TOL_CG = {
+    "qpos": (1.5e-5, 0.0),
+    "qvel": (2e-3, 0.0),
+    "planner": (5e-4, 0.0),
+    "obs_actor": (2e-3, 0.0),
+    "obs_critic": (8e-2, 0.0),
+    "obs_extra": (1.5, 0.0),
+    "reward": (2.5e-4, 0.0),
+    "reward_terms": (6e-5, 0.0),
+}
+
+
+@pytest.mark.parametrize("solver", ["newton", "cg"])
+def test_one_step_matches_oracle(torch_gpu, variant, oracle_mod, solver):
+    torch = torch_gpu
+    from test_gpu_parity import MaxErr, one_step_outputs, oracle_steps
+
+    from zbot_amd.engine import HipEngine
+
+    name, cm = variant
+    cfg = default_config(solver=solver)
+    n = 64
+    env = contact_env(oracle_mod, cm, cfg, n, seed=11)
+    eng = HipEngine(cm, cfg, n, seed=11)
+    err = MaxErr(f"colliders {name} {solver} one-step")
+    tols = COLLIDER_TOL_CG if solver == "cg" else COLLIDER_TOL
+    for t in range(2):
+        eng.set_state(torch.from_numpy(env.state.copy()))
+        eng.set_rand(torch.from_numpy(env.rand.copy()))
+        a = oracle_mod.synthetic_actions(cm.cmodel, 11, n, 0, t)
+        ref, ref64 = oracle_steps(oracle_mod, cm, cfg, env, a, 11)
+        out = eng.step(torch.from_numpy(a).cuda())
+        torch.cuda.synchronize()
+        gs = eng.get_state().cpu().numpy()
+        np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
+        for key, got, want in one_step_outputs(gs, out, env.state, ref):
+            err.add(key, got, want, *tols[key], ref64=ref64[key])
+    err.report()
+
+
+def test_rollout_launch_equals_steps(torch_gpu, variant, oracle_mod):
+    """zb_rollout over T steps is bit-identical to T zb_step launches with the general colliders
+    (auto-resets included)."""
+    torch = torch_gpu
+    from zbot_amd.engine import HipEngine
+
+    _, cm = variant
+    cfg = default_config(push=True)
+    n, T = 32, 6
+    A = torch.from_numpy(np.stack([oracle_mod.synthetic_actions(cm.cmodel, 4, n, 0, t, std=0.5)
+                                   for t in range(T)])).cuda()
+    env = contact_env(oracle_mod, cm, cfg, n, seed=4)
+    a = HipEngine(cm, cfg, n, seed=4)
+    b = HipEngine(cm, cfg, n, seed=4)
+    for h in (a, b):
+        h.set_state(torch.from_numpy(env.state.copy()))
+        h.set_rand(torch.from_numpy(env.rand.copy()))
+    for t in range(T):
+        a.step(A[t])
+    b.rollout(A, reward_sum=torch.zeros(n, device="cuda"))
+    torch.cuda.synchronize()
+    assert np.array_equal(a.get_state().cpu().numpy(), b.get_state().cpu().numpy())

@@ -388,13 +388,31 @@ def test_actuator_errors(what, err):
         _actuated(mut)
 
 
-def test_non_box_colliders_are_reported():
+def test_colliders_are_parsed_and_unsupported_ones_reported():
     b = load_mjcf("<mujoco><worldbody><body name='b'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
-                  "<geom name='shin' type='capsule' size='0.01 0.05'/>"
+                  "<geom name='shin' type='capsule' size='0.01' fromto='0 0 0 0 0.06 -0.08'/>"
+                  "<geom name='hand' type='sphere' size='0.02' pos='0.1 0 0'/>"
+                  "<geom name='cyl' type='cylinder' size='0.01 0.05'/>"
                   "<geom name='vis' type='mesh' mesh='m' contype='0' conaffinity='0'/></body></worldbody></mujoco>")
-    assert b["skipped_geoms"] == [{"name": "shin", "body": "b", "type": "capsule"}]
-    assert b["geoms"] == []
+    assert b["skipped_geoms"] == [{"name": "cyl", "body": "b", "type": "cylinder"}]
+    shin, hand = b["geoms"]
+    assert shin["type"] == "capsule" and hand == {"name": "hand", "body": "b", "type": "sphere", "size": [0.02],
+                                                  "pos": [0.1, 0.0, 0.0]}
+    # fromto: centre at the midpoint, half-length 0.05, local +z along the segment
+    np.testing.assert_allclose(shin["size"], [0.01, 0.05])
+    np.testing.assert_allclose(shin["pos"], [0.0, 0.03, -0.04])
+    w, x, y, z = shin["quat"]
+    zaxis = [2 * (x * z + w * y), 2 * (y * z - w * x), 1 - 2 * (x * x + y * y)]
+    np.testing.assert_allclose(zaxis, [0.0, 0.6, -0.8], atol=1e-12)
     assert "skipped_geoms" not in load_mjcf(to_mjcf(load_description()))
+
+
+def test_colliders_past_four_are_reported():
+    geoms = "".join(f"<geom name='g{i}' type='box' size='0.01 0.01 0.01'/>" for i in range(6))
+    b = load_mjcf("<mujoco><worldbody><body name='b'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
+                  f"{geoms}</body></worldbody></mujoco>")
+    assert [g["name"] for g in b["geoms"]] == ["g0", "g1", "g2", "g3"]
+    assert [g["name"] for g in b["skipped_geoms"]] == ["g4", "g5"]
 
 
 def test_command_line_round_trip(tmp_path):
@@ -418,33 +436,38 @@ def test_missing_file_is_reported():
 
 
 def test_skipped_colliders_are_rejected_by_zb_create():
-    """A real MJCF whose shins / hands collide (capsules) cannot be simulated by this engine, which
-    collides the two box soles with the floor: zb_create rejects it (ZB_EMODEL, nskip_geom) instead
-    of dropping those contacts silently; compile_model(..., drop_colliders=True) drops them
-    knowingly (missing item 3)."""
+    """A collider the engine has no floor contact for (a cylinder here; or a fifth collider) is not
+    dropped silently: zb_create rejects the model (ZB_EMODEL, nskip_geom); compile_model(...,
+    drop_colliders=True) drops it knowingly (missing item 3). Supported extra colliders
+    (a capsule shin) pass validation."""
     import ctypes as C
     import xml.etree.ElementTree as ET
 
     from zbot_amd import compile_model, default_config
     from zbot_amd import engine as E
 
-    root = ET.fromstring(to_mjcf(load_description()))
-    for b in root.iter("body"):
-        if "knee" in b.get("name"):
-            b.append(ET.fromstring('<geom name="shin_col" type="capsule" size="0.015" fromto="0 0 0 0 0 -0.08" '
-                                   'mass="0"/>'))
-            break
-    desc = load_mjcf(ET.tostring(root, encoding="unicode"))
-    assert [g["name"] for g in desc["skipped_geoms"]] == ["shin_col"]
+    def with_shin(gtype):
+        root = ET.fromstring(to_mjcf(load_description()))
+        for b in root.iter("body"):
+            if "knee" in b.get("name"):
+                size = "0.015" if gtype == "capsule" else "0.015 0.04"
+                b.append(ET.fromstring(f'<geom name="shin_col" type="{gtype}" size="{size}" fromto="0 0 0 0 0 -0.08" '
+                                       'mass="0"/>'))
+                break
+        return load_mjcf(ET.tostring(root, encoding="unicode"))
+
     L = E.load_library()
     h = C.c_void_p()
+    desc = with_shin("cylinder")
+    assert [g["name"] for g in desc["skipped_geoms"]] == ["shin_col"]
     cm = compile_model(desc)
     assert cm.cmodel.nskip_geom == 1
     rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
     assert rc == -4 and b"colliding geoms" in L.zb_last_error()
-    cm = compile_model(desc, drop_colliders=True)
-    assert cm.cmodel.nskip_geom == 0
-    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
-    assert rc != -4  # validation passes (no device here: -2)
-    if rc == 0:
-        L.zb_destroy(h)
+    for cm in (compile_model(desc, drop_colliders=True), compile_model(with_shin("capsule"))):
+        assert cm.cmodel.nskip_geom == 0
+        rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+        assert rc != -4, L.zb_last_error()  # validation passes (no device here: -2)
+        if rc == 0:
+            L.zb_destroy(h)
+    assert compile_model(with_shin("capsule")).cmodel.ngeom == 3
