@@ -111,8 +111,9 @@ __shared__ EnvL g_lds[NTEAM];
 /* The second contact-row bank of the general-collider kernels (XG: geoms 2-3, or any model that is
    not exactly two box soles): its Jacobian rows. Its J'DJ blocks are staged in the Hessian rows'
    space and its per-row scratch reuses rowDA / rowF after the first bank's (hessian_factor), so a
-   block of the XG kernels needs 3 KB more LDS, not 6: 7 blocks per CU instead of 6. Only the XG
-   instantiations reference it, so the LDS of the two-sole kernels is unchanged. */
+   block of the XG kernels needs 3 KB more LDS rather than 6 (23 232 B: 6 blocks per CU against the
+   two-sole kernels' 8). Only the XG instantiations reference it, so the LDS of the two-sole kernels
+   is unchanged. */
 struct __align__(16) EnvX {
   float J[32][CAP];
 };
@@ -1897,7 +1898,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float H[CAP], Hd;
-  uint32_t tb, tb2 = 0u;
+  uint32_t tb, tb2 = 0u, ch2 = 0u;
   float dl2 = 0.f;
   if (full) {
     Hd = load_mrow(c, H);
@@ -1949,7 +1950,8 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     tb = team_ballot(dl != 0.f) & c.rowmask;
     if (XG && r.x.any) {
       dl2 = r.x.ex ? ((r.x.act ? r.x.D : 0.f) - (pa2 ? r.x.D : 0.f)) : 0.f;
-      tb2 = team_ballot(dl2 != 0.f) & c.rowmask2;
+      ch2 = team_ballot(dl2 != 0.f); /* team-uniform: some row of the bank changed */
+      tb2 = ch2 & c.rowmask2;        /* per dof lane: the changed rows on its chain */
     }
     tsync();
   }
@@ -1965,8 +1967,9 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     }
     Hd += dd;
   }
-  if (XG && tb2 != 0u) {
-    /* the second bank's changed rows, their D through rowF after the first bank's (team-uniform) */
+  if (XG && ch2 != 0u) {
+    /* the second bank's changed rows, their D through rowF after the first bank's: every lane of the
+       team writes its row (team-uniform branch), a dof lane then adds the rows on its chain */
     tsync();
     L->rowF[c.l] = dl2;
     tsync();
