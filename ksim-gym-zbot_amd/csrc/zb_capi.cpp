@@ -42,6 +42,7 @@ struct ZbHandle {
   float* stamps; /* ZB_STAMPS diagnostic build only */
   uint32_t* sched; /* chunked step: [2 + npair] counters and per-pair progress (zb_internal.h) */
   int32_t* itpart; /* chunked step: [n] Newton iterations so far */
+  float* xj;       /* general colliders: [n + 1, ZB_XJ_STRIDE] second-bank Jacobian rows (zb_internal.h) */
   int nchunk;      /* work units per pair of envs in zb_step (1: unchunked) */
   int air_mark;    /* zb_mark_rollout_start: the next zb_step / zb_rollout is a rollout's step 0 */
   int air_marked;  /* a marked step has been launched since the last zb_feet_airtime_exact */
@@ -134,6 +135,7 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMemset(h->sched, 0, (3 + (n + 1) / 2) * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&h->itpart, n * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(h->itpart, 0, n * sizeof(int32_t));
+  if (e == hipSuccess && zb::needs_xg(model)) e = hipMalloc(&h->xj, (n + 1) * ZB_XJ_STRIDE * sizeof(float));
   h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device, zb::needs_xg(model) ? 1 : 0));
 #if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
   {
@@ -165,6 +167,7 @@ int zb_destroy(ZbHandle* h) {
   if (h->stamps) (void)hipFree(h->stamps);
   if (h->sched) (void)hipFree(h->sched);
   if (h->itpart) (void)hipFree(h->itpart);
+  if (h->xj) (void)hipFree(h->xj);
   delete h;
   return ZB_OK;
 }
@@ -190,6 +193,7 @@ static zb::StepArgs base_args(ZbHandle* h) {
   a.itpart = h->itpart;
   a.solver = h->cfg.solver;
   a.xg = zb::needs_xg(&h->hmodel) ? 1 : 0;
+  a.xj = h->xj;
   return a;
 }
 

@@ -70,6 +70,8 @@ struct EnvS {
   /* the team's RNG identity (global env id, seed): read only at draw sites (observation noise,
      pushes, resets), so kept here rather than in registers across the substep loop */
   uint32_t env, seed_lo, seed_hi;
+  /* XG kernels: the env's block of second-bank Jacobian rows in global scratch (xrows) */
+  uint32_t xj_lo, xj_hi;
 };
 struct Sensors {
   float fq[4], gyro[3], acc[3], touch[2], force[6];
@@ -108,17 +110,6 @@ struct __align__(16) EnvL {
 /* the block's two team working sets (one wave = two teams) */
 __shared__ EnvL g_lds[NTEAM];
 
-/* The second contact-row bank of the general-collider kernels (XG: geoms 2-3, or any model that is
-   not exactly two box soles): its Jacobian rows. Its J'DJ blocks are staged in the Hessian rows'
-   space and its per-row scratch reuses rowDA / rowF after the first bank's (hessian_factor), so a
-   block of the XG kernels needs 3 KB more LDS rather than 6 (23 232 B: 6 blocks per CU against the
-   two-sole kernels' 8). Only the XG instantiations reference it, so the LDS of the two-sole kernels
-   is unchanged. */
-struct __align__(16) EnvX {
-  float J[32][CAP];
-};
-__shared__ EnvX g_ldsx[NTEAM];
-__device__ __forceinline__ EnvX* envx() { return &g_ldsx[(threadIdx.x & 63) / TEAM]; }
 
 /* ----------------------------- team primitives ----------------------------- */
 __device__ __forceinline__ float tsh(float v, int src) { return __shfl(v, src, TEAM); }
@@ -480,6 +471,21 @@ __device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); 
    workgroup visibility, first row of its hand-off table). */
 typedef __attribute__((address_space(1))) float gfloat_t;
 typedef __attribute__((address_space(1))) uint32_t guint_t;
+typedef float xv4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) xv4f gfloat4_t;
+
+/* The second contact-row bank of the general-collider kernels (XG: geoms 2-3, or any model that
+   is not exactly two box soles) keeps its Jacobian rows in global scratch (StepArgs::xj, one
+   [32][CAP] block per env): 1.5 KB per env in LDS would take those kernels from 8 workgroups per
+   CU to 6. They are written and read only while the bank has rows in the wave (shins or hands on
+   the floor), through the CU's L1; its J'DJ blocks and row scratch reuse the first bank's LDS. */
+__device__ __forceinline__ gfloat_t* xrows(const EnvL* L) {
+  return (gfloat_t*)(((uint64_t)L->s.xj_hi << 32) | (uint64_t)L->s.xj_lo);
+}
+__device__ __forceinline__ void set_xrows(EnvL* L, float* base) {
+  L->s.xj_lo = (uint32_t)(uint64_t)base;
+  L->s.xj_hi = (uint32_t)((uint64_t)base >> 32);
+}
 template <bool CG = true>
 __device__ __forceinline__ float ld_cg(const float* p) {
   if constexpr (CG) return __hip_atomic_load((gfloat_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -662,6 +668,20 @@ __device__ __forceinline__ void st_row(float* p, const float v[CAP]) {
   q[0] = make_float4(v[0], v[1], v[2], v[3]);
   q[1] = make_float4(v[4], v[5], v[6], v[7]);
   q[2] = make_float4(v[8], v[9], v[10], v[11]);
+}
+/* the same for a row of the second bank's global scratch (xrows) */
+__device__ __forceinline__ void ld_row(const gfloat_t* p, float v[CAP]) {
+  const gfloat4_t* q = reinterpret_cast<const gfloat4_t*>(p);
+  const xv4f a = q[0], b = q[1], c4 = q[2];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  v[8] = c4.x; v[9] = c4.y; v[10] = c4.z; v[11] = c4.w;
+}
+__device__ __forceinline__ void st_row(gfloat_t* p, const float v[CAP]) {
+  gfloat4_t* q = reinterpret_cast<gfloat4_t*>(p);
+  q[0] = xv4f{v[0], v[1], v[2], v[3]};
+  q[1] = xv4f{v[4], v[5], v[6], v[7]};
+  q[2] = xv4f{v[8], v[9], v[10], v[11]};
 }
 
 /* ------------------------------- kinematics -------------------------------- */
@@ -1302,7 +1322,8 @@ __device__ __forceinline__ float mul_m(const Ctx& c, float x, int slot) {
 
 /* chain gather: sum_e Jc[e] * vec[slot][anc_e] for a contact row (Jrow: the row in bank 0's or
    bank 1's J, chd: the row's chain head) */
-__device__ __forceinline__ float row_dot(const Ctx& c, const float* Jrow, int chd, int slot) {
+template <typename JP>
+__device__ __forceinline__ float row_dot(const Ctx& c, JP Jrow, int chd, int slot) {
   float jr[CAP], vv[CAP];
   ld_row(Jrow, jr);
 #pragma unroll
@@ -1316,7 +1337,7 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
   return row_dot(c, &c.L->u.J[c.l][0], r.chd, slot);
 }
 __device__ __forceinline__ float row_dot_x(const Ctx& c, const Rows& r, int slot) {
-  return row_dot(c, &envx()->J[c.l][0], r.x.chd, slot);
+  return row_dot(c, (const gfloat_t*)xrows(c.L) + c.l * CAP, r.x.chd, slot);
 }
 
 /* ----------------------------------- RNE ----------------------------------- */
@@ -1566,9 +1587,9 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
 }
 
 /* the contact rows of one bank: collision, then the row of lane l (J at Jrow) */
-template <bool XG, typename CR>
+template <bool XG, typename CR, typename JP>
 __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const BodyK& B, const float cm[3], int bank,
-                                             CR& r, float* Jrow) {
+                                             CR& r, JP Jrow) {
   MP m = c.m;
   CP cfg = c.cfg;
   EnvL* L = c.L;
@@ -1618,9 +1639,9 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   if (TEAM < 64) tb &= 0xffffffffu;
   r.nrow = __popc(tb);
   r.exmask = tb;
-  /* every row is stored, zero where there is no contact (and past the row's
-     depth), so the row products below need no per-entry masks */
-  st_row(Jrow, Jc);
+  /* every row is stored, zero where there is no contact (and past the row's depth), so the row
+     products below need no per-entry masks; the global second bank only while the wave uses it */
+  if (bank == 0 || bal != 0ull) st_row(Jrow, Jc);
 }
 
 /* collision + contact rows (lane r; XG: both banks) + dof rows (lane j) */
@@ -1632,10 +1653,15 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   const int l = c.l;
   contact_rows<XG>(c, s, B, cm, 0, r, &c.L->u.J[l][0]);
   if constexpr (XG) {
-    contact_rows<XG>(c, s, B, cm, 1, r.x, &envx()->J[l][0]);
+    contact_rows<XG>(c, s, B, cm, 1, r.x, xrows(c.L) + l * CAP);
     /* the second bank's work is skipped, bit for bit, while no row of it exists in the wave (the
        usual case: shins and hands off the floor) */
     r.x.any = __ballot(r.x.ex) != 0ull;
+    if (r.x.any) {
+      /* the rows just stored are read by other lanes from here on */
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
   }
   /* ---- dof rows (lane j) ---- */
   r.hf = r.hl = false;
@@ -1726,7 +1752,8 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
    xor 2, quad xor 1). At each stage a lane keeps the half of its column sums on its side and adds
    its partner's copy of them, so lane 16 f + e ends with the geom-f sum of column e (45 instead of
    108 VALU instructions). */
-__device__ __forceinline__ float colsum16(const float* Jrow, float fr) {
+template <typename JP>
+__device__ __forceinline__ float colsum16(JP Jrow, float fr) {
   float q[16];
   {
     float jr[CAP];
@@ -1784,14 +1811,13 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, f
   L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
   float sx0 = 0.f, sx1 = 0.f;
   if (XG && r.x.any) {
-    EnvX* X = envx();
     float f3;
     int a3;
     const float k3 = eval_one(r.x.jar, r.x.D, f3, a3);
     cost += r.x.ex ? k3 : 0.f;
     r.x.f = r.x.ex ? f3 : r.x.f;
     r.x.act = r.x.ex ? a3 : r.x.act;
-    const float cx = colsum16(&X->J[c.l][0], r.x.ex ? r.x.f : 0.f);
+    const float cx = colsum16((const gfloat_t*)xrows(c.L) + c.l * CAP, r.x.ex ? r.x.f : 0.f);
     sx0 = tsh(cx, ddep);
     sx1 = tsh(cx, 16 + ddep);
   }
@@ -1825,7 +1851,7 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float 
  * lane l supplies row 4*chunk + l/16, entry l%16). Staged in the env's L[][]
  * as [foot][12][12]; L[][] is free until factor_ldl writes it. D is rowDA
  * (0 for absent / inactive rows). Wave-uniform: call with every lane active.
- * BANK2: the same for the second bank's geoms (EnvX J, rowDA holding that bank's D), staged in
+ * BANK2: the same for the second bank's geoms (xrows J, rowDA holding that bank's D), staged in
  * the Hessian rows Hs[][], free until hessian_factor stores the assembled rows. */
 template <bool BANK2>
 __device__ __forceinline__ void jdj_mfma() {
@@ -1846,7 +1872,7 @@ __device__ __forceinline__ void jdj_mfma() {
         const int r = 16 * f + 4 * ch + k;
         /* no masks: rowDA is zero for absent / inactive rows, and output rows or
            columns e >= CAP (lanes reading entry CAP-1) are never stored */
-        const float jv = BANK2 ? g_ldsx[t].J[r][ec] : g_lds[t].u.J[r][ec];
+        const float jv = BANK2 ? xrows(&g_lds[t])[r * CAP + ec] : g_lds[t].u.J[r][ec];
         const float dv = g_lds[t].rowDA[r]; /* BANK2: the second bank's, written by hessian_factor */
         acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv * jv, jv, acc[t][f], 0, 0, 0);
       }
@@ -1863,8 +1889,8 @@ __device__ __forceinline__ void jdj_mfma() {
 }
 
 /* H[e] += D_r J_r[e] J_r' over the rows of bitmask tb (pairs of rows per pass; da: the rows' D) */
-__device__ __forceinline__ void add_rows(uint32_t tb, const float (*J)[CAP], const float* da, int ddep, float H[CAP],
-                                         float& Hd) {
+template <typename JP>
+__device__ __forceinline__ void add_rows(uint32_t tb, JP J, const float* da, int ddep, float H[CAP], float& Hd) {
   while (tb) {
     const int k0 = __ffs(tb) - 1;
     tb &= tb - 1u;
@@ -1872,9 +1898,9 @@ __device__ __forceinline__ void add_rows(uint32_t tb, const float (*J)[CAP], con
     const int k1 = h1 ? __ffs(tb) - 1 : k0;
     tb &= tb - 1u;
     float j0[CAP], j1[CAP];
-    ld_row(&J[k0][0], j0);
-    ld_row(&J[k1][0], j1);
-    const float jd0 = J[k0][ddep], jd1 = J[k1][ddep];
+    ld_row(J + k0 * CAP, j0);
+    ld_row(J + k1 * CAP, j1);
+    const float jd0 = J[k0 * CAP + ddep], jd1 = J[k1 * CAP + ddep];
     const float jj0 = da[k0] * jd0;
     const float jj1 = (da[k1] * jd1) * (h1 ? 1.f : 0.f); /* a weight, not a select (loads) */
     Hd += jj0 * jd0;
@@ -1956,7 +1982,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     tsync();
   }
   if (c.l < NV) {
-    add_rows(tb, L->u.J, full ? L->rowDA : L->rowF, ddep, H, Hd);
+    add_rows(tb, (const float*)&L->u.J[0][0], full ? L->rowDA : L->rowF, ddep, H, Hd);
     float dd = 0.f;
     if (full) {
       if (r.hf && r.actf) dd += r.Df;
@@ -1973,7 +1999,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     tsync();
     L->rowF[c.l] = dl2;
     tsync();
-    if (c.l < NV) add_rows(tb2, envx()->J, L->rowF, ddep, H, Hd);
+    if (c.l < NV) add_rows(tb2, (const gfloat_t*)xrows(L), L->rowF, ddep, H, Hd);
   }
   if (XG && full && r.x.any) tsync(); /* the second bank's G rows in Hs[] are read before H is stored there */
   st_row(&L->Hs[c.l][0], H);
@@ -2972,6 +2998,8 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  /* the env's second-bank rows (a team past n: the spare block n) */
+  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(live ? e : a.n_envs) * ZB_XJ_STRIDE);
   /* per-env row addresses are formed where they are used, from an opaque copy of the env
      index: held across the substep loop they were 64-bit values spilled to scratch */
   auto state_row = [&]() { return a.state + (size_t)vopq(ee) * ZB_STATE_STRIDE; };
@@ -3144,6 +3172,8 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  /* the env's second-bank rows (a team past n: the spare block n) */
+  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(inb ? e : a.n_envs) * ZB_XJ_STRIDE);
   float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   float* rnd = live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)ee * ZB_RAND_STRIDE : nullptr;
   EnvS& s = c.L->s;
@@ -3174,6 +3204,8 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
+  /* the env's second-bank rows (a team past n: the spare block n) */
+  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(live ? e : a.n_envs) * ZB_XJ_STRIDE);
   float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   EnvS& s = c.L->s;
   LaneS ls;

@@ -23,6 +23,7 @@
 #define ZB_DBG_CVEL    1536  /* [nbody*6] */
 #define ZB_DBG_MISC    1728  /* nefc, ncon, touch_l, touch_r, imu quat(4), gyro(3), acc(3) */
 #define ZB_DBG_STRIDE  1760
+#define ZB_XJ_STRIDE   (32 * ZB_MAX_DEPTH) /* floats per env of StepArgs::xj */
 #define ZB_NSTAMP      20    /* phase-stamp slots of the -DZB_STAMPS build (zb_engine.hip S_*) */
 
 namespace zb {
@@ -58,6 +59,7 @@ struct StepArgs {
   int air_mark;             /* first step of a rollout: save its contacts + causal airtime term */
   int solver;               /* ZB_SOLVER_NEWTON / ZB_SOLVER_CG: which kernel instantiation runs */
   int xg;                   /* general colliders (zb_host.h needs_xg): the two-bank instantiation */
+  float* xj;                /* xg: [n + 1, ZB_XJ_STRIDE] second-bank Jacobian rows (the last block: ghost teams) */
 };
 
 /* workgroups of step_kernel resident on the device at once (occupancy x CUs) */

@@ -321,9 +321,14 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) 
         qpos0[3:7] = root.quat / np.linalg.norm(root.quat)
 
     geoms = desc.get("geoms", [])
-    geom_names = [g["name"] for g in geoms]
     if len(geoms) > cs.MAX_GEOM:
         raise ValueError("too many collision geoms")
+    # the touch sensors' geoms (the soles) first, then the others in document order: the engine
+    # runs geoms 0-1 in its first contact-row bank and skips the second while it has no contacts
+    # (DESIGN.md §4j), so the colliders that touch the floor all the time belong in the first
+    touch = [sd["touch_geom"] for sd in desc.get("sites", []) if "touch_geom" in sd]
+    geoms = sorted(geoms, key=lambda g: (0 if g["name"] in touch else 1))
+    geom_names = [g["name"] for g in geoms]
 
     if auto_z:
         q = qpos0.copy()

@@ -21,7 +21,8 @@ def test_variant_models_compile(variant):
     name, cm = variant
     m = cm.cmodel
     if name == "limbs":
-        assert cm.geom_names == ["right_shin", "right_foot_sole", "left_foot_sole", "left_hand"]
+        # the touch sensors' soles first (the engine's first contact-row bank), then document order
+        assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "right_shin", "left_hand"]
         assert list(m.geom_type)[:4] == [cs.GEOM_BOX, cs.GEOM_BOX, cs.GEOM_BOX, cs.GEOM_CAPSULE]
         np.testing.assert_allclose(list(m.geom_size[3])[:2], [0.012, np.hypot(0.01, 0.06) / 2], rtol=1e-6)
     else:
