@@ -65,7 +65,7 @@ def test_debug_forward_matches_oracle(torch_gpu, variant, oracle_mod):
 
 
 # One env-step from a touching state at rest (the contacts' first impulses), fp32 engine vs fp32
-# oracle, about 5x the max error measured on MI355X (round 3, profiles/r03_v10_gpu_colliders.log:
+# oracle, about 5x the max error measured on MI355X (round 3, profiles/r03_v12_gpu_colliders.log:
 # Newton qpos 3.0e-7, qvel 3.6e-5, planner 2.2e-5, obs_critic 1.4e-4, obs_extra 4.2e-3, reward
 # 1.6e-6, terms 9.0e-7).
 COLLIDER_TOL = {
