@@ -96,3 +96,46 @@ def test_default_chunking(torch_gpu, cmodel, n, push, steps):
     assert same(torch, ref.get_state(), auto.get_state())
     assert torch.equal(ref.solver_iters(), auto.solver_iters())
     assert same(torch, ref.get_stats(), auto.get_stats())
+
+
+def test_chunked_step_bit_exact_general_colliders(torch_gpu, oracle_mod):
+    """The general-collider kernels (a shin box and a hand capsule beside the soles, DESIGN.md
+    §4j) chunked against unchunked, from states where those colliders touch the floor, so that the
+    second contact bank and its global-scratch rows are in use across the hand-offs."""
+    torch = torch_gpu
+    import numpy as np
+
+    import collider_util as U
+    from zbot_amd import compile_model
+    from zbot_amd import cstructs as cs
+
+    cm = compile_model(U.limbs_desc())
+    cfg = default_config(push=True, randomize=True)
+    n = 37
+    ref, chk = make(cm, cfg, n, 1), make(cm, cfg, n, 5)
+    env = oracle_mod.OracleEnv(cm.cmodel, cfg, n, seed=3)
+    env.reset()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    names = [gd["name"] for gd in cm.desc["geoms"]]  # collider_util's order (document order)
+    extra = [names.index("right_shin"), names.index("left_hand")]
+    touched = 0
+    for t in range(3):
+        st = env.state.copy()
+        st[:, :27] = U.touching_states(cm, n, seed=20 + t).astype(np.float32)
+        st[:, 32:58] = 0.0
+        st[:, cs.S_QACCW:cs.S_QACCW + 32] = 0.0
+        touched += sum(any(len(c[i]) for i in extra) for c in
+                       (U.contacts(cm, q) for q in st[:, :27].astype(np.float64)))
+        for h in (ref, chk):
+            h.set_state(torch.from_numpy(st.copy()))
+            h.set_rand(torch.from_numpy(env.rand.copy()))
+        act = bias + 0.3 * torch.randn(n, 20, device="cuda", generator=g)
+        o1 = {k_: v.clone() for k_, v in ref.step(act).items()}
+        o2 = chk.step(act)
+        for name in o1:
+            assert same(torch, o1[name], o2[name]), (t, name)
+        assert same(torch, ref.get_state(), chk.get_state()), t
+        assert torch.equal(ref.solver_iters(), chk.solver_iters()), t
+    assert touched > 0  # the shin or the hand touches in some of the states
