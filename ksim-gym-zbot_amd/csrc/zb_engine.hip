@@ -1340,6 +1340,48 @@ __device__ __forceinline__ float row_dot_x(const Ctx& c, const Rows& r, int slot
   return row_dot(c, (const gfloat_t*)xrows(c.L) + c.l * CAP, r.x.chd, slot);
 }
 
+/* y = M x (mul_m) and, in the same LDS round trip, the lane's contact-row products with x
+ * (jv, row_dot over vec[slot]) and, when slot2 >= 0, with vec[slot2] (jv2, published before the
+ * call): the row loads go out with mul_m's ancestor gather instead of after its reduction and
+ * exchange point. Bit-identical to mul_m followed by row_dot. */
+__device__ __forceinline__ float row_dot_pre(const Ctx& c, const float jr[CAP], int chd, int slot) {
+  float vv[CAP];
+#pragma unroll
+  for (int e = 0; e < CAP; e++) vv[e] = c.L->vec[slot][anc_lin(chd, e)];
+  float v = 0.f;
+#pragma unroll
+  for (int e = 0; e < CAP; e++) v += jr[e] * vv[e];
+  return v;
+}
+__device__ __forceinline__ float mul_m_dot(const Ctx& c, const Rows& r, const float jr[CAP], float x, int slot, float& jv,
+                                           int slot2, float& jv2) {
+  EnvL* L = c.L;
+  const int j = c.l;
+  const bool ischain = c.chd >= 0;
+  const int nroot = NROOT;
+  if (j < 32) L->vec[slot][j] = x;
+  tsync();
+  float mrow[CAP], vv[CAP];
+  ld_row(&L->M[j & 31][0], mrow);
+#pragma unroll
+  for (int e = 0; e < CAP; e++) vv[e] = L->vec[slot][anc_lin(c.chd, e)];
+  jv = row_dot_pre(c, jr, r.chd, slot);
+  jv2 = slot2 >= 0 ? row_dot_pre(c, jr, r.chd, slot2) : 0.f;
+  float y = 0.f;
+#pragma unroll
+  for (int e = 0; e < CAP; e++) y += mrow[e] * vv[e];
+  if (nroot > 0) {
+    static_assert(RMAX == 6, "reduce6_lane");
+    float si[RMAX];
+#pragma unroll
+    for (int i = 0; i < RMAX; i++) si[i] = (ischain && i < nroot) ? mrow[i] * x : 0.f;
+    const float sr = reduce6_lane(si);
+    if (j < nroot) y += sr;
+  }
+  tsync();
+  return y;
+}
+
 /* ----------------------------------- RNE ----------------------------------- */
 /* inclusive prefix sums of per-dof 6-vectors along the dof tree (root ->
  * dof), by pointer jumping over the parent links: ceil(log2(depth)) rounds of
@@ -1752,12 +1794,9 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
    xor 2, quad xor 1). At each stage a lane keeps the half of its column sums on its side and adds
    its partner's copy of them, so lane 16 f + e ends with the geom-f sum of column e (45 instead of
    108 VALU instructions). */
-template <typename JP>
-__device__ __forceinline__ float colsum16(JP Jrow, float fr) {
+__device__ __forceinline__ float colsum16_pre(const float jr[CAP], float fr) {
   float q[16];
   {
-    float jr[CAP];
-    ld_row(Jrow, jr);
 #pragma unroll
     for (int e = 0; e < CAP; e++) q[e] = jr[e] * fr; /* J rows are zero where no contact */
 #pragma unroll
@@ -1779,13 +1818,19 @@ __device__ __forceinline__ float colsum16(JP Jrow, float fr) {
   const bool s4 = (li & 1) != 0;
   return (s4 ? u2[1] : u2[0]) + dppf<0xB1>(s4 ? u2[0] : u2[1]);
 }
+template <typename JP>
+__device__ __forceinline__ float colsum16(JP Jrow, float fr) {
+  float jr[CAP];
+  ld_row(Jrow, jr);
+  return colsum16_pre(jr, fr);
+}
 
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
 /* returns this lane's cost share; the caller reduces it over the team (alone, or together with
    the Newton loop's other per-iteration sums in one tsum_n) */
 template <bool XG>
-__device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, float qacc, float qs, float fs,
-                                                       float Ma, float& grad) {
+__device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, const float jr[CAP], float qacc,
+                                                       float qs, float fs, float Ma, float& grad) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float cost = 0.f;
@@ -1822,7 +1867,7 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, f
     sx1 = tsh(cx, 16 + ddep);
   }
   /* J'f per dof: a dof adds the column sum at its depth of every geom whose chain holds it */
-  const float colsum = colsum16(&L->u.J[c.l][0], r.ex ? r.f : 0.f);
+  const float colsum = colsum16_pre(jr, r.ex ? r.f : 0.f);
   const float so = tsh(colsum, ddep), sx = tsh(colsum, 16 + ddep);
   tsync();
   float qc = 0.f;
@@ -1840,9 +1885,9 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, f
   return cost;
 }
 template <bool XG>
-__device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, float qacc, float qs, float fs, float Ma,
-                                                  float& grad) {
-  return tsum(update_constraint_lane<XG>(c, r, qacc, qs, fs, Ma, grad));
+__device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, const float jr[CAP], float qacc, float qs,
+                                                  float fs, float Ma, float& grad) {
+  return tsum(update_constraint_lane<XG>(c, r, jr, qacc, qs, fs, Ma, grad));
 }
 
 /* G_f = sum_{r in foot f} D_r J_r J_r' (depth-indexed 12x12) for both feet of
@@ -2012,12 +2057,13 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
 template <bool XG>
-__device__ __forceinline__ float line_search(const Ctx& c, Rows& r, float search, float Ma, float fs, float grad,
-                                             float& Mv) {
+__device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float jr[CAP], float search, float Ma, float fs,
+                                             float grad, float& Mv) {
   CP cfg = c.cfg;
   EnvL* L = c.L;
-  Mv = mul_m(c, search, V_TMP); /* leaves search in vec[V_TMP] */
-  r.Jv = row_dot(c, r, V_TMP); /* J rows are zero where no contact: no branch around the loads */
+  /* leaves search in vec[V_TMP]; J rows are zero where no contact: no branch around the loads */
+  float unused_;
+  Mv = mul_m_dot(c, r, jr, search, V_TMP, r.Jv, -1, unused_);
   if constexpr (XG) r.x.Jv = r.x.any ? row_dot_x(c, r, V_TMP) : 0.f;
   tsync();
   /* the quadratic's coefficients and the slope/curvature at alpha = 0 in one reduction:
@@ -2099,10 +2145,14 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   /* warmstart selection */
   float x = w;
   if (c.l < 32) L->vec[V_TMP2][c.l] = qs; /* mul_m's barrier publishes it with x in vec[V_TMP] */
-  float Ma = mul_m(c, x, V_TMP);
   /* rows that do not exist have zero J and zero aref: no mask */
-  float jw = row_dot(c, r, V_TMP) - r.aref;
-  float js = row_dot(c, r, V_TMP2) - r.aref;
+  float jw, js;
+  /* the lane's contact-row Jacobian: constant through the solve, kept in registers */
+  float jr[CAP];
+  ld_row(&L->u.J[c.l][0], jr);
+  float Ma = mul_m_dot(c, r, jr, x, V_TMP, jw, V_TMP2, js);
+  jw -= r.aref;
+  js -= r.aref;
   float jwx = 0.f, jsx = 0.f;
   if (XG && r.x.any) {
     jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
@@ -2127,7 +2177,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   r.jl = r.sl * x - r.al;
   float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
-  float cost = update_constraint<XG>(c, r, x, qs, fs, Ma, grad);
+  float cost = update_constraint<XG>(c, r, jr, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
   float Dinv = hessian_factor<XG>(c, r, true, 0, 0, 0, 0);
   STAMP(S_HESS0);
@@ -2137,7 +2187,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   while (live && it < cfg->iterations) {
     float Mv;
     STAMP(S_CHECK);
-    float alpha = line_search<XG>(c, r, search, Ma, fs, grad, Mv);
+    float alpha = line_search<XG>(c, r, jr, search, Ma, fs, grad, Mv);
     STAMP(S_LS);
     if (alpha == 0.f) break;
     x += alpha * search;
@@ -2151,7 +2201,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
        value, so the bits of separate tsum calls): cost, |grad|^2 and the active-set change */
     float red[3];
-    red[0] = update_constraint_lane<XG>(c, r, x, qs, fs, Ma, grad);
+    red[0] = update_constraint_lane<XG>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
     red[2] = (r.act != pa || r.actf != pf || r.actl != plo || (XG && r.x.act != pa2)) ? 1.f : 0.f;
     tsum_n<3>(red);
@@ -2191,9 +2241,13 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   EnvL* L = c.L;
   float x = w;
   if (c.l < 32) L->vec[V_TMP2][c.l] = qs;
-  float Ma = mul_m(c, x, V_TMP);
-  float jw = row_dot(c, r, V_TMP) - r.aref;
-  float js = row_dot(c, r, V_TMP2) - r.aref;
+  float jw, js;
+  /* the lane's contact-row Jacobian: constant through the solve, kept in registers */
+  float jr[CAP];
+  ld_row(&L->u.J[c.l][0], jr);
+  float Ma = mul_m_dot(c, r, jr, x, V_TMP, jw, V_TMP2, js);
+  jw -= r.aref;
+  js -= r.aref;
   float jwx = 0.f, jsx = 0.f;
   if (XG && r.x.any) {
     jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
@@ -2216,13 +2270,13 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   r.jl = r.sl * x - r.al;
   const float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
-  float cost = update_constraint<XG>(c, r, x, qs, fs, Ma, grad);
+  float cost = update_constraint<XG>(c, r, jr, x, qs, fs, Ma, grad);
   float mg = solve_ldl(c, grad, DinvM);
   float search = -mg;
   int it = 0;
   while (live && it < cfg->iterations) {
     float Mv;
-    const float alpha = line_search<XG>(c, r, search, Ma, fs, grad, Mv);
+    const float alpha = line_search<XG>(c, r, jr, search, Ma, fs, grad, Mv);
     if (alpha == 0.f) break;
     x += alpha * search;
     Ma += alpha * Mv;
@@ -2232,7 +2286,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
     float red[2];
-    red[0] = update_constraint_lane<XG>(c, r, x, qs, fs, Ma, grad);
+    red[0] = update_constraint_lane<XG>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
     tsum_n<2>(red);
     cost = red[0];
