@@ -337,9 +337,15 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
 constexpr int WM = 16;       /* envs per one-wave workgroup */
 constexpr int WLDA = WM + 1; /* row stride of the [unit][env] tile */
 
+/* wave priority of the slot-sized kernels, which share CUs with step waves in an actor-in-the-loop
+   rollout (diagnostic knob; 0 = the hardware default) */
+#ifndef ZB_POLWAVE_PRIO
+#define ZB_POLWAVE_PRIO 0
+#endif
 template <int KIN, int NOUT, bool ACTOR, int NWV>
 __global__ __launch_bounds__(64 * NWV, 2) void policy_wave_kernel(PolicyArgs a) {
 #pragma clang fp contract(off)
+  if constexpr (ZB_POLWAVE_PRIO > 0) __builtin_amdgcn_s_setprio(ZB_POLWAVE_PRIO);
   constexpr int KPAD = (KIN + 15) / 16 * 16;
   constexpr int GIN = KPAD / 16;
   constexpr int NTO = (NOUT + 15) / 16;

@@ -99,6 +99,14 @@ VARIANTS = {
     # an earlier product kernel (e.g. `git show HEAD:.../zb_policy.hip`): ZB_POL_OLD or variants/zb_policy_prev.hip
     "prev": "file:" + os.environ.get("ZB_POL_OLD", os.path.join(OUT, "zb_policy_prev.hip")),
     "base2": [],
+    # static priority for the second-dispatched half of the 8 waves (MI355X_MICROARCH.md, two waves
+    # per SIMD, item 4): waves 4-7 win VALU / matrix issue arbitration against their SIMD partners
+    "prio47": [("  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;\n",
+                "  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;\n"
+                "  if (__builtin_amdgcn_readfirstlane(w) >= NWAVE / 2) __builtin_amdgcn_s_setprio(1);\n")],
+    "prio03": [("  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;\n",
+                "  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;\n"
+                "  if (__builtin_amdgcn_readfirstlane(w) < NWAVE / 2) __builtin_amdgcn_s_setprio(1);\n")],
 }
 
 
@@ -123,7 +131,8 @@ def build():
                         f"-I{ROOT}/include", f"-I{CSRC}", "-fno-math-errno", "-c", "-o", obj, p], check=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                         os.path.join(OUT, f"libpol_{name}.so"), os.path.join(CSRC, "build", "zb_engine.o"),
-                        os.path.join(CSRC, "build", "zb_capi.o"), os.path.join(CSRC, "build", "zb_ppo.o"), obj],
+                        os.path.join(CSRC, "build", "zb_capi.o"), os.path.join(CSRC, "build", "zb_ppo.o"),
+                        os.path.join(CSRC, "build", "zb_host.o"), obj],
                        check=True)
         print("built", name)
 

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ksim-gym-zbot_amd"))
 import torch  # noqa: E402
 from zbot_amd import compile_model, default_config  # noqa: E402
-from zbot_amd.engine import HipEngine  # noqa: E402
+from zbot_amd.engine import EnvGroups, HipEngine  # noqa: E402
 
 
 def main():
@@ -20,11 +20,16 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--groups", type=int, default=1, help="env groups on their own streams (EnvGroups)")
     a = ap.parse_args()
     cm = compile_model()
     bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
     acts = [bias + 0.05 * torch.randn(a.n, 20, device="cuda") for _ in range(8)]
-    engs = [HipEngine(cm, default_config(), a.n, lib_path=os.path.abspath(p), seed=0) for p in a.libs]
+    if a.groups > 1:
+        engs = [EnvGroups(cm, default_config(), a.n, groups=a.groups, lib_path=os.path.abspath(p), seed=0)
+                for p in a.libs]
+    else:
+        engs = [HipEngine(cm, default_config(), a.n, lib_path=os.path.abspath(p), seed=0) for p in a.libs]
     for e in engs:
         e.reset()
         for t in range(3):
@@ -45,6 +50,8 @@ def main():
             t0 = time.perf_counter()
             for t in range(a.steps):
                 e.step(acts[t % 8], extras=False)
+            if a.groups > 1:
+                e.join()
             torch.cuda.synchronize()
             res[p].append(a.n * a.steps / (time.perf_counter() - t0))
     for p in a.libs:
