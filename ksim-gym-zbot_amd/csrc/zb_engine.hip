@@ -1340,10 +1340,7 @@ __device__ __forceinline__ float row_dot_x(const Ctx& c, const Rows& r, int slot
   return row_dot(c, (const gfloat_t*)xrows(c.L) + c.l * CAP, r.x.chd, slot);
 }
 
-/* y = M x (mul_m) and, in the same LDS round trip, the lane's contact-row products with x
- * (jv, row_dot over vec[slot]) and, when slot2 >= 0, with vec[slot2] (jv2, published before the
- * call): the row loads go out with mul_m's ancestor gather instead of after its reduction and
- * exchange point. Bit-identical to mul_m followed by row_dot. */
+/* row_dot with the lane's row already in registers (jr) */
 __device__ __forceinline__ float row_dot_pre(const Ctx& c, const float jr[CAP], int chd, int slot) {
   float vv[CAP];
 #pragma unroll
@@ -1353,6 +1350,11 @@ __device__ __forceinline__ float row_dot_pre(const Ctx& c, const float jr[CAP], 
   for (int e = 0; e < CAP; e++) v += jr[e] * vv[e];
   return v;
 }
+/* y = M x (mul_m) and, in the same LDS round trip, the lane's contact-row products with x
+ * (jv, row_dot over vec[slot]) and, when slot2 >= 0, with vec[slot2] (jv2, published before the
+ * call): the row loads go out with mul_m's ancestor gather instead of after its reduction and
+ * exchange point. jr: the lane's contact-row Jacobian, loaded once per solve. Bit-identical to
+ * mul_m followed by row_dot. */
 __device__ __forceinline__ float mul_m_dot(const Ctx& c, const Rows& r, const float jr[CAP], float x, int slot, float& jv,
                                            int slot2, float& jv2) {
   EnvL* L = c.L;
@@ -1758,7 +1760,8 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
    and their VALU issue is arbitrated by priority, then age. The solver is a chain of short dependent
    steps (line-search evaluations, exchanges, pivots), the smooth phase around it is denser in
    independent instructions: a wave inside its solver takes precedence over a partner outside it,
-   whose work absorbs the delay (+3 % at C2). Results are unchanged. */
+   whose work absorbs the delay (C2: +3 % on one stream, +0.6 % with two env groups; DESIGN.md §4d
+   round 3). Results are unchanged. */
 #ifndef ZB_SOLVER_PRIO
 #define ZB_SOLVER_PRIO 1
 #endif
