@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--push", action="store_true")
     ap.add_argument("--randomize", action="store_true")
     ap.add_argument("--solver", default="newton")
+    ap.add_argument("--tol", type=float, default=None, help="solver tolerance of the GPU and fp32 oracle runs")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -27,6 +28,8 @@ def main():
     O.build()
     cm = compile_model()
     cfg = default_config(push=a.push, randomize=a.randomize, solver=a.solver)
+    if a.tol is not None:
+        cfg.tolerance = a.tol
     n = 64
     env = O.OracleEnv(cm.cmodel, cfg, n, seed=7)
     env.reset()
