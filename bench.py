@@ -48,13 +48,16 @@ def host_cpu() -> dict:
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": model}
 
 
-def baseline_threads() -> int:
-    """OpenMP threads of the CPU twin: every CPU this process may run on (sched_getaffinity), unless
-    the host caps the job's CPU share through OMP_NUM_THREADS (the GPU box sets it to its
-    per-GPU share of 16 and asks jobs to keep it)."""
+def baseline_threads() -> tuple[int, str]:
+    """OpenMP threads of the CPU twin and where that number came from: every CPU this process may
+    run on (sched_getaffinity), unless the host caps the job's CPU share through OMP_NUM_THREADS
+    (the GPU box sets it to its per-GPU share of 16 and asks jobs to keep it)."""
     aff = len(os.sched_getaffinity(0))
-    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return max(1, min(aff, cap) if cap > 0 else aff)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    cap = int(env or 0)
+    if 0 < cap < aff:
+        return cap, f"OMP_NUM_THREADS={env} (the host's per-job CPU share, of {aff} CPUs in the affinity mask)"
+    return max(1, aff), f"sched_getaffinity: all {aff} CPUs this process may run on"
 
 
 def _time_twin(O, cm, cfg, n_envs: int, budget_s: float, max_steps: int, min_steps: int = 2):
@@ -78,7 +81,7 @@ def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int, max_steps
     sample of the headline workload: the same env count, as many env-steps as fit in budget_s
     (max_steps > 0: exactly that many, the C1 rollout). With c1_leg, the reference's own
     CPU-runnable case (C1: 64 envs x 128 env-steps) is timed beside it."""
-    threads = baseline_threads()
+    threads, cap_src = baseline_threads()
     os.environ["OMP_NUM_THREADS"] = str(threads)  # read by the OpenMP runtime at the oracle's first load
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # noqa: PLC0415  (cpu_baseline leg: the oracle is the CPU twin being timed)
@@ -92,12 +95,15 @@ def cpu_baseline(cm, cfg, budget_s: float, workload: str, n_envs: int, max_steps
         "sample": f"{n_envs} envs x {steps} env-steps of the same workload ({workload}) on the CPU twin "
                   f"(oracle/zb_oracle.c, fp32, OpenMP {threads} threads), {el:.1f} s",
         "envs": n_envs,
+        "threads_cap": cap_src,
+        "per_core": n_envs * steps / el / threads,
+        "per_core_unit": "env-steps/s per thread (one thread per core)",
         "host": host_cpu(),
     }
     if c1_leg:
         s1, e1 = _time_twin(O, cm, cfg, 64, 0.0, 128)
         out["c1"] = {"value": 64 * s1 / e1, "unit": "env-steps/s", "sample": f"64 envs x {s1} env-steps (C1), "
-                     f"{e1:.2f} s", "cores": threads}
+                     f"{e1:.2f} s", "cores": threads, "per_core": 64 * s1 / e1 / threads}
     return out
 
 
@@ -234,6 +240,123 @@ def bench_c2_rollout(eng, n: int, T: int, dev, rank: int, world: int, sigma: flo
         "ms_per_rollout": 1e3 * wall,
         "rollout_steps": T,
         "episodes_done": ends,
+    }
+
+
+def _timed_steps(step, steps: int, warmup: int, dev, world: int) -> float:
+    """Wall seconds of `steps` calls of step(t) after `warmup` untimed ones, bracketed by
+    synchronize (+ barrier when distributed), max over ranks."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+
+    for t in range(warmup):
+        step(t)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for t in range(steps):
+        step(warmup + t)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    return float(wall.item())
+
+
+def _synthetic_actions(n: int, T: int, dev, seed: int, sigma: float):
+    import torch  # noqa: PLC0415
+    from zbot_amd import cstructs as cs  # noqa: PLC0415
+    from zbot_amd.constants import JOINT_BIASES  # noqa: PLC0415
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    bias = torch.tensor([b for _, b, _ in JOINT_BIASES], device=dev)
+    return bias + sigma * torch.randn(T, n, cs.NJ, device=dev, generator=g)
+
+
+def bench_ksim_env(cm, n: int, steps: int, warmup: int, dev, rank: int, world: int, seed: int) -> dict:
+    """The headline workload driven through the ksim-shaped API (zbot_amd.task.ZbotWalkingEnv.step,
+    train.py's ZbotWalkingTask): its default env groups (two from 4096 envs up), every output a
+    StepResult (observations incl. the extra ones, reward terms), curriculum level passed per
+    step. The loop does not read the results, as an open-loop rollout does not, so the groups are
+    never joined between steps."""
+    from zbot_amd.task import ZbotWalkingEnv  # noqa: PLC0415
+
+    env = ZbotWalkingEnv(n, seed=seed, device=dev.index, env_offset=rank * n, model=cm)
+    acts = _synthetic_actions(n, 64, dev, 1234 + rank, 0.05)
+    env.reset()
+    wall = _timed_steps(lambda t: env.step(acts[t % 64]), steps, warmup, dev, world)
+    return {
+        "workload": f"C2 through ZbotWalkingEnv.step: {n} envs/GPU, {env.groups} env groups, {steps} timed steps "
+                    f"(after {warmup}), every StepResult output written (obs_extra and reward terms included)",
+        "env_steps_per_s": world * n * steps / wall,
+        "ms_per_step": 1e3 * wall / steps,
+        "groups": env.groups,
+    }
+
+
+def bench_train_defaults(cm, dev, rank: int, world: int, seed: int, n: int = 512, T: int = 200) -> dict:
+    """train.py's own training size (train.py:1770 num_envs=512, :1775 rollout_length_seconds 4.0 at
+    ctrl_dt 0.02 = 200 steps): one 200-step rollout of 512 envs per GPU from reset through
+    ZbotWalkingEnv (one handle below 4096 envs), [T, n] reward / done rows, FeetAirtime row 0
+    patched; actions JOINT_BIASES + 0.2 N(0,1). Latency-bound: 512 envs are 256 waves on 1024
+    SIMDs."""
+    import torch  # noqa: PLC0415
+    from zbot_amd.task import ZbotWalkingEnv  # noqa: PLC0415
+
+    env = ZbotWalkingEnv(n, seed=seed, device=dev.index, env_offset=rank * n, model=cm)
+    eng = env.engine
+    acts = _synthetic_actions(n, T, dev, 777 + rank, 0.2)
+    rew = torch.empty(T, n, device=dev)
+    done = torch.empty(T, n, dtype=torch.uint8, device=dev)
+
+    def rollout(_):
+        eng.mark_rollout_start()
+        for t in range(T):
+            eng.step(acts[t], curriculum=env.curriculum_level, reward=rew[t], done=done[t])
+        eng.feet_airtime_exact(rew[0], None, curriculum=env.curriculum_level)
+
+    env.reset()
+    wall = _timed_steps(rollout, 2, 1, dev, world)
+    assert bool(torch.isfinite(rew).all())
+    return {
+        "workload": f"train.py defaults: {n} envs/GPU x {T}-step rollout (train.py:1770,1775), one handle, automatic "
+                    "resets inside, [T, n] reward / done rows, FeetAirtime row 0 patched; 2 timed rollouts after 1",
+        "env_steps_per_s": world * n * T * 2 / wall,
+        "ms_per_rollout": 1e3 * wall / 2,
+        "ms_per_step": 1e3 * wall / (2 * T),
+        "episodes_done": int(done.sum().item()),
+    }
+
+
+def bench_general_colliders(cfg, n: int, steps: int, warmup: int, dev, rank: int, world: int, seed: int,
+                            groups: int) -> dict:
+    """C2 on the limbs model (assets/zbot_like_limbs.xml: shin boxes and hand capsules collide with
+    the floor besides the soles), which runs the general-collider kernel instantiation (DESIGN.md
+    §4j); same groups and actions as the headline."""
+    from zbot_amd import compile_model  # noqa: PLC0415
+    from zbot_amd.engine import EnvGroups, HipEngine  # noqa: PLC0415
+    from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
+
+    path = os.path.join(ROOT, "ksim-gym-zbot_amd", "assets", "zbot_like_limbs.xml")
+    cm = compile_model(load_mjcf(path))
+    if groups > 1:
+        eng = EnvGroups(cm, cfg, n, groups=groups, env_offset=rank * n, device=dev.index, seed=seed)
+    else:
+        eng = HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=seed)
+    acts = _synthetic_actions(n, 64, dev, 1234 + rank, 0.05)
+    eng.reset()
+
+    wall = _timed_steps(lambda t: eng.step(acts[t % 64], extras=False), steps, warmup, dev, world)
+    eng.check()
+    return {
+        "workload": f"C2 on the limbs model ({os.path.relpath(path, ROOT)}: {len(cm.geom_names)} floor colliders "
+                    f"{cm.geom_names}), {n} envs/GPU, {groups} env groups, {steps} timed steps (after {warmup})",
+        "env_steps_per_s": world * n * steps / wall,
+        "ms_per_step": 1e3 * wall / steps,
     }
 
 
@@ -393,6 +516,9 @@ def main() -> None:
     ap.add_argument("--no-pipeline", action="store_true", help="skip the end-to-end rollout-pipeline leg")
     ap.add_argument("--no-c2-rollout", action="store_true",
                     help="skip the C2-as-stated leg (one 256-step rollout with resets inside, timed whole)")
+    ap.add_argument("--no-extra-legs", action="store_true",
+                    help="skip the ksim_env (ZbotWalkingEnv.step), train_defaults (512 x 200) and general_colliders "
+                         "(limbs model) legs")
     ap.add_argument("--inloop-critic", type=int, default=0,
                     help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
                          "(1 one-wave, 2 two-wave, 3 four-wave; DESIGN.md §4f); 0 = the 8-wave critic afterwards")
@@ -473,6 +599,13 @@ def main() -> None:
     policy_leg = None if args.no_policy else bench_policy_in_loop(eng1, n, 48, dev, rank, engp)
     pipe_leg = None if args.no_pipeline else bench_rollout_pipeline(engp or eng1, n, 32, 2, dev, world,
                                                                      args.inloop_critic)
+
+    extra_legs = {}
+    if not args.no_extra_legs and args.config == "c2" and args.model is None:
+        extra_legs["ksim_env"] = bench_ksim_env(cm, n, args.steps, args.warmup, dev, rank, world, args.seed)
+        extra_legs["train_defaults"] = bench_train_defaults(cm, dev, rank, world, args.seed)
+        extra_legs["general_colliders"] = bench_general_colliders(cfg, n, args.steps, args.warmup, dev, rank, world,
+                                                                  args.seed, G)
 
     eng.reset()
     for t in range(args.warmup):
@@ -627,6 +760,9 @@ def main() -> None:
             out["policy_in_loop"] = policy_leg
         if pipe_leg is not None:
             out["rollout_pipeline"] = pipe_leg
+        for k, leg in extra_legs.items():
+            leg["vs_headline"] = leg["env_steps_per_s"] / value
+            out[k] = leg
         if world == 1 and not args.no_cpu_baseline:
             if args.config == "c1":  # the whole C1 rollout on the CPU twin: 64 envs x 128 env-steps
                 out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, "C1", n_envs=n, max_steps=128,

@@ -205,6 +205,9 @@ class HipEngine:
                                  _ptr(self.done), _ptr(self.success), float(curriculum), self._stream()))
         return self.outputs()
 
+    def join(self) -> None:
+        """Nothing to join: one handle runs on the caller's current stream (EnvGroups.join's twin)."""
+
     def mark_rollout_start(self) -> None:
         """The next step() / rollout() is step 0 of a rollout (zb_mark_rollout_start): it saves what
         feet_airtime_exact() needs to give ksim's FeetAirtime row 0."""

@@ -23,7 +23,7 @@ from . import cstructs as cs
 from .config import default_config
 from .constants import JOINT_BIASES, REWARDS
 from .curriculum import EpisodeLengthCurriculum, rollout_episode_length
-from .engine import HipEngine
+from .engine import EnvGroups, HipEngine
 from .model import compile_model
 
 # obs_critic layout (train.py:1664-1679)
@@ -82,15 +82,41 @@ def observation_dict(out: dict) -> dict:
     return obs
 
 
-@dataclass
 class StepResult:
-    obs: dict
-    actor_inputs: object
-    critic_inputs: object
-    reward: object
-    reward_terms: dict
-    done: object
-    success: object = None  # time-limit ends without a failure (ksim successes_t)
+    """One step's outputs under ksim's names (views into the engine's output buffers).
+
+    With env groups (ZbotWalkingEnv(groups=G > 1)) the buffers are still being written on the group
+    streams when step() returns. The first read of any field makes the caller's current stream wait
+    for every group (EnvGroups.join; no host synchronisation), so a loop that only steps, as an
+    open-loop rollout does, never serialises the groups, and a loop that reads the outputs sees
+    them complete."""
+
+    FIELDS = ("obs", "actor_inputs", "critic_inputs", "reward", "reward_terms", "done", "success")
+
+    def __init__(self, obs, actor_inputs, critic_inputs, reward, reward_terms, done, success=None, join=None):
+        self._v = dict(obs=obs, actor_inputs=actor_inputs, critic_inputs=critic_inputs, reward=reward,
+                       reward_terms=reward_terms, done=done, success=success)
+        self._join = join
+
+    def _get(self, k):
+        if self._join is not None:
+            self._join()
+            self._join = None
+        return self._v[k]
+
+    obs = property(lambda self: self._get("obs"))
+    actor_inputs = property(lambda self: self._get("actor_inputs"))
+    critic_inputs = property(lambda self: self._get("critic_inputs"))
+    reward = property(lambda self: self._get("reward"))
+    reward_terms = property(lambda self: self._get("reward_terms"))
+    done = property(lambda self: self._get("done"))
+    success = property(lambda self: self._get("success"))  # time-limit ends without a failure (ksim successes_t)
+
+
+def default_groups(num_envs: int) -> int:
+    """Env groups of ZbotWalkingEnv: two from 4096 envs up (one step-kernel round per group fills the
+    other's drain), else one handle."""
+    return 2 if num_envs >= 4096 else 1
 
 
 class ZbotWalkingEnv:
@@ -99,22 +125,37 @@ class ZbotWalkingEnv:
     `num_envs`, `dt`, `ctrl_dt`, `iterations`, `ls_iterations` default to
     train.py:1768-1781 (512 envs, 0.001, 0.02, 8, 8).
 
+    `groups`: env groups, each a handle stepping on its own HIP stream (zbot_amd.EnvGroups,
+    DESIGN.md §4f); the default is two from 4096 envs up. Results are the same bits for every
+    group count; StepResult fields join the groups when first read.
+
     `curriculum` is ksim's EpisodeLengthCurriculum of get_curriculum (train.py:1595-1602);
-    `curriculum_level` starts at its initial level and moves when update_curriculum() is called
-    once per rollout (a training step). Assigning `curriculum_level` directly overrides it.
+    `curriculum_level` starts at its initial level (0.5, the curriculum's floor) and moves when
+    update_curriculum() is called once per rollout (a training step). Assigning
+    `curriculum_level` directly overrides it.
     """
 
     def __init__(self, num_envs: int = 512, *, seed: int = 0, device: int = 0, env_offset: int = 0,
                  push: bool = False, randomize: bool = False, obs_noise: bool = True, model=None,
-                 curriculum: EpisodeLengthCurriculum | None = None, **cfg_kw):
+                 curriculum: EpisodeLengthCurriculum | None = None, groups: int | None = None, **cfg_kw):
         self.model = model or compile_model()
         self.cfg = default_config(push=push, randomize=randomize, obs_noise=obs_noise, **cfg_kw)
-        self.engine = HipEngine(self.model, self.cfg, num_envs, env_offset=env_offset, device=device, seed=seed)
+        self.groups = default_groups(num_envs) if groups is None else int(groups)
+        if self.groups > 1:
+            self.engine = EnvGroups(self.model, self.cfg, num_envs, groups=self.groups, env_offset=env_offset,
+                                    device=device, seed=seed)
+        else:
+            self.engine = HipEngine(self.model, self.cfg, num_envs, env_offset=env_offset, device=device, seed=seed)
         self.num_envs = num_envs
         self.curriculum = curriculum or EpisodeLengthCurriculum()
         self.curriculum_state = self.curriculum.initial_state()
         self.curriculum_level = self.curriculum_state.level
         self._last_done = None
+
+    def join(self) -> None:
+        """Make the caller's current stream wait for every group's enqueued steps (a no-op with one
+        handle). StepResult does this on its first read."""
+        self.engine.join()
 
     def _result(self, out: dict, with_reward: bool) -> StepResult:
         terms = {}
@@ -129,6 +170,7 @@ class ZbotWalkingEnv:
             reward_terms=terms,
             done=out["done"] if with_reward else None,
             success=out["success"] if with_reward else None,
+            join=self.engine.join if self.groups > 1 else None,
         )
 
     def reset(self, mask=None) -> StepResult:
@@ -151,6 +193,7 @@ class ZbotWalkingEnv:
         """Patch the rollout's row 0 (its reward [n] / reward terms [n, 12] buffers, as recorded from
         the first step() after begin_rollout) to ksim's FeetAirtimeReward (train.py:515-546)."""
         self.engine.feet_airtime_exact(reward0, terms0, curriculum=self.curriculum_level)
+        self.engine.join()  # the patched row is read on the caller's stream next
 
     def update_curriculum(self) -> float:
         """EpisodeLengthCurriculum update after a rollout (train.py:1595-1602; zbot_amd.curriculum):
@@ -158,6 +201,7 @@ class ZbotWalkingEnv:
         (RCCL all_gather when distributed), then the level law. Returns the new level."""
         if self._last_done is None:
             raise RuntimeError("update_curriculum() needs a rollout: step() first")
+        self.engine.join()
         length = rollout_episode_length(self.engine.get_stats(), self.engine.get_state(), self._last_done,
                                         self.cfg.ctrl_dt)
         self.curriculum_state = self.curriculum.update(self.curriculum_state, length)

@@ -3,9 +3,9 @@
     python tests/golden/make_golden.py
 
 The reference (JAX/MJX/ksim) cannot run in this container, so
-the fixtures pin the build's own oracle: a C1-shaped rollout (32 envs x 16
-env-steps, seed 0, default train.py configuration incl. observation noise) and
-a domain-randomized + push variant (configs 3/5 features). Tests re-run the
+the fixtures pin the build's own oracle: BASELINE's C1 rollout (64 envs x 128
+env-steps, seed 0, default train.py configuration incl. observation noise), a
+domain-randomized + push variant (configs 3/5 features) and a CG-solver case. Tests re-run the
 oracle against them (regression pin) and compare the HIP engine to them.
 """
 
@@ -23,7 +23,8 @@ import oracle as O  # noqa: E402
 from zbot_amd import compile_model, default_config  # noqa: E402
 
 CASES = {
-    "c1_seed0": dict(n=32, steps=16, seed=0, push=False, randomize=False, std=0.05),
+    # BASELINE.json configs[0]: 64 parallel envs, 128-step rollout (round 4: was 32 x 16)
+    "c1_64x128_seed0": dict(n=64, steps=128, seed=0, push=False, randomize=False, std=0.05),
     "c5_push_seed1": dict(n=16, steps=16, seed=1, push=True, randomize=True, std=0.1),
     # round 3: the CG solver variant (ZbEnvConfig.solver)
     "c2_cg_seed2": dict(n=16, steps=16, seed=2, push=False, randomize=False, std=0.05, solver="cg"),

@@ -68,9 +68,12 @@ class MaxErr:
     lands further away (that env: 2.8x the qpos bound, 6.3x the planner bound); the budget admits
     one such env per output and step, within 10x the bound."""
 
-    def __init__(self, name, budget=1, loose=10.0):
+    def __init__(self, name, budget=1, loose=10.0, max_ill=3):
         self.name, self.err, self.bad, self.err_well = name, {}, [], {}
         self.budget, self.loose, self.nout = budget, loose, {}
+        # envs per output and step that may take the discontinuity slack (measured 0-3 of 64 in r03)
+        self.max_ill = max_ill
+        self.over = set()  # envs over the bound in the last add() calls (cleared by take_over())
 
     def add(self, key, got, ref, tol, rtol=0.0, ref64=None):
         """Record |got - ref| against tol + rtol |ref| elementwise (rows = envs; asserted in
@@ -87,6 +90,9 @@ class MaxErr:
             slack = 2.0 * gap.reshape(gap.shape[0], -1).max(1).reshape((-1,) + (1,) * (gap.ndim - 1))
             ill = np.asarray(slack).reshape(-1) > tol
             self.ill = max(getattr(self, "ill", 0), int(ill.sum()))
+            if int(ill.sum()) > self.max_ill:
+                self.bad.append(f"{key}: {int(ill.sum())} envs at a discontinuity (fp32 / fp64 oracles disagree by "
+                                f"more than {tol:.1e}), more than the {self.max_ill} the contract allows")
             if d.size and (~ill).any():
                 self.err_well[key] = max(self.err_well.get(key, 0.0), float(d[~ill].max()))
         e = float(d.max()) if d.size else 0.0
@@ -96,11 +102,17 @@ class MaxErr:
         excess = d - rtol * np.abs(ref) - slack
         rows = excess.reshape(excess.shape[0], -1).max(1) if excess.ndim > 1 else excess
         n_over = int((rows > tol).sum())
+        self.over |= set(np.nonzero(rows > tol)[0].tolist())
         self.nout[key] = max(self.nout.get(key, 0), n_over)
         worst = float(rows.max())
         if n_over > self.budget or not worst <= self.loose * tol:
             self.bad.append(f"{key} max error {e:.3e}: {n_over} envs over {tol:.1e} + {rtol:.0e} |ref| "
                             f"(budget {self.budget}), worst excess {worst:.3e} (limit {self.loose * tol:.1e})")
+
+    def take_over(self) -> list:
+        """Envs over the bound since the last call (the budget's users), sorted."""
+        out, self.over = sorted(self.over), set()
+        return out
 
     def report(self):
         print(f"\n[{self.name}] max |error|: " + ", ".join(f"{k} {v:.2e}" for k, v in self.err.items()))
@@ -216,7 +228,23 @@ def oracle_steps(O, cm, cfg, env, a, seed):
     e64.rand[:] = env.rand
     r64 = e64.step(a)
     ref = env.step(a)
-    return ref, {k: want for k, _, want in one_step_outputs(e64.state, r64, e64.state, r64)}
+    ref64 = {k: want for k, _, want in one_step_outputs(e64.state, r64, e64.state, r64)}
+    ref64["_iters"] = e64.iters.copy()
+    return ref, ref64
+
+
+def print_budget_envs(err, t, eng, env, ref64, gs):
+    """Name the solver exit iteration of every env that used the budget: the engine's and the fp32 /
+    fp64 oracles' total solver iterations over the step, and the env's fp32-fp64 oracle gap."""
+    envs = err.take_over()
+    if not envs:
+        return
+    gi = eng.solver_iters().cpu().numpy()
+    for e in envs:
+        gap = float(np.abs(env.state[e, :27] - ref64["qpos"][e]).max())
+        print(f"[{err.name}] step {t} env {e} over the bound: solver iterations engine {int(gi[e])}, "
+              f"oracle f32 {int(env.iters[e])}, f64 {int(ref64['_iters'][e])}; fp32/fp64 oracle qpos gap {gap:.2e}, "
+              f"qpos error {float(np.abs(gs[e, :27] - env.state[e, :27]).max()):.2e}")
 
 
 @pytest.mark.parametrize("solver", ["newton", "cg"])
@@ -240,10 +268,41 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize, solver)
         tol = ONE_STEP_TOL_CG if solver == "cg" else ONE_STEP_TOL
         for key, got, want in one_step_outputs(gs, out, env.state, ref):
             err.add(key, got, want, *tol[key], ref64=ref64[key])
+        print_budget_envs(err, t, eng, env, ref64, gs)
         # integer bookkeeping is exact
         for w in (cs.S_EP_STEPS, cs.S_RNG_STEP, cs.S_EPISODE):
             assert np.array_equal(gs[:, w].view(np.uint32), env.state[:, w].view(np.uint32))
     err.report()
+
+
+def test_one_step_parity_without_early_exit(torch_gpu, cmodel, oracle_mod):
+    """The cause of the one-step budget, shown: with the solver's early exit off (tolerance 0: every
+    substep runs train.py's 8 Newton iterations unless the cost rises), engine and fp32 oracle no
+    longer leave the loop at different iterations, and the randomized cases hold every bound with
+    NO exception (budget 0). At the default tolerance the same state gave one env 2.8x / 6.3x / 5.2x
+    over the qpos / planner / reward bounds (r04 v1: engine 55 vs oracle 56 iterations), at
+    tolerance 0 its error is 1.2e-7 (profiles/r04_v1_diag_rand_tol0.log)."""
+    torch = torch_gpu
+    for push in (False, True):
+        cfg = default_config(push=push, randomize=True)
+        cfg.tolerance = 0.0
+        n = 64
+        env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
+        eng = engine(cmodel, cfg, n, seed=7)
+        err = MaxErr(f"one-step newton tolerance 0 push={push} randomize=True", budget=0, loose=1.0)
+        for t in range(3):
+            eng.set_state(torch.from_numpy(env.state.copy()))
+            eng.set_rand(torch.from_numpy(env.rand.copy()))
+            a = oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100 + t)
+            ref, ref64 = oracle_steps(oracle_mod, cmodel, cfg, env, a, 7)
+            out = eng.step(torch.from_numpy(a).cuda())
+            torch.cuda.synchronize()
+            gs = eng.get_state().cpu().numpy()
+            np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
+            for key, got, want in one_step_outputs(gs, out, env.state, ref):
+                err.add(key, got, want, *ONE_STEP_TOL[key], ref64=ref64[key])
+            print_budget_envs(err, t, eng, env, ref64, gs)
+        err.report()
 
 
 # Multi-step rollouts from the same reset (contact dynamics are chaotic): the first 8 rewards and
@@ -254,7 +313,37 @@ GOLDEN_TOL = {"reward": 1e-5, "final_base_pos": 1e-5}
 GOLDEN_TOL_CG = {"reward": 5e-3, "final_base_pos": 2e-3}
 
 
-@pytest.mark.parametrize("name", ["c1_seed0", "c5_push_seed1", "c2_cg_seed2"])
+# Steps of a golden rollout over which done flags and the final state are compared exactly / to the
+# bound; past them (C1: 128 steps) the trajectories in contact separate chaotically and the
+# ensemble statistics are compared instead (golden_ensemble_check).
+GOLDEN_EXACT_STEPS = 16
+
+
+def golden_ensemble_check(name, rew, done, final_state, g, k=5.0):
+    """Ensemble contract of a long golden rollout (BASELINE C1: 64 envs x 128 steps), engine vs
+    the oracle fixture, from the same reset and actions: the per-step ensemble mean reward within
+    k standard errors at every step, the rollout's mean reward within k standard errors of the
+    per-env time averages, the episode-end count within 3 + 2 sqrt(count), the final mean base
+    height within k standard errors. Prints the measured values."""
+    n = rew.shape[1]
+    ref_r = g["reward"].astype(np.float64)
+    se_t = np.maximum(ref_r.std(1) / np.sqrt(n), 1e-6)
+    dev_t = np.abs(rew.mean(1) - ref_r.mean(1))
+    se_all = ref_r.mean(0).std() / np.sqrt(n)
+    d_all = abs(float(rew.mean()) - float(ref_r.mean()))
+    ends, ends_ref = int(done.sum()), int(g["done"].sum())
+    z, z_ref = final_state[:, 2].astype(np.float64), g["final_state"][:, 2].astype(np.float64)
+    se_z = max(z_ref.std() / np.sqrt(n), 1e-6)
+    print(f"\n[golden {name} ensemble] mean reward {rew.mean():.6f} vs {ref_r.mean():.6f} ({d_all / se_all:.2f} SE); "
+          f"worst step {int(dev_t.argmax())}: {float((dev_t / se_t).max()):.2f} SE; episode ends {ends} vs {ends_ref}; "
+          f"final base height {z.mean():.6f} vs {z_ref.mean():.6f} ({abs(z.mean() - z_ref.mean()) / se_z:.2f} SE)")
+    assert (dev_t <= k * se_t).all(), f"step ensemble mean reward off by {float((dev_t / se_t).max()):.2f} SE"
+    assert d_all <= k * se_all
+    assert abs(ends - ends_ref) <= 3 + 2 * np.sqrt(ends_ref)
+    assert abs(z.mean() - z_ref.mean()) <= k * se_z
+
+
+@pytest.mark.parametrize("name", ["c1_64x128_seed0", "c5_push_seed1", "c2_cg_seed2"])
 def test_golden_rollout(torch_gpu, cmodel, name):
     torch = torch_gpu
     g = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
@@ -272,13 +361,17 @@ def test_golden_rollout(torch_gpu, cmodel, name):
         rew.append(o["reward"].cpu().numpy().copy())
         done.append(o["done"].cpu().numpy().copy())
     rew, done = np.stack(rew), np.stack(done)
-    np.testing.assert_array_equal(done, g["done"])
+    ex = min(steps, GOLDEN_EXACT_STEPS)
+    np.testing.assert_array_equal(done[:ex], g["done"][:ex])
     err = MaxErr(f"golden {name}")
     tol = GOLDEN_TOL_CG if solver == "cg" else GOLDEN_TOL
     for t in range(8):
         err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"])
     gs = eng.get_state().cpu().numpy()
-    err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], tol["final_base_pos"])
+    if steps <= GOLDEN_EXACT_STEPS:
+        err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], tol["final_base_pos"])
+    else:
+        golden_ensemble_check(name, rew, done, gs, g)
     err.add("final_rand", eng.get_rand().cpu().numpy(), g["final_rand"], 1e-6)
     err.report()
 
