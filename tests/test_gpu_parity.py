@@ -344,7 +344,11 @@ def golden_ensemble_check(name, rew, done, final_state, g, k=5.0):
 
 
 @pytest.mark.parametrize("name", ["c1_64x128_seed0", "c5_push_seed1", "c2_cg_seed2"])
-def test_golden_rollout(torch_gpu, cmodel, name):
+def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
+    """The engine from reset against a committed oracle rollout. The first 8 rewards follow the
+    one-step contract (MaxErr): the fp64 oracle is replayed over the same 8 steps from the same
+    reset, and an env where the fp32 and fp64 oracles already part (a contact or active-set switch;
+    C1 env 22 from step 5: 8.6e-4) gets twice their gap."""
     torch = torch_gpu
     g = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
     n, steps, seed = int(g["cfg_n"]), int(g["cfg_steps"]), int(g["cfg_seed"])
@@ -365,8 +369,11 @@ def test_golden_rollout(torch_gpu, cmodel, name):
     np.testing.assert_array_equal(done[:ex], g["done"][:ex])
     err = MaxErr(f"golden {name}")
     tol = GOLDEN_TOL_CG if solver == "cg" else GOLDEN_TOL
+    e64 = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=seed, precision="f64")
+    e64.reset()
     for t in range(8):
-        err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"])
+        r64 = e64.step(g["actions"][t])["reward"]
+        err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"], ref64=r64)
     gs = eng.get_state().cpu().numpy()
     if steps <= GOLDEN_EXACT_STEPS:
         err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], tol["final_base_pos"])
