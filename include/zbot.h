@@ -141,7 +141,9 @@ int zb_rollout(ZbHandle* h, const float* actions, int n_steps,
  * which adds scale·(ksim term − causal term) to reward0[e] and writes ksim's
  * term into reward_terms0[e][ZB_T_FEET_AIRTIME] (either pointer nullable;
  * reward0 may be zb_rollout's reward_sum, the patch is additive). Rows t ≥ 1
- * are untouched. curriculum_level is the level the first step ran at.
+ * are untouched. The handle's episode statistics get the same delta in their
+ * reward sum (ZB_ST_REWARD, zb_get_stats); episode returns (ZB_ST_RETURN) keep
+ * the causal row-0 term, as an episode can span the rollout boundary. curriculum_level is the level the first step ran at.
  * ZB_EARG if no marked step ran since the mark (or the rollout was already
  * patched). Added in ABI version 3.
  */

@@ -3344,10 +3344,16 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   }
 }
 
-int step_resident_blocks(int device, int xg) {
+int step_resident_blocks(int device, int xg, int solver) {
   int per_cu = 0, cus = 0;
-  const hipError_t e = xg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, true>, 64, 0)
-                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, false>, 64, 0);
+  /* the instantiation the handle launches: CG and Newton differ in registers and LDS */
+  hipError_t e;
+  if (solver == ZB_SOLVER_CG)
+    e = xg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_CG, true>, 64, 0)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_CG, false>, 64, 0);
+  else
+    e = xg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, true>, 64, 0)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, false>, 64, 0);
   if (e != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
   return per_cu * cus;
@@ -3386,9 +3392,12 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
    airtime after the trajectory's last step. The first step of a marked rollout saved c_0 and its
    causal term in the state row (ZB_S_AIR0_*); the state row now holds air[T-1]. One lane per env:
    term0 = Σ_feet c_0 · (air[T-1] - penalty), added to reward0 as scale · (term0 - causal0) and
-   written over reward_terms0's FeetAirtime slot. */
+   written over reward_terms0's FeetAirtime slot. The episode statistics' reward sum (ZB_ST_REWARD)
+   gets the same delta, so it stays the sum of the rollout's patched rows; episode returns
+   (ZB_ST_RETURN, the state row's running return) keep the causal row 0 (include/zbot.h). */
 __global__ __launch_bounds__(256) void airtime_exact_kernel(const float* __restrict__ state, const ZbEnvConfig* cfg,
-                                                            int n, float curriculum, float* reward0, float* terms0) {
+                                                            int n, float curriculum, float* reward0, float* terms0,
+                                                            float* stats) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const float* st = state + (size_t)e * ZB_STATE_STRIDE;
@@ -3399,15 +3408,17 @@ __global__ __launch_bounds__(256) void airtime_exact_kernel(const float* __restr
   term += (st[ZB_S_AIRTIME] - pen) * ((bits & 1u) ? 1.f : 0.f);
   term += (st[ZB_S_AIRTIME + 1] - pen) * ((bits & 2u) ? 1.f : 0.f);
   const float sc = cfg->reward_scale[ZB_T_FEET_AIRTIME] * (cfg->reward_by_curriculum[ZB_T_FEET_AIRTIME] ? curriculum : 1.f);
-  if (reward0) reward0[e] += sc * (term - causal);
+  const float delta = sc * (term - causal);
+  if (reward0) reward0[e] += delta;
   if (terms0) terms0[(size_t)e * ZB_NUM_TERMS + ZB_T_FEET_AIRTIME] = term;
+  if (stats) stats[(size_t)e * ZB_NUM_STATS + ZB_ST_REWARD] += delta;
 }
 
 hipError_t launch_airtime_exact(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((unsigned)((a.n_envs + 255) / 256)), block(256);
   hipLaunchKernelGGL(airtime_exact_kernel, grid, block, 0, s, (const float*)a.state, a.cfg, a.n_envs, a.curriculum,
-                     a.reward, a.reward_terms);
+                     a.reward, a.reward_terms, a.stats);
   return hipGetLastError();
 }
 

@@ -63,7 +63,7 @@ struct StepArgs {
 };
 
 /* workgroups of step_kernel resident on the device at once (occupancy x CUs) */
-int step_resident_blocks(int device, int xg);
+int step_resident_blocks(int device, int xg, int solver);
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s);
 hipError_t launch_reset(const StepArgs& a, hipStream_t s);

@@ -369,9 +369,10 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                 if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
                     continue  # visual only
                 gt = ga.get("type", "sphere")
-                if gt not in COLLIDER_TYPES or len(desc["geoms"]) >= MAX_COLLIDERS:
-                    # the engine collides up to 4 boxes, capsules and spheres with the floor; other
-                    # colliding geoms are listed so a caller can see what the model leaves out
+                if gt not in COLLIDER_TYPES:
+                    # the engine collides boxes, capsules and spheres with the floor; other colliding
+                    # geoms are listed so a caller can see what the model leaves out (the count cap,
+                    # MAX_COLLIDERS, is applied after the touch sensors pick their geoms, below)
                     desc.setdefault("skipped_geoms", []).append({"name": ga.get("name", ""), "body": name, "type": gt})
                     continue
                 nsz = COLLIDER_TYPES[gt]
@@ -385,7 +386,11 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                     gd["pos"] = [float(v) for v in fpos]
                     gq = _mat_quat(fR)
                 else:
-                    gd["size"] = _floats(ga["size"], nsz)[:nsz]
+                    # MuJoCo stores three sizes and ignores the ones a type does not use
+                    sz = _floats(ga.get("size", ""))
+                    if len(sz) < nsz:
+                        raise ValueError(f"geom {gd['name']}: a {gt} needs {nsz} sizes, got {ga.get('size')!r}")
+                    gd["size"] = sz[:nsz]
                     if "pos" in ga:
                         gd["pos"] = _floats(ga["pos"], 3)
                 if gq != [1.0, 0.0, 0.0, 0.0]:
@@ -467,6 +472,22 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
             sd["touch_geom"] = geom
         elif touched is not None:
             raise ValueError(f"touch sensor on site {sd['name']}: no collider on body {sd['body']}")
+    # at most MAX_COLLIDERS floor colliders: the touch sensors' geoms (the soles) first, then the
+    # others in document order; the rest are listed as skipped (zb_create refuses such a model)
+    touch = {sd["touch_geom"] for sd in desc["sites"] if "touch_geom" in sd}
+    if len(touch) > MAX_COLLIDERS:
+        raise ValueError(f"{len(touch)} touch-sensor colliders, the engine has contacts for {MAX_COLLIDERS}")
+    room = MAX_COLLIDERS - len(touch)
+    keep = []
+    for g in desc["geoms"]:
+        if g["name"] in touch:
+            keep.append(g)
+        elif room > 0:
+            keep.append(g)
+            room -= 1
+        else:
+            desc.setdefault("skipped_geoms", []).append({"name": g["name"], "body": g["body"], "type": g["type"]})
+    desc["geoms"] = keep
     return desc
 
 

@@ -55,9 +55,13 @@ def test_feet_airtime_exact_rollout_matches_ksim(oracle_mod):
     eng.reset()
     _rollout(eng, cs, 5, seed=1, mark=False)  # airtime carries and contact history from a first rollout
     T = 200
+    eng.get_stats(clear=True)
     terms, rew, done, cont, carry0 = _rollout(eng, cs, T, seed=2)
     before_t, before_r = terms.clone(), rew.clone()
     eng.feet_airtime_exact(rew[0], terms[0], curriculum=1.0)
+    # the statistics' reward sum follows the patched row 0 (fp32 running sums: rtol 1e-5)
+    np.testing.assert_allclose(eng.get_stats()[:, cs.ST_REWARD].double().cpu().numpy(),
+                               rew.double().sum(0).cpu().numpy(), rtol=1e-5, atol=1e-4)
     final_air = eng.get_state()[:, cs.S_AIRTIME:cs.S_AIRTIME + 2]
     torch.cuda.synchronize()
     ref, carry = oracle_mod.feet_airtime_traj(cont.cpu().numpy(), done.cpu().numpy().astype(bool),

@@ -305,6 +305,37 @@ def test_one_step_parity_without_early_exit(torch_gpu, cmodel, oracle_mod):
         err.report()
 
 
+def test_rollout_without_early_exit(torch_gpu, cmodel, oracle_mod):
+    """C1's first 8 steps from reset (64 envs, the golden fixture's actions) with the solver's early
+    exit off in the engine and both oracles: every env within the golden reward bound with no
+    exception (budget 0), except where the fp32 and fp64 oracles themselves part (slack 2x gap).
+    With the early exit on, one env drifts to 2.15e-4 by step 7 (test_golden_rollout's budget)."""
+    torch = torch_gpu
+    g = dict(np.load(os.path.join(GOLDEN, "c1_64x128_seed0.npz")))
+    n, seed = int(g["cfg_n"]), int(g["cfg_seed"])
+    cfg = default_config()
+    cfg.tolerance = 0.0
+    eng = engine(cmodel, cfg, n, seed=seed)
+    eng.reset()
+    e32 = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=seed)
+    e64 = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=seed, precision="f64")
+    e32.reset()
+    e64.reset()
+    err = MaxErr("C1 8 steps, tolerance 0", budget=0, loose=1.0)
+    for t in range(8):
+        a = g["actions"][t]
+        r32, r64 = e32.step(a), e64.step(a)
+        out = eng.step(torch.from_numpy(a).cuda())
+        torch.cuda.synchronize()
+        err.add(f"reward[{t}]", out["reward"].cpu().numpy(), r32["reward"], GOLDEN_TOL["reward"], ref64=r64["reward"])
+        for e in err.take_over():
+            print(f"[{err.name}] step {t} env {e}: engine {float(out['reward'][e]):.7f} oracle f32 "
+                  f"{float(r32['reward'][e]):.7f} f64 {float(r64['reward'][e]):.7f}")
+    gs = eng.get_state().cpu().numpy()
+    err.add("base_pos[7]", gs[:, :3], e32.state[:, :3], GOLDEN_TOL["final_base_pos"], ref64=e64.state[:, :3])
+    err.report()
+
+
 # Multi-step rollouts from the same reset (contact dynamics are chaotic): the first 8 rewards and
 # the final base position of the committed oracle fixtures.
 # Measured (round 3): rewards <= 1.8e-6 over the 8 steps, final base position <= 2.0e-6.
@@ -367,13 +398,19 @@ def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
     rew, done = np.stack(rew), np.stack(done)
     ex = min(steps, GOLDEN_EXACT_STEPS)
     np.testing.assert_array_equal(done[:ex], g["done"][:ex])
-    err = MaxErr(f"golden {name}")
+    # one env per step may be up to 100x the bound: an exit-iteration difference (MaxErr) early in
+    # the rollout compounds over the steps (C1: one env of 64 at 2.15e-4 by step 7, r04 v3;
+    # test_rollout_without_early_exit shows it vanish with the early exit off)
+    err = MaxErr(f"golden {name}", loose=100.0)
     tol = GOLDEN_TOL_CG if solver == "cg" else GOLDEN_TOL
     e64 = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=seed, precision="f64")
     e64.reset()
     for t in range(8):
         r64 = e64.step(g["actions"][t])["reward"]
         err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"], ref64=r64)
+        for e in err.take_over():
+            print(f"[golden {name}] step {t} env {e} over the bound: engine {rew[t, e]:.7f} oracle f32 "
+                  f"{g['reward'][t, e]:.7f} f64 {r64[e]:.7f}")
     gs = eng.get_state().cpu().numpy()
     if steps <= GOLDEN_EXACT_STEPS:
         err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], tol["final_base_pos"])

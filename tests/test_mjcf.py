@@ -471,3 +471,30 @@ def test_skipped_colliders_are_rejected_by_zb_create():
         if rc == 0:
             L.zb_destroy(h)
     assert compile_model(with_shin("capsule")).cmodel.ngeom == 3
+
+
+def test_collider_sizes_beyond_the_type_are_ignored():
+    """MuJoCo keeps three sizes per geom and ignores the ones a type does not use (a default class
+    often sets all three): a sphere with size='0.05 0 0' is a sphere of radius 0.05; too few sizes
+    for the type is an error."""
+    b = load_mjcf("<mujoco><worldbody><body name='b'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
+                  "<geom name='s' type='sphere' size='0.05 0 0'/><geom name='c' type='capsule' size='0.01 0.04 0'/>"
+                  "</body></worldbody></mujoco>")
+    assert [g["size"] for g in b["geoms"]] == [[0.05], [0.01, 0.04]]
+    with pytest.raises(ValueError, match="needs 3 sizes"):
+        load_mjcf("<mujoco><worldbody><body name='b'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
+                  "<geom name='x' type='box' size='0.05 0.02'/></body></worldbody></mujoco>")
+
+
+def test_touch_sensor_colliders_win_the_cap():
+    """With more than four colliders the touch sensors' geoms (the soles) are kept even when four
+    other colliders come first in the document; the overflow is listed as skipped."""
+    geoms = "".join(f"<geom name='g{i}' type='sphere' size='0.01'/>" for i in range(4))
+    b = load_mjcf("<mujoco><worldbody><body name='a'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
+                  f"{geoms}<body name='foot'><joint name='j' type='hinge'/><inertial mass='1' diaginertia='1 1 1'/>"
+                  "<geom name='sole' type='box' size='0.02 0.03 0.005'/><site name='foot_site'/></body></body>"
+                  "</worldbody><actuator><motor joint='j'/></actuator>"
+                  "<sensor><touch site='foot_site'/></sensor></mujoco>")
+    assert [g["name"] for g in b["geoms"]] == ["g0", "g1", "g2", "sole"]
+    assert [g["name"] for g in b["skipped_geoms"]] == ["g3"]
+    assert [s.get("touch_geom") for s in b["sites"]] == ["sole"]
