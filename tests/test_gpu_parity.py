@@ -329,8 +329,11 @@ def test_rollout_without_early_exit(torch_gpu, cmodel, oracle_mod):
         torch.cuda.synchronize()
         err.add(f"reward[{t}]", out["reward"].cpu().numpy(), r32["reward"], GOLDEN_TOL["reward"], ref64=r64["reward"])
         for e in err.take_over():
+            dt = out["reward_terms"][e].cpu().numpy() - r32["reward_terms"][e]
             print(f"[{err.name}] step {t} env {e}: engine {float(out['reward'][e]):.7f} oracle f32 "
-                  f"{float(r32['reward'][e]):.7f} f64 {float(r64['reward'][e]):.7f}")
+                  f"{float(r32['reward'][e]):.7f} f64 {float(r64['reward'][e]):.7f}; term errors "
+                  f"{np.array2string(dt, precision=2)}; qpos error "
+                  f"{float(np.abs(eng.get_state().cpu().numpy()[e, :27] - e32.state[e, :27]).max()):.2e}")
     gs = eng.get_state().cpu().numpy()
     err.add("base_pos[7]", gs[:, :3], e32.state[:, :3], GOLDEN_TOL["final_base_pos"], ref64=e64.state[:, :3])
     err.report()
