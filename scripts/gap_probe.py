@@ -32,6 +32,9 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--variants", default="bench,noev,nomark,nofork,graph")
+    ap.add_argument("--configs", default="",
+                    help="extra group layouts timed with plain EnvGroups.step, e.g. '1x0,2x2,3x1,4x1' "
+                         "(groups x chunks per group launch; chunks 0 = zb_create's automatic choice)")
     args = ap.parse_args()
 
     import torch  # noqa: PLC0415
@@ -129,6 +132,32 @@ def main() -> None:
             out["kernel_avg_ms"] = sum(ks) / len(ks)
         print(variant, out["ms_per_step"][variant]["median"], flush=True, file=sys.stderr)
     eng.check()
+    for spec in filter(None, args.configs.split(",")):
+        G, ch = (int(x) for x in spec.split("x"))
+        if G == 1:
+            from zbot_amd.engine import HipEngine  # noqa: PLC0415
+
+            e2 = HipEngine(compile_model(), default_config(), n, device=0)
+            e2.set_step_chunks(ch)
+        else:
+            e2 = EnvGroups(compile_model(), default_config(), n, groups=G, device=0, chunks=ch)
+        e2.reset()
+        for t in range(8):
+            e2.step(acts[t], extras=False)
+        e2.join()
+        torch.cuda.synchronize()
+        times = []
+        for rep in range(args.reps):
+            t0 = time.perf_counter()
+            for t in range(K):
+                e2.step(acts[(8 + t) % 64], extras=False)
+            e2.join()
+            torch.cuda.synchronize()
+            times.append((time.perf_counter() - t0) * 1e3 / K)
+        e2.check()
+        out["ms_per_step"][f"G{G}_chunks{ch}"] = {"median": statistics.median(times), "min": min(times), "all": times}
+        print(spec, statistics.median(times), flush=True, file=sys.stderr)
+        del e2
     print(json.dumps(out))
 
 
