@@ -331,6 +331,11 @@ __device__ __forceinline__ int vopq(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+/* a compile-time bool as a value (a generic lambda's argument picks its instantiation) */
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
 
 /* Diagnostic phase stamps (separate build, -DZB_STAMPS): cycles per phase of the
    step, accumulated per env; never compiled into the product library. */
@@ -650,6 +655,10 @@ struct Rows {
   /* the joint-limit row (exists only past a limit, at most one side per dof):
      Jacobian sl * e_dof (sl = +1 lower, -1 upper), jl = sl * qacc - al */
   float sl, al, Dl, jl, flim; int actl;
+  /* wave-uniform: some joint-limit row exists in either env of the wave. While none does (the
+     usual case: no C2 substep has a dof past a limit) the solvers skip the limit row's terms,
+     which would all be exact zeros, so the results are the same bits */
+  bool anyl;
   int nrow;
   uint32_t exmask; /* team-uniform: existing contact rows */
   XRow x;          /* second bank (XG kernels only) */
@@ -1753,6 +1762,8 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
       r.al = r.hl ? a1 : 0.f;
     }
   }
+  /* taken with every lane active, so the flag is one wave-uniform (scalar) value */
+  r.anyl = __ballot(r.hl) != 0ull;
   tsync();
 }
 
@@ -1789,11 +1800,13 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
   int a;
   const float k0 = eval_one(jc, r.D, f, a);
   const float k1 = eval_fric(jf_, r.Df, r.Rf, r.fl, f, a);
-  const float k2 = eval_one(jl_, r.Dl, f, a);
   float cost = 0.f;
   cost += r.ex ? k0 : 0.f;
   cost += r.hf ? k1 : 0.f;
-  cost += r.hl ? k2 : 0.f;
+  if (r.anyl) {
+    const float k2 = eval_one(jl_, r.Dl, f, a);
+    cost += r.hl ? k2 : 0.f;
+  }
   if constexpr (XG) {
     const float k3 = eval_one(jx, r.x.D, f, a);
     cost += r.x.ex ? k3 : 0.f;
@@ -1849,20 +1862,24 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
   if (c.l < NV) cost += 0.5f * (Ma - fs) * (qacc - qs);
   {
     /* all four row kinds evaluated, results kept only for rows that exist */
-    float f0, f1, f2, f3;
-    int a0, a1, a2, a3;
+    float f0, f1;
+    int a0, a1;
     const float k0 = eval_one(r.jar, r.D, f0, a0);
     const float k1 = eval_fric(r.jf, r.Df, r.Rf, r.fl, f1, a1);
-    const float k2 = eval_one(r.jl, r.Dl, f2, a2);
     cost += r.ex ? k0 : 0.f;
     cost += r.hf ? k1 : 0.f;
-    cost += r.hl ? k2 : 0.f;
     r.f = r.ex ? f0 : r.f;
     r.act = r.ex ? a0 : r.act;
     r.ff = r.hf ? f1 : r.ff;
     r.actf = r.hf ? a1 : r.actf;
-    r.flim = r.hl ? f2 : r.flim;
-    r.actl = r.hl ? a2 : r.actl;
+    if (r.anyl) {
+      float f2;
+      int a2;
+      const float k2 = eval_one(r.jl, r.Dl, f2, a2);
+      cost += r.hl ? k2 : 0.f;
+      r.flim = r.hl ? f2 : r.flim;
+      r.actl = r.hl ? a2 : r.actl;
+    }
   }
   if (r.ex) L->rowF[c.l] = r.f;
   L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
@@ -1891,7 +1908,7 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
       qc += (f2 ? sx0 : 0.f) + (f3 ? sx1 : 0.f);
     }
     if (r.hf) qc += r.ff;
-    if (r.hl) qc += r.sl * r.flim;
+    if (r.anyl && r.hl) qc += r.sl * r.flim;
   }
   grad = Ma - fs - qc;
   return cost;
@@ -2043,10 +2060,10 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     float dd = 0.f;
     if (full) {
       if (r.hf && r.actf) dd += r.Df;
-      if (r.hl && r.actl) dd += r.Dl;
+      if (r.anyl && r.hl && r.actl) dd += r.Dl;
     } else {
       if (r.hf) dd += (float)(r.actf - pf) * r.Df;
-      if (r.hl) dd += (float)(r.actl - plo) * r.Dl;
+      if (r.anyl && r.hl) dd += (float)(r.actl - plo) * r.Dl;
     }
     Hd += dd;
   }
@@ -2085,7 +2102,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   const float jv0 = isd ? search : 0.f;
   float g20 = (r.ex && r.act) ? r.D * r.Jv * r.Jv : 0.f;
   g20 += (r.hf && r.actf) ? r.Df * jv0 * jv0 : 0.f;
-  g20 += (r.hl && r.actl) ? r.Dl * jv0 * jv0 : 0.f;
+  if (r.anyl) g20 += (r.hl && r.actl) ? r.Dl * jv0 * jv0 : 0.f;
   if constexpr (XG) g20 += (r.x.ex && r.x.act) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
   float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
   tsum_n<4>(cc);
@@ -2095,56 +2112,69 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   /* row existence folded into the constants (zero for a row that does not exist) */
   const float DJ = r.ex ? r.D * r.Jv : 0.f, DJ2 = DJ * r.Jv;
   const float Rf = r.Rf * r.fl, DfJ = r.hf ? r.Df * jv0 : 0.f, DfJ2 = DfJ * jv0;
-  const float sv = r.sl * jv0, jl0 = r.jl;
-  const float DlJ = r.hl ? r.Dl * sv : 0.f, DlJ2 = DlJ * sv;
+  float sv = 0.f, jl0 = 0.f, DlJ = 0.f, DlJ2 = 0.f;
+  if (r.anyl) {
+    sv = r.sl * jv0;
+    jl0 = r.jl;
+    DlJ = r.hl ? r.Dl * sv : 0.f;
+    DlJ2 = DlJ * sv;
+  }
   const float DXJ = (XG && r.x.ex) ? r.x.D * r.x.Jv : 0.f, DXJ2 = DXJ * r.x.Jv;
-  auto eval = [&](float alpha, float& d1, float& d2) {
-    /* branch-free; rows that do not exist or are inactive add exact zeros */
-    float g1, g2;
-    {
-      /* contact: active below zero */
-      const float x = r.jar + alpha * r.Jv;
-      g1 = DJ * fminf(x, 0.f);
-      g2 = x < 0.f ? DJ2 : 0.f;
-    }
-    {
-      /* frictionloss: linear zone |x| < R fl, saturated at -+fl outside (the force
-         D x clamped to the saturation: D x = fl at x = R fl) */
-      const float x = r.jf + alpha * jv0;
-      g1 += DfJ * __builtin_amdgcn_fmed3f(x, -Rf, Rf);
-      g2 += fabsf(x) < Rf ? DfJ2 : 0.f;
-    }
-    {
-      /* joint limit: active below zero */
-      const float x = jl0 + alpha * sv;
-      g1 += DlJ * fminf(x, 0.f);
-      g2 += x < 0.f ? DlJ2 : 0.f;
-    }
-    if (XG && r.x.any) {
-      /* second-bank contact row */
-      const float x = r.x.jar + alpha * r.x.Jv;
-      g1 += DXJ * fminf(x, 0.f);
-      g2 += x < 0.f ? DXJ2 : 0.f;
-    }
-    float gg[2] = {g1, g2};
-    tsum_n<2>(gg);
-    d1 = c1 + alpha * c2 + gg[0];
-    d2 = c2 + gg[1];
-  };
   float d1 = cc[2], d2 = c2 + cc[3];
   if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
-  float gtol = cfg->ls_tolerance * (-d1);
-  float lo = 0.f, hi = -1.f;
-  float alpha = -d1 / d2;
-  for (int it = 0; it < cfg->ls_iterations; it++) {
-    eval(alpha, d1, d2);
-    if (fabsf(d1) <= gtol) break;
-    if (d1 < 0.f) lo = alpha; else hi = alpha;
-    float an = alpha - d1 / d2;
-    if (!(an > lo) || (hi >= 0.f && !(an < hi))) an = 0.5f * (lo + (hi >= 0.f ? hi : 2.f * alpha));
-    alpha = an;
-  }
-  return alpha;
+  const float gtol = cfg->ls_tolerance * (-d1);
+  /* the iteration loop in two copies, with and without the joint-limit row (LIM): a branch on
+     r.anyl inside the evaluation is if-converted by the compiler into selects around the row's
+     arithmetic, which then runs in every evaluation */
+  auto iterate = [&](auto lim) -> float {
+    constexpr bool LIM = decltype(lim)::value;
+    auto eval = [&](float alpha, float& e1, float& e2) {
+      /* branch-free; rows that do not exist or are inactive add exact zeros */
+      float g1, g2;
+      {
+        /* contact: active below zero */
+        const float x = r.jar + alpha * r.Jv;
+        g1 = DJ * fminf(x, 0.f);
+        g2 = x < 0.f ? DJ2 : 0.f;
+      }
+      {
+        /* frictionloss: linear zone |x| < R fl, saturated at -+fl outside (the force
+           D x clamped to the saturation: D x = fl at x = R fl) */
+        const float x = r.jf + alpha * jv0;
+        g1 += DfJ * __builtin_amdgcn_fmed3f(x, -Rf, Rf);
+        g2 += fabsf(x) < Rf ? DfJ2 : 0.f;
+      }
+      if constexpr (LIM) {
+        /* joint limit: active below zero (the copy without it runs while no row of the wave
+           exists, whose terms here would be exact zeros) */
+        const float x = jl0 + alpha * sv;
+        g1 += DlJ * fminf(x, 0.f);
+        g2 += x < 0.f ? DlJ2 : 0.f;
+      }
+      if (XG && r.x.any) {
+        /* second-bank contact row */
+        const float x = r.x.jar + alpha * r.x.Jv;
+        g1 += DXJ * fminf(x, 0.f);
+        g2 += x < 0.f ? DXJ2 : 0.f;
+      }
+      float gg[2] = {g1, g2};
+      tsum_n<2>(gg);
+      e1 = c1 + alpha * c2 + gg[0];
+      e2 = c2 + gg[1];
+    };
+    float lo = 0.f, hi = -1.f;
+    float alpha = -d1 / d2;
+    for (int it = 0; it < cfg->ls_iterations; it++) {
+      eval(alpha, d1, d2);
+      if (fabsf(d1) <= gtol) break;
+      if (d1 < 0.f) lo = alpha; else hi = alpha;
+      float an = alpha - d1 / d2;
+      if (!(an > lo) || (hi >= 0.f && !(an < hi))) an = 0.5f * (lo + (hi >= 0.f ? hi : 2.f * alpha));
+      alpha = an;
+    }
+    return alpha;
+  };
+  return r.anyl ? iterate(BoolC<true>{}) : iterate(BoolC<false>{});
 }
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
@@ -2208,7 +2238,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     r.jar += alpha * r.Jv;
     if constexpr (XG) r.x.jar += alpha * r.x.Jv;
     r.jf += alpha * search;
-    r.jl += alpha * (r.sl * search);
+    if (r.anyl) r.jl += alpha * (r.sl * search);
     float oldcost = cost;
     const int pa = r.act, pf = r.actf, plo = r.actl, pa2 = XG ? r.x.act : 0;
     /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
@@ -2216,7 +2246,8 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     float red[3];
     red[0] = update_constraint_lane<XG>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
-    red[2] = (r.act != pa || r.actf != pf || r.actl != plo || (XG && r.x.act != pa2)) ? 1.f : 0.f;
+    red[2] = (r.act != pa || r.actf != pf || (XG && r.x.act != pa2)) ? 1.f : 0.f;
+    if (r.anyl && r.actl != plo) red[2] = 1.f;
     tsum_n<3>(red);
     cost = red[0];
     STAMP(S_UPD);
@@ -2298,7 +2329,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     r.jar += alpha * r.Jv;
     if constexpr (XG) r.x.jar += alpha * r.x.Jv;
     r.jf += alpha * search;
-    r.jl += alpha * (r.sl * search);
+    if (r.anyl) r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
     float red[2];
     red[0] = update_constraint_lane<XG>(c, r, jr, x, qs, fs, Ma, grad);
