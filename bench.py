@@ -302,8 +302,8 @@ def bench_train_defaults(cm, dev, rank: int, world: int, seed: int, n: int = 512
     """train.py's own training size (train.py:1770 num_envs=512, :1775 rollout_length_seconds 4.0 at
     ctrl_dt 0.02 = 200 steps): one 200-step rollout of 512 envs per GPU from reset through
     ZbotWalkingEnv (one handle below 4096 envs), [T, n] reward / done rows, FeetAirtime row 0
-    patched; actions JOINT_BIASES + 0.2 N(0,1). Latency-bound: 512 envs fill at most half of the
-    1024 SIMDs, one wave each (the solo layout; 256 waves of two envs in the paired one)."""
+    patched; actions JOINT_BIASES + 0.2 N(0,1). Latency-bound: 512 envs are 256 waves on 1024
+    SIMDs."""
     import torch  # noqa: PLC0415
     from zbot_amd.task import ZbotWalkingEnv  # noqa: PLC0415
 
@@ -319,26 +319,15 @@ def bench_train_defaults(cm, dev, rank: int, world: int, seed: int, n: int = 512
             eng.step(acts[t], curriculum=env.curriculum_level, reward=rew[t], done=done[t])
         eng.feet_airtime_exact(rew[0], None, curriculum=env.curriculum_level)
 
-    from zbot_amd.engine import LAYOUT_AUTO, LAYOUT_PAIRS  # noqa: PLC0415
-
     env.reset()
     wall = _timed_steps(rollout, 2, 1, dev, world)
     assert bool(torch.isfinite(rew).all())
-    layout = "solo" if eng.step_layout != LAYOUT_PAIRS else "pairs"
-    # the same rollouts with two envs per wave, for the layout's gain (the same bits)
-    eng.set_step_layout(LAYOUT_PAIRS)
-    env.reset()
-    wall_pairs = _timed_steps(rollout, 2, 1, dev, world)
-    eng.set_step_layout(LAYOUT_AUTO)
     return {
         "workload": f"train.py defaults: {n} envs/GPU x {T}-step rollout (train.py:1770,1775), one handle, automatic "
-                    f"resets inside, [T, n] reward / done rows, FeetAirtime row 0 patched; 2 timed rollouts after 1; "
-                    f"step layout {layout} (automatic: one env per wave up to one wave per SIMD)",
+                    "resets inside, [T, n] reward / done rows, FeetAirtime row 0 patched; 2 timed rollouts after 1",
         "env_steps_per_s": world * n * T * 2 / wall,
         "ms_per_rollout": 1e3 * wall / 2,
         "ms_per_step": 1e3 * wall / (2 * T),
-        "step_layout": layout,
-        "env_steps_per_s_pairs_layout": world * n * T * 2 / wall_pairs,
         "episodes_done": int(done.sum().item()),
     }
 

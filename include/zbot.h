@@ -180,21 +180,6 @@ int zb_get_solver_iters(ZbHandle* h, int32_t* iters_dev, void* stream);
  * Env groups on their own streams fill the drain themselves and run unchunked. */
 int zb_set_step_chunks(ZbHandle* h, int k);
 
-/* Envs per wavefront in the handle's zb_step / zb_rollout launches. The reference
- * has no such knob: it is the launch shape of the vmap'd step (train.py:1770 num_envs, the
- * batch every MjxEngine.step covers). ZB_LAYOUT_PAIRS: two envs per wave, one per 32-lane team.
- * ZB_LAYOUT_SOLO: one env per wave, the other team a ghost of the same env (same inputs, same
- * control flow, nothing stored), so no wave waits on a partner env's longer solver loop; it runs
- * unchunked. ZB_LAYOUT_AUTO (the zb_create default): solo while the launch has at most one wave
- * per SIMD (n_envs <= 4 x the device's CUs), else pairs. Every layout gives the same bits.
- * zb_get_step_layout returns the layout in effect (PAIRS or SOLO), or a negative error code. Added in
- * ABI version 4. */
-#define ZB_LAYOUT_AUTO 0
-#define ZB_LAYOUT_PAIRS 1
-#define ZB_LAYOUT_SOLO 2
-int zb_set_step_layout(ZbHandle* h, int layout);
-int zb_get_step_layout(ZbHandle* h);
-
 /* Diagnostic: one forward pass (no integration) on the qpos/qvel stored in
  * state_dev [n_envs, ZB_STATE_STRIDE] with ctrl_dev [n_envs, 20] (nullable ->
  * zero ctrl); dumps M, bias, qacc_smooth, qacc, xpos, cinert, cvel and sensor

@@ -23,7 +23,7 @@ using zb::check_cfg;
 using zb::check_model;
 using zb::fail;
 
-#define ZB_ABI_VERSION 4
+#define ZB_ABI_VERSION 3
 
 struct ZbHandle {
   int device;
@@ -44,8 +44,6 @@ struct ZbHandle {
   int32_t* itpart; /* chunked step: [n] Newton iterations so far */
   float* xj;       /* general colliders: [n + 1, ZB_XJ_STRIDE] second-bank Jacobian rows (zb_internal.h) */
   int nchunk;      /* work units per pair of envs in zb_step (1: unchunked) */
-  int layout;      /* zb_set_step_layout: ZB_LAYOUT_AUTO / _PAIRS / _SOLO */
-  int solo;        /* the layout in effect: one env per wave (zb_step / zb_rollout, unchunked) */
   int air_mark;    /* zb_mark_rollout_start: the next zb_step / zb_rollout is a rollout's step 0 */
   int air_marked;  /* a marked step has been launched since the last zb_feet_airtime_exact */
 };
@@ -71,21 +69,6 @@ static int choose_chunks(int n_envs, int n_substeps, int resident) {
   }
   if (k > n_substeps) k = n_substeps;
   return k < 1 ? 1 : k;
-}
-
-/* Envs per wave for zb_step / zb_rollout. Two envs share a wave (one per 32-lane
-   team) unless the launch leaves SIMDs idle anyway: with n <= 4 x CUs envs (one wave per SIMD at
-   most), each env gets a wave of its own, the second team a ghost of the same env, so a wave never
-   waits on its partner env's longer solver loop. Same bits either way. ZB_STEP_LAYOUT overrides
-   (1 = pairs, 2 = solo). */
-static int choose_solo(int n_envs, int layout, int device) {
-  const char* ov = getenv("ZB_STEP_LAYOUT");
-  if (ov && *ov) layout = atoi(ov);
-  if (layout == ZB_LAYOUT_PAIRS) return 0;
-  if (layout == ZB_LAYOUT_SOLO) return 1;
-  int cus = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-  return n_envs > 0 && n_envs <= 4 * cus ? 1 : 0;
 }
 
 #define HIPCHK(expr)                                                                       \
@@ -154,8 +137,6 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMemset(h->itpart, 0, n * sizeof(int32_t));
   if (e == hipSuccess && zb::needs_xg(model)) e = hipMalloc(&h->xj, (n + 1) * ZB_XJ_STRIDE * sizeof(float));
   h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device, zb::needs_xg(model) ? 1 : 0, cfg->solver));
-  h->layout = ZB_LAYOUT_AUTO;
-  h->solo = choose_solo(n_envs, h->layout, device);
 #if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
   {
     /* phase stamps: ZB_NSTAMP per env; wave times: 4 words per (chunk, pair), up to one chunk per
@@ -248,8 +229,7 @@ int zb_step(ZbHandle* h, const float* action, float* obs_actor, float* obs_criti
   a.done = done;
   a.success = success;
   a.curriculum = curriculum_level;
-  a.solo = h->solo;
-  a.nchunk = h->solo ? 1 : h->nchunk;
+  a.nchunk = h->nchunk;
   a.air_mark = h->air_mark;
   hipError_t e = zb::launch_step(a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_step launch: %s", hipGetErrorString(e));
@@ -272,7 +252,6 @@ int zb_rollout(ZbHandle* h, const float* actions, int n_steps, float* obs_actor,
   a.done = done;
   a.success = success;
   a.curriculum = curriculum_level;
-  a.solo = h->solo;
   a.air_mark = h->air_mark;
   hipError_t e = zb::launch_step(a, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ZB_ELAUNCH, "zb_rollout launch: %s", hipGetErrorString(e));
@@ -349,21 +328,6 @@ int zb_set_step_chunks(ZbHandle* h, int k) {
     h->nchunk = k > h->cfg.n_substeps ? h->cfg.n_substeps : k;
   }
   return ZB_OK;
-}
-
-int zb_set_step_layout(ZbHandle* h, int layout) {
-  if (!h) return fail(ZB_EARG, "null handle");
-  if (layout != ZB_LAYOUT_AUTO && layout != ZB_LAYOUT_PAIRS && layout != ZB_LAYOUT_SOLO)
-    return fail(ZB_EARG, "zb_set_step_layout: layout = %d", layout);
-  int rc = use_device(h);
-  if (rc) return rc;
-  h->layout = layout;
-  h->solo = choose_solo(h->n, layout, h->device);
-  return ZB_OK;
-}
-int zb_get_step_layout(ZbHandle* h) {
-  if (!h) return fail(ZB_EARG, "null handle");
-  return h->solo ? ZB_LAYOUT_SOLO : ZB_LAYOUT_PAIRS;
 }
 
 int zb_check(ZbHandle* h) {

@@ -3056,11 +3056,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
      control step. The state passes between chunks through the state row exactly
      as it passes between control steps, so the results do not depend on the chunking. */
   const int K = a.nchunk;
-  /* envs per wave: two (one per team), or one under the solo layout (a.solo, unchunked only),
-     where team 1 runs as a ghost of team 0's env: the same inputs, hence the same control flow,
-     so the wave never waits on a partner env's longer solver loop */
-  const int epw = a.solo ? 1 : NTEAM;
-  const int npair = (a.n_envs + epw - 1) / epw;
+  const int npair = (a.n_envs + NTEAM - 1) / NTEAM;
   int pair = blockIdx.x, ch = 0;
   bool timed_out = false;
   if (K > 1) {
@@ -3089,7 +3085,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       }
     }
   }
-  const int e = a.solo ? pair : pair * NTEAM + team;
+  const int e = pair * NTEAM + team;
 #ifdef ZB_WAVETIME
   /* diagnostic build: the pair's start / end on the 100 MHz constant clock and its CU */
   const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
@@ -3097,23 +3093,19 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   /* Both teams of a wave stay live to the end: forward()'s J'DJ runs on the
      matrix cores with operands from all 64 lanes (jdj_mfma). A team past the
      last env (odd n) runs as a ghost copy of env n-1 that stores nothing. */
-  const bool live = e < a.n_envs && !(a.solo && team == 1);
-  const int ee = e < a.n_envs ? e : a.n_envs - 1;
-  /* a solo ghost mirrors its env exactly, the randomization row included (read, and at a reset
-     rewritten with the bits team 0 writes there in the same store instruction) */
-  const bool mirror = live || a.solo;
+  const bool live = e < a.n_envs;
+  const int ee = live ? e : a.n_envs - 1;
   const ZbModel* m = a.model;
   const ZbEnvConfig* cfg = a.cfg;
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
   /* the env's second-bank rows (a team past n: the spare block n) */
-  /* (a solo ghost shares its env's block, writing the bits team 0 writes) */
-  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(mirror ? ee : a.n_envs) * ZB_XJ_STRIDE);
+  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(live ? e : a.n_envs) * ZB_XJ_STRIDE);
   /* per-env row addresses are formed where they are used, from an opaque copy of the env
      index: held across the substep loop they were 64-bit values spilled to scratch */
   auto state_row = [&]() { return a.state + (size_t)vopq(ee) * ZB_STATE_STRIDE; };
   auto rand_row = [&]() {
-    return mirror && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)vopq(ee) * ZB_RAND_STRIDE : nullptr;
+    return live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)vopq(ee) * ZB_RAND_STRIDE : nullptr;
   };
 #ifdef ZB_STAMPS
   if (c.l < NSTAMP) c.L->stamp[c.l] = 0;
@@ -3419,9 +3411,7 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
 #else
   const StepArgs& b = a;
 #endif
-  if (b.solo && b.nchunk != 1) return hipErrorInvalidValue;
-  const int epw = b.solo ? 1 : NTEAM;
-  dim3 grid((unsigned)((b.n_envs + epw - 1) / epw * b.nchunk)), block(64);
+  dim3 grid((unsigned)((b.n_envs + NTEAM - 1) / NTEAM * b.nchunk)), block(64);
   ZB_LAUNCH_VARIANT(step_kernel, grid, block, s, b);
   return hipGetLastError();
 }

@@ -60,7 +60,6 @@ struct StepArgs {
   int solver;               /* ZB_SOLVER_NEWTON / ZB_SOLVER_CG: which kernel instantiation runs */
   int xg;                   /* general colliders (zb_host.h needs_xg): the two-bank instantiation */
   float* xj;                /* xg: [n + 1, ZB_XJ_STRIDE] second-bank Jacobian rows (the last block: ghost teams) */
-  int solo;                 /* step_kernel: one env per wave (team 1 a ghost of team 0's env), unchunked */
 };
 
 /* workgroups of step_kernel resident on the device at once (occupancy x CUs) */

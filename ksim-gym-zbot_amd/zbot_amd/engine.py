@@ -13,9 +13,7 @@ import os
 from . import cstructs as cs
 
 LIB_NAME = "libzbot_hip.so"
-ABI_VERSION = 4  # include/zbot.h: 2 added zb_step / zb_rollout's `success`, 3 the exact FeetAirtime patch,
-#               4 the step layout (zb_set_step_layout / zb_get_step_layout)
-LAYOUT_AUTO, LAYOUT_PAIRS, LAYOUT_SOLO = 0, 1, 2  # ZB_LAYOUT_*
+ABI_VERSION = 3  # include/zbot.h: 2 added zb_step / zb_rollout's `success`, 3 the exact FeetAirtime patch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 CSRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 
@@ -66,16 +64,13 @@ def load_library(path: str | None = None) -> C.CDLL:
         getattr(L, f).argtypes = [vp, vp, vp]
     L.zb_get_stats.argtypes = [vp, vp, C.c_int, vp]
     L.zb_set_step_chunks.argtypes = [vp, C.c_int]
-    L.zb_set_step_layout.argtypes = [vp, C.c_int]
-    L.zb_get_step_layout.argtypes = [vp]
     L.zb_debug_forward.argtypes = [vp, vp, vp, vp, vp]
     L.zb_mark_rollout_start.argtypes = [vp]
     L.zb_check.argtypes = [vp]
     L.zb_feet_airtime_exact.argtypes = [vp, vp, vp, C.c_float, vp]
     for f in ("zb_create", "zb_destroy", "zb_reset", "zb_step", "zb_rollout", "zb_get_state", "zb_set_state",
               "zb_get_rand", "zb_set_rand", "zb_get_stats", "zb_get_solver_iters", "zb_debug_forward",
-              "zb_set_step_chunks", "zb_set_step_layout", "zb_get_step_layout", "zb_mark_rollout_start",
-              "zb_feet_airtime_exact", "zb_check"):
+              "zb_set_step_chunks", "zb_mark_rollout_start", "zb_feet_airtime_exact", "zb_check"):
         getattr(L, f).restype = C.c_int
     # post-rollout PPO inputs (include/zbot_ppo.h)
     L.zb_gae_partials_words.argtypes = [C.c_int]
@@ -262,19 +257,6 @@ class HipEngine:
         """Work units per pair of envs in step() (0: the automatic choice, 1: whole control steps;
         DESIGN.md §4e). The same bits for every k."""
         _check(self.L.zb_set_step_chunks(self.h, int(k)))
-
-    def set_step_layout(self, layout: int) -> None:
-        """Envs per wave in step() / rollout(): LAYOUT_AUTO (solo while n_envs <= 4 x CUs),
-        LAYOUT_PAIRS (two per wave) or LAYOUT_SOLO (one per wave, the other team a ghost of the same
-        env). The same bits for every layout."""
-        _check(self.L.zb_set_step_layout(self.h, int(layout)))
-
-    @property
-    def step_layout(self) -> int:
-        """The layout in effect: LAYOUT_PAIRS or LAYOUT_SOLO."""
-        r = self.L.zb_get_step_layout(self.h)
-        _check(min(r, 0))
-        return r
 
     def check(self) -> None:
         """Synchronise and raise ZbError if a launch since the last check flagged its results
