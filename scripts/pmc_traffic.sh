@@ -7,7 +7,7 @@ set -e -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 STEPS=${STEPS:-6}
-B="bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --groups 1 --no-ppo --no-policy --no-pipeline --no-c2-rollout"
+B="bench.py --steps $STEPS --warmup 2 --no-cpu-baseline --groups 1 --no-ppo --no-policy --no-pipeline --no-c2-rollout --no-extra-legs"
 mkdir -p gpurun_out
 for pass in fetch:FETCH_SIZE write:WRITE_SIZE "valu:SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES"; do
   name=${pass%%:*}; ctrs=${pass#*:}

@@ -28,6 +28,9 @@ CASES = {
     "c5_push_seed1": dict(n=16, steps=16, seed=1, push=True, randomize=True, std=0.1),
     # round 3: the CG solver variant (ZbEnvConfig.solver)
     "c2_cg_seed2": dict(n=16, steps=16, seed=2, push=False, randomize=False, std=0.05, solver="cg"),
+    # round 4: CG at C1's ensemble size, with pushes (the GPU test compares its first 8 rewards and
+    # the 64-step ensemble statistics)
+    "c2_cg_64x64_seed4": dict(n=64, steps=64, seed=4, push=True, randomize=False, std=0.1, solver="cg"),
 }
 
 
