@@ -332,6 +332,32 @@ def bench_train_defaults(cm, dev, rank: int, world: int, seed: int, n: int = 512
     }
 
 
+def bench_c1(cm, dev, rank: int, world: int, seed: int, n: int = 64, T: int = 128) -> dict:
+    """BASELINE configs[0] on the GPU: the reference's own CPU case (64 envs x 128-step rollout) as
+    one handle's 128 zb_step launches from reset, beside cpu_baseline.c1 (the CPU twin on the same
+    shape). 64 envs are 32 waves: each control step lasts as long as its slowest env."""
+    import torch  # noqa: PLC0415
+    from zbot_amd.config import default_config  # noqa: PLC0415
+    from zbot_amd.engine import HipEngine  # noqa: PLC0415
+
+    eng = HipEngine(cm, default_config(), n, env_offset=rank * n, device=dev.index, seed=seed)
+    acts = _synthetic_actions(n, T, dev, 64 + rank, 0.05)
+
+    def rollout(_):
+        eng.reset()
+        for t in range(T):
+            eng.step(acts[t], extras=False)
+
+    wall = _timed_steps(rollout, 2, 1, dev, world)
+    return {
+        "workload": f"C1 on the GPU: {n} envs/GPU x {T}-step rollout from reset (BASELINE configs[0]), one handle, "
+                    "2 timed rollouts after 1",
+        "env_steps_per_s": world * n * T * 2 / wall,
+        "ms_per_rollout": 1e3 * wall / 2,
+        "ms_per_step": 1e3 * wall / (2 * T),
+    }
+
+
 def bench_general_colliders(cfg, n: int, steps: int, warmup: int, dev, rank: int, world: int, seed: int,
                             groups: int) -> dict:
     """C2 on the limbs model (assets/zbot_like_limbs.xml: shin boxes and hand capsules collide with
@@ -604,6 +630,7 @@ def main() -> None:
     if not args.no_extra_legs and args.config == "c2" and args.model is None:
         extra_legs["ksim_env"] = bench_ksim_env(cm, n, args.steps, args.warmup, dev, rank, world, args.seed)
         extra_legs["train_defaults"] = bench_train_defaults(cm, dev, rank, world, args.seed)
+        extra_legs["c1_gpu"] = bench_c1(cm, dev, rank, world, args.seed)
         extra_legs["general_colliders"] = bench_general_colliders(cfg, n, args.steps, args.warmup, dev, rank, world,
                                                                   args.seed, G)
 
@@ -769,6 +796,10 @@ def main() -> None:
                                                    c1_leg=False)
             else:  # the headline's env count (C2: 8192), a bounded number of env-steps
                 out["cpu_baseline"] = cpu_baseline(cm, cfg, args.cpu_baseline_sec, args.config.upper(), n_envs=n)
+            c1cpu = out["cpu_baseline"].get("c1")
+            if c1cpu and "c1_gpu" in out:
+                # the same C1 shape on the GPU and on the CPU twin, in one run
+                out["c1_gpu"]["vs_cpu_baseline_c1"] = out["c1_gpu"]["env_steps_per_s"] / c1cpu["value"]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
