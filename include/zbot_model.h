@@ -15,7 +15,7 @@
  *     (root only) or hinge; other bodies are welded (no joint);
  *   - nbody <= ZB_MAX_BODY, nv <= ZB_MAX_DOF, dof-chain depth <= ZB_MAX_DEPTH;
  *   - collision = floor plane (world geom) vs up to ZB_MAX_GEOM per-body boxes,
- *     capsules or spheres (the two foot soles first by convention);
+ *     capsules, cylinders or spheres (the two foot soles first by convention);
  *   - actuators = motors on hinge joints (joint transmission, gear).
  * All floats are fp32; all vectors are padded to 4 so rows are 16-B aligned.
  */
@@ -38,7 +38,7 @@ extern "C" {
 #define ZB_MAX_GEOM  4   /* floor colliders */
 #define ZB_MAX_SITE  8
 #define ZB_MAX_ACT   32
-#define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-capsule 2, plane-sphere 1 */
+#define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-cylinder 4, plane-capsule 2, plane-sphere 1 */
 #define ZB_MAX_CON  (ZB_MAX_GEOM * ZB_CON_PER_GEOM)
 
 /* joint types (mjtJoint values where they exist) */
@@ -49,6 +49,7 @@ extern "C" {
 /* collider types (mjtGeom values) */
 #define ZB_GEOM_SPHERE  2
 #define ZB_GEOM_CAPSULE 3
+#define ZB_GEOM_CYLINDER 5
 #define ZB_GEOM_BOX     6
 
 typedef struct ZbModel {
@@ -127,8 +128,8 @@ typedef struct ZbModel {
   int32_t  geom_type[ZB_MAX_GEOM];      /* ZB_GEOM_* */
   float    geom_pos[ZB_MAX_GEOM][4];
   float    geom_quat[ZB_MAX_GEOM][4];
-  float    geom_size[ZB_MAX_GEOM][4];    /* mjModel.geom_size: box half sizes; capsule radius,
-                                           half-length (local z); sphere radius */
+  float    geom_size[ZB_MAX_GEOM][4];    /* mjModel.geom_size: box half sizes; capsule / cylinder
+                                           radius, half-length (local z); sphere radius */
   /* floor: geom_priority=2 (train.py:1330) -> floor friction/solref/solimp win */
   float    floor_friction[4];            /* sliding, torsional, rolling */
   float    floor_solref[4];

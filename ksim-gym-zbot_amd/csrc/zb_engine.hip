@@ -1584,58 +1584,106 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
 #pragma unroll
   for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
   const int ty = XG ? m->geom_type[g] : ZB_GEOM_BOX;
-  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE;
+  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE, cyl = XG && ty == ZB_GEOM_CYLINDER;
   /* the lane's point relative to the geom centre, geom frame -> body frame -> world */
   float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
   float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
   const float s0 = m->geom_size[g][0], s1 = m->geom_size[g][1], s2 = m->geom_size[g][2];
-  float v[3];
-  if (box) {
-    v[0] = (slot & 1) ? s0 : -s0;
-    v[1] = (slot & 2) ? s1 : -s1;
-    v[2] = -s2;
-  } else {
-    v[0] = 0.f;
-    v[1] = 0.f;
-    v[2] = cap ? (slot == 0 ? s1 : -s1) : 0.f;
-  }
-  float w[3], t[3];
-  quat_rotate(w, gq, v);
-  if (box) {
-    /* the corner's offset along the normal: the z row of the body rotation times w */
-    const float rz0 = 2.f * (xqs[1] * xqs[3] - xqs[0] * xqs[2]), rz1 = 2.f * (xqs[2] * xqs[3] + xqs[0] * xqs[1]);
-    const float rz2 = 1.f - 2.f * (xqs[1] * xqs[1] + xqs[2] * xqs[2]);
-    if (rz0 * w[0] + rz1 * w[1] + rz2 * w[2] > 0.f) {
-      /* corner k lies above the centre: its mirror 7-k is the one MuJoCo keeps */
+  float p[3], dist;
+  bool slot_ok;
+  float t1x = 0.f, t1y = 1.f;
+  if (cyl) {
+    /* mjc_PlaneCylinder (oracle collision()): the axis a turned toward the plane, v the radius
+       vector in the disk planes toward it; slot 0 the near disk's deepest point c + v + a, 1 the far
+       disk's c + v - a, 2 / 3 the near disk's points 120 degrees away, c + a - v / 2 +- v1; none
+       unless slot 0 is within the margin */
+    const float ez[3] = {0.f, 0.f, 1.f}, ex[3] = {1.f, 0.f, 0.f};
+    float ab[3], a[3], eb[3], xw[3], cw[3];
+    quat_rotate(ab, gq, ez);
+    quat_rotate(a, xqs, ab);
+    quat_rotate(eb, gq, ex);
+    quat_rotate(xw, xqs, eb);
+    quat_rotate(cw, xqs, gp);
+    const float c0 = xp[0] + cw[0], c1 = xp[1] + cw[1], c2 = xp[2] + cw[2];
+    float prja = a[2];
+    if (prja > 0.f) {
 #pragma unroll
-      for (int k = 0; k < 3; k++) w[k] = -w[k];
+      for (int k = 0; k < 3; k++) a[k] = -a[k];
+      prja = -prja;
     }
+    float v[3] = {a[0] * prja, a[1] * prja, a[2] * prja - 1.f};
+    const float len = sqrtf(dot3(v, v));
+    const bool par = !(len >= MINVAL); /* the disks parallel to the plane: the geom's x axis */
+    const float sv = par ? s0 : s0 / len;
+#pragma unroll
+    for (int k = 0; k < 3; k++) v[k] = (par ? xw[k] : v[k]) * sv;
+    const float prjv = v[2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) a[k] *= s1;
+    prja *= s1;
+    const float d1 = c2 + prja + prjv;
+    float v1[3];
+    cross3(v1, v, a);
+    const float n1 = sqrtf(dot3(v1, v1));
+    const float sc = n1 > 0.f ? s0 * 0.8660254037844386f / n1 : 0.f;
+    const float sa = slot == 1 ? -1.f : 1.f;                    /* +a, except the far disk */
+    const float svv = slot >= 2 ? -0.5f : 1.f;                  /* +v, -v / 2 on the triangle */
+    const float s1v = slot == 2 ? sc : (slot == 3 ? -sc : 0.f); /* +- v1 on the triangle */
+    p[0] = c0 + svv * v[0] + sa * a[0] + s1v * v1[0];
+    p[1] = c1 + svv * v[1] + sa * a[1] + s1v * v1[1];
+    p[2] = c2 + svv * v[2] + sa * a[2] + s1v * v1[2];
+    dist = slot == 0 ? d1 : (slot == 1 ? c2 - prja + prjv : c2 + prja - 0.5f * prjv);
+    slot_ok = d1 <= m->floor_margin;
+  } else {
+    float v[3];
+    if (box) {
+      v[0] = (slot & 1) ? s0 : -s0;
+      v[1] = (slot & 2) ? s1 : -s1;
+      v[2] = -s2;
+    } else {
+      v[0] = 0.f;
+      v[1] = 0.f;
+      v[2] = cap ? (slot == 0 ? s1 : -s1) : 0.f;
+    }
+    float w[3], t[3];
+    quat_rotate(w, gq, v);
+    if (box) {
+      /* the corner's offset along the normal: the z row of the body rotation times w */
+      const float rz0 = 2.f * (xqs[1] * xqs[3] - xqs[0] * xqs[2]), rz1 = 2.f * (xqs[2] * xqs[3] + xqs[0] * xqs[1]);
+      const float rz2 = 1.f - 2.f * (xqs[1] * xqs[1] + xqs[2] * xqs[2]);
+      if (rz0 * w[0] + rz1 * w[1] + rz2 * w[2] > 0.f) {
+        /* corner k lies above the centre: its mirror 7-k is the one MuJoCo keeps */
+#pragma unroll
+        for (int k = 0; k < 3; k++) w[k] = -w[k];
+      }
+    }
+    float gl[3] = {gp[0] + w[0], gp[1] + w[1], gp[2] + w[2]};
+    quat_rotate(t, xqs, gl);
+    const float rad = box ? 0.f : s0;
+    p[0] = xp[0] + t[0];
+    p[1] = xp[1] + t[1];
+    p[2] = xp[2] + t[2] - rad;
+    dist = p[2];
+    if (cap) {
+      /* the +z axis of the capsule in the world: the rotated offset / half-length, sign of the +end */
+      float u[3];
+      quat_rotate(u, xqs, w);
+      const float ax = slot == 0 ? u[0] : -u[0], ay = slot == 0 ? u[1] : -u[1];
+      const float bn = sqrtf(ax * ax + ay * ay) / s1;
+      const bool dflt = bn < 0.5f;
+      const float inv = dflt ? 0.f : 1.f / (bn * s1);
+      t1x = dflt ? 0.f : ax * inv;
+      t1y = dflt ? 1.f : ay * inv;
+    }
+    slot_ok = box || (cap ? slot < 2 : slot == 0);
   }
-  float gl[3] = {gp[0] + w[0], gp[1] + w[1], gp[2] + w[2]};
-  quat_rotate(t, xqs, gl);
-  const float rad = box ? 0.f : s0;
-  float p[3] = {xp[0] + t[0], xp[1] + t[1], xp[2] + t[2] - rad};
-  const float dist = p[2];
   pos[0] = p[0]; pos[1] = p[1]; pos[2] = p[2] - 0.5f * dist;
   mu = m->floor_friction[0] * s.floor_mu;
-  float t1x = 0.f, t1y = 1.f;
-  if (cap) {
-    /* the +z axis of the capsule in the world: the rotated offset / half-length, sign of the +end */
-    float u[3];
-    quat_rotate(u, xqs, w);
-    const float ax = slot == 0 ? u[0] : -u[0], ay = slot == 0 ? u[1] : -u[1];
-    const float bn = sqrtf(ax * ax + ay * ay) / s1;
-    const bool dflt = bn < 0.5f;
-    const float inv = dflt ? 0.f : 1.f / (bn * s1);
-    t1x = dflt ? 0.f : ax * inv;
-    t1y = dflt ? 1.f : ay * inv;
-  }
   const float sg = (edge & 1) ? -mu : mu;
   /* edges 0/1: n +- mu t1; 2/3: n +- mu t2, t2 = n x t1 = (-t1y, t1x, 0) */
   dir[0] = edge < 2 ? sg * t1x : -sg * t1y;
   dir[1] = edge < 2 ? sg * t1y : sg * t1x;
   dir[2] = 1.f;
-  const bool slot_ok = box || (cap ? slot < 2 : slot == 0);
   return (gvalid && slot_ok) ? dist : 1e30f;
 }
 

@@ -23,9 +23,9 @@ MJCF semantics (XML reference, MuJoCo 3.3.4 [U]):
     inertiafromgeom="true"), the mass and inertia of the body's box / sphere /
     capsule / cylinder / ellipsoid geoms (density or mass, fromto,
     inertiagrouprange), composed about their common centre of mass;
-  * box / capsule (size or fromto) / sphere <geom>s with a nonzero contype or
+  * box / capsule / cylinder (size or fromto) / sphere <geom>s with a nonzero contype or
     conaffinity as floor colliders, up to 4 in document order (the engine's
-    plane-box / plane-capsule / plane-sphere contacts; other colliding geoms
+    plane-box / plane-capsule / plane-cylinder / plane-sphere contacts; other colliding geoms
     are listed in desc["skipped_geoms"] and make zb_create refuse the model), the
     <geom type="plane"> of the worldbody as the floor (friction, solref,
     solimp, margin);
@@ -50,7 +50,7 @@ import numpy as np
 from .model import load_description
 
 # floor colliders the engine has contacts for (type -> sizes) and how many (ZB_MAX_GEOM)
-COLLIDER_TYPES = {"box": 3, "capsule": 2, "sphere": 1}
+COLLIDER_TYPES = {"box": 3, "capsule": 2, "cylinder": 2, "sphere": 1}
 MAX_COLLIDERS = 4
 
 
@@ -370,7 +370,7 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                     continue  # visual only
                 gt = ga.get("type", "sphere")
                 if gt not in COLLIDER_TYPES:
-                    # the engine collides boxes, capsules and spheres with the floor; other colliding
+                    # the engine collides boxes, capsules, cylinders and spheres with the floor; other colliding
                     # geoms are listed so a caller can see what the model leaves out (the count cap,
                     # MAX_COLLIDERS, is applied after the touch sensors pick their geoms, below)
                     desc.setdefault("skipped_geoms", []).append({"name": ga.get("name", ""), "body": name, "type": gt})
@@ -379,7 +379,7 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                 gd = {"name": ga.get("name", f"{name}_geom{len(desc['geoms'])}"), "body": name, "type": gt}
                 gq = orientation(c, ga)
                 if "fromto" in ga:
-                    if gt != "capsule":
+                    if gt not in ("capsule", "cylinder"):
                         raise ValueError(f"geom {gd['name']}: fromto on a {gt} collider")
                     fpos, fR, hl = _fromto_frame(_floats(ga["fromto"], 6))
                     gd["size"] = [_floats(ga["size"])[0], hl]

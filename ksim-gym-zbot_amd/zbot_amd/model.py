@@ -471,11 +471,12 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) 
         m.joint_bias[a] = JOINT_BIASES[a][1]
         m.joint_weight[a] = JOINT_BIASES[a][2]
 
-    gtypes = {"box": (cs.GEOM_BOX, 3), "capsule": (cs.GEOM_CAPSULE, 2), "sphere": (cs.GEOM_SPHERE, 1)}
+    gtypes = {"box": (cs.GEOM_BOX, 3), "capsule": (cs.GEOM_CAPSULE, 2), "cylinder": (cs.GEOM_CYLINDER, 2),
+              "sphere": (cs.GEOM_SPHERE, 1)}
     for gi, gd in enumerate(geoms):
         gt = gd.get("type", "box")
         if gt not in gtypes:
-            raise ValueError(f"geom {gd['name']}: type {gt!r} (box, capsule and sphere collide with the floor)")
+            raise ValueError(f"geom {gd['name']}: type {gt!r} (box, capsule, cylinder and sphere collide with the floor)")
         code, nsize = gtypes[gt]
         if len(gd["size"]) < nsize or any(not (v > 0) for v in gd["size"][:nsize]):
             raise ValueError(f"geom {gd['name']}: a {gt} needs {nsize} positive sizes")

@@ -558,7 +558,13 @@ static void smooth_forces(const ZbModel* m, ZbData* d) {
  *   capsule (mjc_PlaneCapsule): the end spheres, the +half-length end first; tangent frame along
  *     the capsule axis projected on the plane (mjx plane_capsule: +y when that projection is
  *     shorter than 0.5, i.e. the axis is within 30 degrees of the normal);
- *   sphere (mjc_PlaneSphere): one contact.
+ *   sphere (mjc_PlaneSphere): one contact;
+ *   cylinder (mjc_PlaneCylinder): the axis a turned toward the plane, v the radius vector in the
+ *     disk planes toward it (a prj(a) - n normalised to the radius; the geom's x axis times the
+ *     radius when the disks are parallel to the plane), then up to 4 points, each kept within the
+ *     margin, none when the first is not: the near disk's deepest point c + v + a, the far disk's
+ *     c + v - a, and the two points of the near disk 120 degrees away from the first,
+ *     c + a - v / 2 +- v1 (v1 = (v x a) normalised to sqrt(3)/2 of the radius).
  * Contact point: the deepest point moved back along the normal by half the distance. Frames other
  * than the capsule's are mju_makeFrame(+z): t1 = +y, t2 = n x t1 = -x. */
 static void add_contact(const ZbModel* m, ZbData* d, int g, const real p[3], real dist, const real t1[3]) {
@@ -614,6 +620,50 @@ static void collision(const ZbModel* m, ZbData* d) {
       real p[3] = {c[0], c[1], c[2] - sz[0]};
       const real dist = p[2];
       if (dist <= margin) add_contact(m, d, g, p, dist, ty);
+    } else if (m->geom_type[g] == ZB_GEOM_CYLINDER) {
+      /* the plane: normal n = +z through the origin, so dot(x, n) = x[2] */
+      real a[3] = {R[2], R[5], R[8]};
+      real prja = a[2];
+      if (prja > 0) {
+        for (int k = 0; k < 3; k++) a[k] = -a[k];
+        prja = -prja;
+      }
+      const real dist0 = c[2];
+      real v[3] = {a[0] * prja, a[1] * prja, a[2] * prja - 1};
+      const real len = SQRT(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+      if (len >= MINVAL) {
+        for (int k = 0; k < 3; k++) v[k] *= sz[0] / len;
+      } else {
+        v[0] = R[0] * sz[0];
+        v[1] = R[3] * sz[0];
+        v[2] = R[6] * sz[0];
+      }
+      const real prjv = v[2];
+      for (int k = 0; k < 3; k++) a[k] *= sz[1];
+      prja *= sz[1];
+      const real d1 = dist0 + prja + prjv;
+      if (d1 <= margin) {
+        real p[3] = {c[0] + v[0] + a[0], c[1] + v[1] + a[1], c[2] + v[2] + a[2]};
+        add_contact(m, d, g, p, d1, ty);
+        const real d2 = dist0 - prja + prjv;
+        if (d2 <= margin) {
+          real q[3] = {c[0] + v[0] - a[0], c[1] + v[1] - a[1], c[2] + v[2] - a[2]};
+          add_contact(m, d, g, q, d2, ty);
+        }
+        const real d3 = dist0 + prja - (real)0.5 * prjv;
+        if (d3 <= margin) {
+          real v1[3] = {v[1] * a[2] - v[2] * a[1], v[2] * a[0] - v[0] * a[2], v[0] * a[1] - v[1] * a[0]};
+          const real n1 = SQRT(v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2]);
+          const real s1 = n1 > 0 ? sz[0] * SQRT((real)3) * (real)0.5 / n1 : (real)0;
+          for (int k = 0; k < 3; k++) v1[k] *= s1;
+          for (int e = 0; e < 2; e++) {
+            const real sg = e == 0 ? (real)1 : (real)-1;
+            real q[3] = {c[0] + a[0] - (real)0.5 * v[0] + sg * v1[0], c[1] + a[1] - (real)0.5 * v[1] + sg * v1[1],
+                         c[2] + a[2] - (real)0.5 * v[2] + sg * v1[2]};
+            add_contact(m, d, g, q, d3, ty);
+          }
+        }
+      }
     }
   }
 }

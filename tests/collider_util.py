@@ -1,7 +1,7 @@
-"""Floor colliders for the tests: two model variants with colliders beyond the box soles, an
-independent numpy restatement of MuJoCo's plane-box / plane-capsule / plane-sphere contact sets
-(engine_collision_primitive.c mjc_PlaneBox, mjc_PlaneCapsule, mjc_PlaneSphere), and states whose
-colliders touch the floor. Test infrastructure only."""
+"""Floor colliders for the tests: three model variants with colliders beyond the box soles, an
+independent numpy restatement of MuJoCo's plane-box / plane-capsule / plane-cylinder / plane-sphere
+contact sets (engine_collision_primitive.c mjc_PlaneBox, mjc_PlaneCapsule, mjc_PlaneCylinder,
+mjc_PlaneSphere), and states whose colliders touch the floor. Test infrastructure only."""
 
 from __future__ import annotations
 
@@ -51,6 +51,23 @@ def round_desc() -> dict:
     return _variant(edit)
 
 
+def cyl_desc() -> dict:
+    """A cylinder right foot (the touch sensor's zone, axis vertical when the foot is flat), the box
+    left sole and a tilted cylinder on the left shin (3 colliders)."""
+
+    def edit(root):
+        for g in root.iter("geom"):
+            if g.get("name") == "right_foot_sole":
+                g.set("type", "cylinder")
+                g.set("size", "0.03 0.006")
+        for b in root.iter("body"):
+            if b.get("name") == "left_knee_pitch_link":
+                b.append(ET.fromstring('<geom name="left_shin" type="cylinder" size="0.018" '
+                                       'fromto="0 0 -0.02 0.01 0.005 -0.09"/>'))
+
+    return _variant(edit)
+
+
 def _qmat(q) -> np.ndarray:
     w, x, y, z = np.asarray(q, np.float64) / np.linalg.norm(q)
     return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
@@ -92,6 +109,37 @@ def box_corners(c, R, sz, margin=0.0) -> list[tuple[int, float]]:
     return out
 
 
+def cylinder_points(c, R, sz, margin=0.0) -> list[tuple[np.ndarray, float]]:
+    """mjc_PlaneCylinder against the floor z = 0: the axis turned toward the plane (a, scaled to the
+    half-length), the radius vector v in the disk planes pointing down the slope (the geom's x axis
+    when the disks are parallel to the plane); the near disk's deepest point c + v + a, which must
+    be within the margin for any contact, the far disk's c + v - a, and the near disk's two points
+    120 degrees from the first, c + a - v/2 +- sqrt(3)/2 r (v x a)/|v x a|."""
+    r, h = sz[0], sz[1]
+    a = R[:, 2].copy()
+    if a[2] > 0:
+        a = -a
+    n = np.array([0.0, 0.0, 1.0])
+    v = a * a[2] - n
+    ln = np.linalg.norm(v)
+    v = R[:, 0] * r if ln < 1e-15 else v * (r / ln)
+    a = a * h
+    pts = [c + v + a]
+    if pts[0][2] > margin:
+        return []
+    out = [(pts[0], float(pts[0][2]))]
+    far = c + v - a
+    if far[2] <= margin:
+        out.append((far, float(far[2])))
+    w = np.cross(v, a)
+    w = w / np.linalg.norm(w) * r * np.sqrt(3.0) / 2
+    for sg in (1.0, -1.0):
+        q = c + a - 0.5 * v + sg * w
+        if q[2] <= margin:
+            out.append((q, float(q[2])))
+    return out
+
+
 def contacts(cm, qpos, margin=0.0) -> list[list[tuple[np.ndarray, float]]]:
     """Per collider, its floor contacts (point, distance) by MuJoCo's rules: box corners in index
     order (bit 0 x, 1 y, 2 z) below the centre along the normal and within the margin, at most 4;
@@ -107,6 +155,8 @@ def contacts(cm, qpos, margin=0.0) -> list[list[tuple[np.ndarray, float]]]:
                 d = e[2] - sz[0]
                 if d <= margin:
                     cons.append((e, d))
+        elif ty == "cylinder":
+            cons = cylinder_points(c, R, sz, margin)
         else:
             d = c[2] - sz[0]
             if d <= margin:
@@ -125,6 +175,9 @@ def lowest_point(cm, qpos) -> float:
                 z = min(z, c[2] + (R @ loc)[2])
         elif ty == "capsule":
             z = min(z, c[2] - sz[1] * abs(R[2, 2]) - sz[0])
+        elif ty == "cylinder":
+            # the lowest rim point: half-length along the axis plus the radius across it
+            z = min(z, c[2] - sz[1] * abs(R[2, 2]) - sz[0] * np.sqrt(max(0.0, 1.0 - R[2, 2] ** 2)))
         else:
             z = min(z, c[2] - sz[0])
     return float(z)

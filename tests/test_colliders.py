@@ -12,9 +12,12 @@ from zbot_amd import compile_model, default_config
 from zbot_amd import cstructs as cs
 
 
-@pytest.fixture(scope="module", params=["limbs", "round"])
+DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc}
+
+
+@pytest.fixture(scope="module", params=list(DESCS))
 def variant(request):
-    return request.param, compile_model(U.limbs_desc() if request.param == "limbs" else U.round_desc())
+    return request.param, compile_model(DESCS[request.param]())
 
 
 def test_variant_models_compile(variant):
@@ -25,11 +28,17 @@ def test_variant_models_compile(variant):
         assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "right_shin", "left_hand"]
         assert list(m.geom_type)[:4] == [cs.GEOM_BOX, cs.GEOM_BOX, cs.GEOM_BOX, cs.GEOM_CAPSULE]
         np.testing.assert_allclose(list(m.geom_size[3])[:2], [0.012, np.hypot(0.01, 0.06) / 2], rtol=1e-6)
-    else:
+    elif name == "round":
         assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "head_ball"]
         assert list(m.geom_type)[:3] == [cs.GEOM_CAPSULE, cs.GEOM_CAPSULE, cs.GEOM_SPHERE]
         # the touch sensors read the capsule feet
         assert (m.geom_right_foot, m.geom_left_foot) == (0, 1)
+    else:
+        assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "left_shin"]
+        assert list(m.geom_type)[:3] == [cs.GEOM_CYLINDER, cs.GEOM_BOX, cs.GEOM_CYLINDER]
+        np.testing.assert_allclose(list(m.geom_size[0])[:2], [0.03, 0.006], rtol=1e-6)
+        np.testing.assert_allclose(list(m.geom_size[2])[:2], [0.018, np.sqrt(0.01**2 + 0.005**2 + 0.07**2) / 2],
+                                   rtol=1e-6)
     assert m.nskip_geom == 0
     for g in range(m.ngeom):
         assert m.geom_lastdof[g] == cm.bodies[m.geom_body[g]].lastdof
@@ -94,3 +103,42 @@ def test_limbs_asset_is_the_test_variant():
         assert f.read() == to_mjcf(U.limbs_desc()) + "\n"
     a, b = compile_model(load_mjcf(path)).cmodel, compile_model(U.limbs_desc()).cmodel
     assert bytes(a) == bytes(b)
+
+
+def test_cylinder_known_answers():
+    """Known answers for the cylinder rule (mjc_PlaneCylinder; pins the numpy restatement that
+    test_oracle_contact_sets_match_mujoco_rules checks the oracle against). Radius 0.02, half-length
+    0.05, centre height h:
+    * upright (axis along z), h = 0.049: the bottom disk is 1 mm under the floor; its points at 0
+      (the x axis, the disks being parallel to the plane) and +-120 degrees, all at -0.001; the top
+      disk is far above;
+    * lying (axis along x), h = 0.019: the lowest line of the barrel, its two ends at -0.001; the
+      120-degree points are 1.5 r higher;
+    * tilted 30 degrees from the floor about y, h = 0.02 * cos30 + 0.05 * sin30 - 0.001: only the
+      near disk's deepest point touches; the 120-degree pair lies 1.5 * 0.02 * cos30 - 0.001 above the
+      floor (a margin of 0.03 brings it in) and the far disk's point 0.05 * 2 * sin30 - 0.001 (0.06)."""
+    r, h = 0.02, 0.05
+    up = U.cylinder_points(np.array([0.0, 0.0, 0.049]), np.eye(3), [r, h])
+    assert len(up) == 3
+    np.testing.assert_allclose([d for _, d in up], [-0.001] * 3, atol=1e-12)
+    np.testing.assert_allclose(up[0][0], [r, 0.0, -0.001], atol=1e-12)
+    ang = sorted(np.degrees(np.arctan2(p[1], p[0])) for p, _ in up)
+    np.testing.assert_allclose(ang, [-120.0, 0.0, 120.0], atol=1e-9)
+    Ry = np.array([[0.0, 0.0, 1.0], [0.0, 1.0, 0.0], [-1.0, 0.0, 0.0]])  # local z -> world x
+    lying = U.cylinder_points(np.array([0.0, 0.0, 0.019]), Ry, [r, h])
+    assert len(lying) == 2
+    np.testing.assert_allclose(sorted(p[0] for p, _ in lying), [-h, h], atol=1e-12)
+    np.testing.assert_allclose([d for _, d in lying], [-0.001, -0.001], atol=1e-12)
+    t = np.radians(60.0)  # axis 60 degrees from vertical = 30 degrees from the floor
+    Rt = np.array([[np.cos(t), 0.0, np.sin(t)], [0.0, 1.0, 0.0], [-np.sin(t), 0.0, np.cos(t)]])
+    c30, s30 = np.cos(np.radians(30.0)), np.sin(np.radians(30.0))
+    z0 = r * c30 + h * s30 - 0.001
+    one = U.cylinder_points(np.array([0.0, 0.0, z0]), Rt, [r, h])
+    assert len(one) == 1
+    np.testing.assert_allclose(one[0][1], -0.001, atol=1e-12)
+    three = U.cylinder_points(np.array([0.0, 0.0, z0]), Rt, [r, h], margin=0.03)
+    np.testing.assert_allclose([d for _, d in three], [-0.001, 1.5 * r * c30 - 0.001, 1.5 * r * c30 - 0.001], atol=1e-12)
+    four = U.cylinder_points(np.array([0.0, 0.0, z0]), Rt, [r, h], margin=0.06)
+    assert len(four) == 4
+    np.testing.assert_allclose([d for _, d in four],
+                               [-0.001, 2 * h * s30 - 0.001, 1.5 * r * c30 - 0.001, 1.5 * r * c30 - 0.001], atol=1e-12)

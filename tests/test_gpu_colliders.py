@@ -22,9 +22,12 @@ def torch_gpu():
     return torch
 
 
-@pytest.fixture(scope="module", params=["limbs", "round"])
+DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc}
+
+
+@pytest.fixture(scope="module", params=list(DESCS))
 def variant(request):
-    return request.param, compile_model(U.limbs_desc() if request.param == "limbs" else U.round_desc())
+    return request.param, compile_model(DESCS[request.param]())
 
 
 def contact_env(O, cm, cfg, n, seed):
