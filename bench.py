@@ -218,15 +218,15 @@ def bench_c2_rollout(eng, n: int, T: int, dev, rank: int, world: int, sigma: flo
     eng.reset(extras=False)
     eng.get_stats(clear=True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     rollout()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     wall = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
     wall = float(wall.item())
     eng.check()
@@ -252,16 +252,16 @@ def _timed_steps(step, steps: int, warmup: int, dev, world: int) -> float:
     for t in range(warmup):
         step(t)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     for t in range(steps):
         step(warmup + t)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     wall = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
     return float(wall.item())
 
@@ -490,16 +490,16 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int, inlo
 
     once()  # first use of every kernel and of the moment collective, untimed
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         res = once()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     wall = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)
     wall = float(wall.item())
     assert bool(torch.isfinite(res.advantages_t).all())
@@ -551,6 +551,10 @@ def main() -> None:
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo rehearses the "
                          "multi-rank path on a one-GPU box, ranks sharing device local_rank %% device_count)")
+    ap.add_argument("--init-dist", action="store_true",
+                    help="initialise the process group even at WORLD_SIZE 1 (under torch.distributed.run with one "
+                         "rank): the barriers, the max-over-ranks timer and the statistics all_gather then run "
+                         "through RCCL on a one-GPU box")
     args = ap.parse_args()
 
     import torch  # noqa: PLC0415
@@ -566,7 +570,7 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or args.init_dist:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -601,7 +605,7 @@ def main() -> None:
         # per-rollout episode statistics: per-GPU partials summed in fixed env order,
         # then an RCCL all_gather and a fixed rank-order sum (bit-reproducible)
         part = eng.get_stats(clear=False).double().sum(0)
-        if world > 1:
+        if dist.is_initialized():
             allp = [torch.zeros_like(part) for _ in range(world)]
             dist.all_gather(allp, part)
             return torch.stack(allp).sum(0)
@@ -651,7 +655,7 @@ def main() -> None:
             a.record(stream)
             b.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -667,12 +671,12 @@ def main() -> None:
         eng.join()
     total_stats = reduce_stats()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     el_t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     elapsed = float(el_t.item())
 
@@ -774,6 +778,7 @@ def main() -> None:
                         "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 lane-FLOP; the binding resource of this "
                         "latency/VALU-bound kernel",
             },
+            "process_group": dist.get_backend() if dist.is_initialized() else None,
             "episode_stats": {
                 "episodes_done": float(total_stats[2].item()),
                 "mean_return": float((total_stats[0] / total_stats[2].clamp(min=1)).item()),
@@ -801,7 +806,7 @@ def main() -> None:
                 # the same C1 shape on the GPU and on the CPU twin, in one run
                 out["c1_gpu"]["vs_cpu_baseline_c1"] = out["c1_gpu"]["env_steps_per_s"] / c1cpu["value"]
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
