@@ -66,7 +66,8 @@ void zb_default_config(ZbEnvConfig* cfg);
  * (body 1, free joint) branches; nu = 20 hinge actuators, nv = 26; the free
  * joint's 6 dofs form the root of the dof tree and every limb is an
  * unbranched chain of consecutive dofs of at most 6 (dof depth <= 12); body
- * depth <= 8; 1 to 4 floor colliders (boxes, capsules, cylinders, spheres; model
+ * depth <= 8; 1 to 4 floor colliders (boxes, capsules, cylinders, spheres,
+ * ellipsoids; model
  * nskip_geom = 0). Exactly two box colliders (the soles) run the two-sole
  * kernels; any other collider set runs the general-collider instantiation
  * (a second bank of 32 contact rows, larger LDS).

@@ -38,7 +38,7 @@ extern "C" {
 #define ZB_MAX_GEOM  4   /* floor colliders */
 #define ZB_MAX_SITE  8
 #define ZB_MAX_ACT   32
-#define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-cylinder 4, plane-capsule 2, plane-sphere 1 */
+#define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-cylinder 4, plane-capsule 2, plane-sphere / -ellipsoid 1 */
 #define ZB_MAX_CON  (ZB_MAX_GEOM * ZB_CON_PER_GEOM)
 
 /* joint types (mjtJoint values where they exist) */
@@ -49,6 +49,7 @@ extern "C" {
 /* collider types (mjtGeom values) */
 #define ZB_GEOM_SPHERE  2
 #define ZB_GEOM_CAPSULE 3
+#define ZB_GEOM_ELLIPSOID 4
 #define ZB_GEOM_CYLINDER 5
 #define ZB_GEOM_BOX     6
 

@@ -1565,7 +1565,9 @@ __device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& g
  *   capsule (mjc_PlaneCapsule, XG): slots 0 / 1 = the sphere at the +/- half-length end, tangent
  *     frame along the axis projected on the plane (mjx plane_capsule: +y when that projection is
  *     shorter than 0.5);
- *   sphere (mjc_PlaneSphere, XG): slot 0.
+ *   sphere (mjc_PlaneSphere, XG): slot 0;
+ *   ellipsoid (mjc_PlaneEllipsoid, XG): slot 0, the support point along -n;
+ *   cylinder (mjc_PlaneCylinder, XG): slots 0-3 (below).
  * Sets the contact point (the deepest point moved back by half the distance), the pyramid edge
  * direction n +- mu t (t1 = +y, t2 = n x t1 = -x for boxes and spheres: mju_makeFrame(+z)) and the
  * friction; returns the signed distance, 1e30 where the slot holds no contact. Recomputed by the
@@ -1584,7 +1586,8 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
 #pragma unroll
   for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
   const int ty = XG ? m->geom_type[g] : ZB_GEOM_BOX;
-  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE, cyl = XG && ty == ZB_GEOM_CYLINDER;
+  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE, cyl = XG && ty == ZB_GEOM_CYLINDER,
+             ell = XG && ty == ZB_GEOM_ELLIPSOID;
   /* the lane's point relative to the geom centre, geom frame -> body frame -> world */
   float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
   float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
@@ -1634,6 +1637,26 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
     p[2] = c2 + svv * v[2] + sa * a[2] + s1v * v1[2];
     dist = slot == 0 ? d1 : (slot == 1 ? c2 - prja + prjv : c2 + prja - 0.5f * prjv);
     slot_ok = d1 <= m->floor_margin;
+  } else if (ell) {
+    /* mjc_PlaneEllipsoid (oracle collision()): n = +z taken into the geom frame (body, then geom
+       rotation inverted), sn = s .* n_g, the support point -s .* sn / |sn| back to the world */
+    const float ez[3] = {0.f, 0.f, 1.f};
+    const float xqc[4] = {xqs[0], -xqs[1], -xqs[2], -xqs[3]}, gqc[4] = {gq[0], -gq[1], -gq[2], -gq[3]};
+    float nb[3], ng[3];
+    quat_rotate(nb, xqc, ez);
+    quat_rotate(ng, gqc, nb);
+    const float sn0 = s0 * ng[0], sn1 = s1 * ng[1], sn2 = s2 * ng[2];
+    const float inv = 1.f / sqrtf(sn0 * sn0 + sn1 * sn1 + sn2 * sn2);
+    const float loc[3] = {-s0 * sn0 * inv, -s1 * sn1 * inv, -s2 * sn2 * inv};
+    float w[3], t[3];
+    quat_rotate(w, gq, loc);
+    const float gl[3] = {gp[0] + w[0], gp[1] + w[1], gp[2] + w[2]};
+    quat_rotate(t, xqs, gl);
+    p[0] = xp[0] + t[0];
+    p[1] = xp[1] + t[1];
+    p[2] = xp[2] + t[2];
+    dist = p[2];
+    slot_ok = slot == 0;
   } else {
     float v[3];
     if (box) {

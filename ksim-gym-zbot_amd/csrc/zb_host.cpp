@@ -102,8 +102,8 @@ int check_model(const ZbModel* m) {
     return fail(ZB_EMODEL, "ngeom=%d: 1 to %d floor colliders", m->ngeom, ZB_MAX_GEOM);
   for (int g = 0; g < m->ngeom; g++) {
     const int ty = m->geom_type[g];
-    const int nsz = ty == ZB_GEOM_BOX ? 3 : (ty == ZB_GEOM_CAPSULE || ty == ZB_GEOM_CYLINDER) ? 2 : ty == ZB_GEOM_SPHERE ? 1 : 0;
-    if (nsz == 0) return fail(ZB_EMODEL, "geom %d: type %d (box 6, cylinder 5, capsule 3, sphere 2)", g, ty);
+    const int nsz = (ty == ZB_GEOM_BOX || ty == ZB_GEOM_ELLIPSOID) ? 3 : (ty == ZB_GEOM_CAPSULE || ty == ZB_GEOM_CYLINDER) ? 2 : ty == ZB_GEOM_SPHERE ? 1 : 0;
+    if (nsz == 0) return fail(ZB_EMODEL, "geom %d: type %d (box 6, cylinder 5, ellipsoid 4, capsule 3, sphere 2)", g, ty);
     for (int k = 0; k < nsz; k++)
       if (!(m->geom_size[g][k] > 0.f)) return fail(ZB_EMODEL, "geom %d: size[%d] must be positive", g, k);
   }

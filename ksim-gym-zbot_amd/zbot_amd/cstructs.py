@@ -21,7 +21,7 @@ MODEL_VERSION = 6
 JNT_NONE = -1
 JNT_FREE = 0
 JNT_HINGE = 3
-GEOM_SPHERE, GEOM_CAPSULE, GEOM_CYLINDER, GEOM_BOX = 2, 3, 5, 6
+GEOM_SPHERE, GEOM_CAPSULE, GEOM_ELLIPSOID, GEOM_CYLINDER, GEOM_BOX = 2, 3, 4, 5, 6
 
 # zbot_layout.h
 NJ = 20

@@ -50,7 +50,7 @@ import numpy as np
 from .model import load_description
 
 # floor colliders the engine has contacts for (type -> sizes) and how many (ZB_MAX_GEOM)
-COLLIDER_TYPES = {"box": 3, "capsule": 2, "cylinder": 2, "sphere": 1}
+COLLIDER_TYPES = {"box": 3, "capsule": 2, "cylinder": 2, "sphere": 1, "ellipsoid": 3}
 MAX_COLLIDERS = 4
 
 
@@ -370,7 +370,7 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                     continue  # visual only
                 gt = ga.get("type", "sphere")
                 if gt not in COLLIDER_TYPES:
-                    # the engine collides boxes, capsules, cylinders and spheres with the floor; other colliding
+                    # the engine collides boxes, capsules, cylinders, spheres and ellipsoids with the floor; other colliding
                     # geoms are listed so a caller can see what the model leaves out (the count cap,
                     # MAX_COLLIDERS, is applied after the touch sensors pick their geoms, below)
                     desc.setdefault("skipped_geoms", []).append({"name": ga.get("name", ""), "body": name, "type": gt})
@@ -379,10 +379,14 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                 gd = {"name": ga.get("name", f"{name}_geom{len(desc['geoms'])}"), "body": name, "type": gt}
                 gq = orientation(c, ga)
                 if "fromto" in ga:
-                    if gt not in ("capsule", "cylinder"):
+                    if gt == "sphere":
                         raise ValueError(f"geom {gd['name']}: fromto on a {gt} collider")
                     fpos, fR, hl = _fromto_frame(_floats(ga["fromto"], 6))
-                    gd["size"] = [_floats(ga["size"])[0], hl]
+                    # the segment's half-length is the last size (capsule / cylinder: the second)
+                    sz = _floats(ga["size"])
+                    if len(sz) < nsz - 1:
+                        raise ValueError(f"geom {gd['name']}: a {gt} with fromto needs {nsz - 1} sizes")
+                    gd["size"] = sz[:nsz - 1] + [hl]
                     gd["pos"] = [float(v) for v in fpos]
                     gq = _mat_quat(fR)
                 else:

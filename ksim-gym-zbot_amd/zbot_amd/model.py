@@ -472,7 +472,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) 
         m.joint_weight[a] = JOINT_BIASES[a][2]
 
     gtypes = {"box": (cs.GEOM_BOX, 3), "capsule": (cs.GEOM_CAPSULE, 2), "cylinder": (cs.GEOM_CYLINDER, 2),
-              "sphere": (cs.GEOM_SPHERE, 1)}
+              "sphere": (cs.GEOM_SPHERE, 1), "ellipsoid": (cs.GEOM_ELLIPSOID, 3)}
     for gi, gd in enumerate(geoms):
         gt = gd.get("type", "box")
         if gt not in gtypes:

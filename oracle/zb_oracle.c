@@ -564,7 +564,9 @@ static void smooth_forces(const ZbModel* m, ZbData* d) {
  *     radius when the disks are parallel to the plane), then up to 4 points, each kept within the
  *     margin, none when the first is not: the near disk's deepest point c + v + a, the far disk's
  *     c + v - a, and the two points of the near disk 120 degrees away from the first,
- *     c + a - v / 2 +- v1 (v1 = (v x a) normalised to sqrt(3)/2 of the radius).
+ *     c + a - v / 2 +- v1 (v1 = (v x a) normalised to sqrt(3)/2 of the radius);
+ *   ellipsoid (mjc_PlaneEllipsoid): one contact at the support point along -n, in the geom frame
+ *     -s .* sn / |sn| with sn = s .* (R' n) (s the three semi-axes).
  * Contact point: the deepest point moved back along the normal by half the distance. Frames other
  * than the capsule's are mju_makeFrame(+z): t1 = +y, t2 = n x t1 = -x. */
 static void add_contact(const ZbModel* m, ZbData* d, int g, const real p[3], real dist, const real t1[3]) {
@@ -618,6 +620,16 @@ static void collision(const ZbModel* m, ZbData* d) {
       }
     } else if (m->geom_type[g] == ZB_GEOM_SPHERE) {
       real p[3] = {c[0], c[1], c[2] - sz[0]};
+      const real dist = p[2];
+      if (dist <= margin) add_contact(m, d, g, p, dist, ty);
+    } else if (m->geom_type[g] == ZB_GEOM_ELLIPSOID) {
+      /* R' n with n = +z: the z components of the geom's axes, row 2 of R */
+      real sn[3], loc[3], w[3];
+      for (int k = 0; k < 3; k++) sn[k] = sz[k] * R[6 + k];
+      const real nrm = SQRT(sn[0] * sn[0] + sn[1] * sn[1] + sn[2] * sn[2]);
+      for (int k = 0; k < 3; k++) loc[k] = -sz[k] * sn[k] / nrm;
+      mulmv3(w, R, loc);
+      real p[3] = {c[0] + w[0], c[1] + w[1], c[2] + w[2]};
       const real dist = p[2];
       if (dist <= margin) add_contact(m, d, g, p, dist, ty);
     } else if (m->geom_type[g] == ZB_GEOM_CYLINDER) {

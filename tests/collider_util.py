@@ -1,7 +1,7 @@
 """Floor colliders for the tests: three model variants with colliders beyond the box soles, an
-independent numpy restatement of MuJoCo's plane-box / plane-capsule / plane-cylinder / plane-sphere
-contact sets (engine_collision_primitive.c mjc_PlaneBox, mjc_PlaneCapsule, mjc_PlaneCylinder,
-mjc_PlaneSphere), and states whose colliders touch the floor. Test infrastructure only."""
+independent numpy restatement of MuJoCo's plane-box / plane-capsule / plane-cylinder / plane-sphere /
+plane-ellipsoid contact sets (engine_collision_primitive.c mjc_PlaneBox, mjc_PlaneCapsule,
+mjc_PlaneCylinder, mjc_PlaneSphere, mjc_PlaneEllipsoid), and states whose colliders touch the floor. Test infrastructure only."""
 
 from __future__ import annotations
 
@@ -53,7 +53,8 @@ def round_desc() -> dict:
 
 def cyl_desc() -> dict:
     """A cylinder right foot (the touch sensor's zone, axis vertical when the foot is flat), the box
-    left sole and a tilted cylinder on the left shin (3 colliders)."""
+    left sole, a tilted cylinder on the left shin and a tilted ellipsoid on the right hand
+    (4 colliders)."""
 
     def edit(root):
         for g in root.iter("geom"):
@@ -64,6 +65,9 @@ def cyl_desc() -> dict:
             if b.get("name") == "left_knee_pitch_link":
                 b.append(ET.fromstring('<geom name="left_shin" type="cylinder" size="0.018" '
                                        'fromto="0 0 -0.02 0.01 0.005 -0.09"/>'))
+            if b.get("name") == "right_gripper_roll_link":
+                b.append(ET.fromstring('<geom name="right_hand" type="ellipsoid" size="0.012 0.02 0.035" '
+                                       'pos="0 0 -0.03" euler="0.3 -0.2 0.5"/>'))
 
     return _variant(edit)
 
@@ -140,6 +144,15 @@ def cylinder_points(c, R, sz, margin=0.0) -> list[tuple[np.ndarray, float]]:
     return out
 
 
+def ellipsoid_point(c, R, sz) -> tuple[np.ndarray, float]:
+    """mjc_PlaneEllipsoid against the floor z = 0: the support point along -n, R (-s .* sn / |sn|)
+    with sn = s .* (R' n)."""
+    s = np.asarray(sz[:3], np.float64)
+    sn = s * R[2, :]
+    p = c + R @ (-s * sn / np.linalg.norm(sn))
+    return p, float(p[2])
+
+
 def contacts(cm, qpos, margin=0.0) -> list[list[tuple[np.ndarray, float]]]:
     """Per collider, its floor contacts (point, distance) by MuJoCo's rules: box corners in index
     order (bit 0 x, 1 y, 2 z) below the centre along the normal and within the margin, at most 4;
@@ -157,6 +170,10 @@ def contacts(cm, qpos, margin=0.0) -> list[list[tuple[np.ndarray, float]]]:
                     cons.append((e, d))
         elif ty == "cylinder":
             cons = cylinder_points(c, R, sz, margin)
+        elif ty == "ellipsoid":
+            p, d = ellipsoid_point(c, R, sz)
+            if d <= margin:
+                cons.append((p, d))
         else:
             d = c[2] - sz[0]
             if d <= margin:
@@ -178,6 +195,8 @@ def lowest_point(cm, qpos) -> float:
         elif ty == "cylinder":
             # the lowest rim point: half-length along the axis plus the radius across it
             z = min(z, c[2] - sz[1] * abs(R[2, 2]) - sz[0] * np.sqrt(max(0.0, 1.0 - R[2, 2] ** 2)))
+        elif ty == "ellipsoid":
+            z = min(z, ellipsoid_point(c, R, sz)[1])
         else:
             z = min(z, c[2] - sz[0])
     return float(z)

@@ -34,8 +34,9 @@ def test_variant_models_compile(variant):
         # the touch sensors read the capsule feet
         assert (m.geom_right_foot, m.geom_left_foot) == (0, 1)
     else:
-        assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "left_shin"]
-        assert list(m.geom_type)[:3] == [cs.GEOM_CYLINDER, cs.GEOM_BOX, cs.GEOM_CYLINDER]
+        assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "left_shin", "right_hand"]
+        assert list(m.geom_type)[:4] == [cs.GEOM_CYLINDER, cs.GEOM_BOX, cs.GEOM_CYLINDER, cs.GEOM_ELLIPSOID]
+        np.testing.assert_allclose(list(m.geom_size[3])[:3], [0.012, 0.02, 0.035], rtol=1e-6)
         np.testing.assert_allclose(list(m.geom_size[0])[:2], [0.03, 0.006], rtol=1e-6)
         np.testing.assert_allclose(list(m.geom_size[2])[:2], [0.018, np.sqrt(0.01**2 + 0.005**2 + 0.07**2) / 2],
                                    rtol=1e-6)
@@ -60,7 +61,8 @@ def test_zb_create_accepts_the_variants(variant):
 def test_oracle_contact_sets_match_mujoco_rules(variant, oracle_mod, precision):
     """Over states with every collider type touching the floor, the oracle's contact count equals
     the numpy restatement's (box: the corners below the centre within the margin, at most 4;
-    capsule: the end spheres; sphere), and some contacts of every collider occur."""
+    capsule: the end spheres; cylinder: up to four rim points; sphere; ellipsoid: the support
+    point), and some contacts of every collider occur."""
     name, cm = variant
     cfg = default_config()
     qs = U.touching_states(cm, 96, seed=3).astype(np.float32)
@@ -142,3 +144,28 @@ def test_cylinder_known_answers():
     assert len(four) == 4
     np.testing.assert_allclose([d for _, d in four],
                                [-0.001, 2 * h * s30 - 0.001, 1.5 * r * c30 - 0.001, 1.5 * r * c30 - 0.001], atol=1e-12)
+
+
+def test_ellipsoid_known_answers():
+    """Known answers for the ellipsoid rule (mjc_PlaneEllipsoid, the support point along -n): semi-axes
+    (a, b, c) = (0.03, 0.01, 0.02), centre height h.
+    * axis-aligned: the point (0, 0, h - c);
+    * rolled 90 degrees about x (local y vertical): (0, 0, h - b);
+    * pitched by t about y: depth sqrt(a^2 sin^2 t + c^2 cos^2 t) below the centre, at
+      x = (a^2 - c^2) sin t cos t / that depth (the tangent point of the tilted ellipse)."""
+    a, b, c, h = 0.03, 0.01, 0.02, 0.1
+    p, d = U.ellipsoid_point(np.array([0.0, 0.0, h]), np.eye(3), [a, b, c])
+    np.testing.assert_allclose(p, [0.0, 0.0, h - c], atol=1e-15)
+    assert d == pytest.approx(h - c)
+    Rx = np.array([[1.0, 0.0, 0.0], [0.0, 0.0, -1.0], [0.0, 1.0, 0.0]])
+    p, d = U.ellipsoid_point(np.array([0.0, 0.0, h]), Rx, [a, b, c])
+    np.testing.assert_allclose(p, [0.0, 0.0, h - b], atol=1e-15)
+    t = np.radians(30.0)
+    Ry = np.array([[np.cos(t), 0.0, np.sin(t)], [0.0, 1.0, 0.0], [-np.sin(t), 0.0, np.cos(t)]])
+    p, d = U.ellipsoid_point(np.array([0.0, 0.0, h]), Ry, [a, b, c])
+    dep = np.sqrt(a * a * np.sin(t) ** 2 + c * c * np.cos(t) ** 2)
+    np.testing.assert_allclose(p, [(a * a - c * c) * np.sin(t) * np.cos(t) / dep, 0.0, h - dep], atol=1e-15)
+    # the same point is the lowest of a dense sample of the surface
+    u, v = np.meshgrid(np.linspace(0, 2 * np.pi, 721), np.linspace(0, np.pi, 361))
+    surf = Ry @ np.stack([a * np.cos(u) * np.sin(v), b * np.sin(u) * np.sin(v), c * np.cos(v)]).reshape(3, -1)
+    assert surf[2].min() + h == pytest.approx(d, abs=1e-6)

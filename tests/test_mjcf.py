@@ -393,10 +393,13 @@ def test_colliders_are_parsed_and_unsupported_ones_reported():
                   "<geom name='shin' type='capsule' size='0.01' fromto='0 0 0 0 0.06 -0.08'/>"
                   "<geom name='hand' type='sphere' size='0.02' pos='0.1 0 0'/>"
                   "<geom name='cyl' type='cylinder' size='0.01 0.05 0.3'/>"
-                  "<geom name='ell' type='ellipsoid' size='0.01 0.02 0.03'/>"
+                  "<geom name='ell' type='ellipsoid' size='0.01 0.02 0.03' fromto='0 0 0 0 0 -0.1'/>"
+                  "<geom name='foot' type='mesh' mesh='m'/>"
                   "<geom name='vis' type='mesh' mesh='m' contype='0' conaffinity='0'/></body></worldbody></mujoco>")
-    assert b["skipped_geoms"] == [{"name": "ell", "body": "b", "type": "ellipsoid"}]
-    shin, hand, cyl = b["geoms"]
+    assert b["skipped_geoms"] == [{"name": "foot", "body": "b", "type": "mesh"}]
+    shin, hand, cyl, ell = b["geoms"]
+    # an ellipsoid with fromto: the two semi-axes across, the segment's half-length along
+    np.testing.assert_allclose(ell["size"], [0.01, 0.02, 0.05])
     # a cylinder keeps its radius and half-length (MuJoCo's third size is unused)
     assert cyl == {"name": "cyl", "body": "b", "type": "cylinder", "size": [0.01, 0.05]}
     assert shin["type"] == "capsule" and hand == {"name": "hand", "body": "b", "type": "sphere", "size": [0.02],
@@ -439,10 +442,10 @@ def test_missing_file_is_reported():
 
 
 def test_skipped_colliders_are_rejected_by_zb_create():
-    """A collider the engine has no floor contact for (an ellipsoid here; or a fifth collider) is not
+    """A collider the engine has no floor contact for (a mesh here; or a fifth collider) is not
     dropped silently: zb_create rejects the model (ZB_EMODEL, nskip_geom); compile_model(...,
     drop_colliders=True) drops it knowingly (missing item 3). Supported extra colliders
-    (a capsule or, since round 4, a cylinder shin) pass validation."""
+    (a capsule or, since round 4, a cylinder or an ellipsoid shin) pass validation."""
     import ctypes as C
     import xml.etree.ElementTree as ET
 
@@ -454,21 +457,21 @@ def test_skipped_colliders_are_rejected_by_zb_create():
         for b in root.iter("body"):
             if "knee" in b.get("name"):
                 shape = ('size="0.015 0.02 0.04" pos="0 0 -0.04"' if gtype == "ellipsoid"
-                         else 'size="0.015" fromto="0 0 0 0 0 -0.08"')
+                         else 'mesh="shin"' if gtype == "mesh" else 'size="0.015" fromto="0 0 0 0 0 -0.08"')
                 b.append(ET.fromstring(f'<geom name="shin_col" type="{gtype}" {shape} mass="0"/>'))
                 break
         return load_mjcf(ET.tostring(root, encoding="unicode"))
 
     L = E.load_library()
     h = C.c_void_p()
-    desc = with_shin("ellipsoid")
+    desc = with_shin("mesh")
     assert [g["name"] for g in desc["skipped_geoms"]] == ["shin_col"]
     cm = compile_model(desc)
     assert cm.cmodel.nskip_geom == 1
     rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
     assert rc == -4 and b"colliding geoms" in L.zb_last_error()
     for cm in (compile_model(desc, drop_colliders=True), compile_model(with_shin("capsule")),
-               compile_model(with_shin("cylinder"))):
+               compile_model(with_shin("cylinder")), compile_model(with_shin("ellipsoid"))):
         assert cm.cmodel.nskip_geom == 0
         rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
         assert rc != -4, L.zb_last_error()  # validation passes (no device here: -2)
