@@ -160,7 +160,10 @@ typedef struct ZbModel {
   int32_t  nskip_geom;                 /* colliding geoms of the source model the engine cannot
                                           collide (other types, or past ZB_MAX_GEOM): zb_create
                                           rejects nskip_geom > 0 */
-  int32_t  pad_tab;
+  int32_t  nskip_pair;                 /* robot geom pairs the source model collides with each
+                                          other (contype / conaffinity, MuJoCo's filters): the
+                                          engine has floor contacts only, so zb_create rejects
+                                          nskip_pair > 0 */
   int32_t  body_nchild[ZB_MAX_BODY];
   int32_t  body_child[ZB_MAX_BODY][8]; /* -1 padded */
   int32_t  depth_maxchild[16];         /* max #children over bodies at a depth */

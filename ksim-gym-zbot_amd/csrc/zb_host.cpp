@@ -95,6 +95,10 @@ int check_model(const ZbModel* m) {
     return fail(ZB_EMODEL, "the source model has %d colliding geoms the engine does not collide with the floor (it "
                            "collides the 2 box soles): compile_model(..., drop_colliders=True) to simulate without "
                            "them knowingly", m->nskip_geom);
+  if (m->nskip_pair != 0)
+    return fail(ZB_EMODEL, "the source model collides %d pairs of its own geoms with each other; the engine has "
+                           "floor contacts only: compile_model(..., drop_self_contacts=True) to simulate without "
+                           "them knowingly", m->nskip_pair);
   if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
   /* colliders: two banks of 32 contact-row lanes, 16 rows (4 contacts x 4 pyramid edges) per geom */

@@ -199,7 +199,7 @@ class ZbModel(C.Structure):
         ("max_body_depth", C.c_int32),
         ("mrow_size", C.c_int32),
         ("nskip_geom", C.c_int32),
-        ("pad_tab", C.c_int32),
+        ("nskip_pair", C.c_int32),
         ("body_nchild", _i(MAX_BODY)),
         ("body_child", _i(MAX_BODY, 8)),
         ("depth_maxchild", _i(16)),

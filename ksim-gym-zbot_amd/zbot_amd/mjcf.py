@@ -23,12 +23,16 @@ MJCF semantics (XML reference, MuJoCo 3.3.4 [U]):
     inertiafromgeom="true"), the mass and inertia of the body's box / sphere /
     capsule / cylinder / ellipsoid geoms (density or mass, fromto,
     inertiagrouprange), composed about their common centre of mass;
-  * box / capsule / cylinder (size or fromto) / sphere <geom>s with a nonzero contype or
-    conaffinity as floor colliders, up to 4 in document order (the engine's
-    plane-box / plane-capsule / plane-cylinder / plane-sphere contacts; other colliding geoms
-    are listed in desc["skipped_geoms"] and make zb_create refuse the model), the
-    <geom type="plane"> of the worldbody as the floor (friction, solref,
-    solimp, margin);
+  * box / capsule / cylinder / ellipsoid (size or fromto) / sphere <geom>s whose
+    contype / conaffinity pass MuJoCo's test against the floor's
+    ((ct1 & ca2) || (ct2 & ca1)) as floor colliders, up to 4 in document order
+    (the engine's plane-box / -capsule / -cylinder / -sphere / -ellipsoid contacts;
+    other such geoms are listed in desc["skipped_geoms"] and make zb_create refuse
+    the model), the <geom type="plane"> of the worldbody as the floor (friction,
+    solref, solimp, margin, contype, conaffinity);
+  * the robot's own geom pairs MuJoCo would collide (self_pairs below): listed in
+    desc["self_pairs"]; the engine has floor contacts only, so zb_create refuses
+    such a model unless compiled with drop_self_contacts=True;
   * <motor> / plain <general> actuators (gear, ctrlrange, ctrllimited), one per
     hinge; <site>s and <touch> sensors; <option timestep gravity>.
 The servo model (FeetechParams, train.py:1121-1134) is not part of MJCF: it
@@ -226,6 +230,43 @@ class _Defaults:
         return out
 
 
+def self_pairs(geoms: list[dict], parent: dict[str, str], welded: set[str], excludes: set[frozenset],
+               explicit: list[tuple[str, str]] = (), filterparent: bool = True) -> list[list[str]]:
+    """Robot geom pairs MuJoCo's collision filter passes (engine_collision_driver.c, as documented in
+    the MJCF reference's "Contact" section): geoms g1, g2 with (contype1 & conaffinity2) or
+    (contype2 & conaffinity1) nonzero, on different weld bodies (a body without a joint is welded to
+    its parent), not a weld body and its weld parent (filterparent, unless the parent is the world),
+    not <contact><exclude>-d; plus the explicit <contact><pair>s. geoms: {"name", "body", "contype",
+    "conaffinity"}; parent: body -> parent body; welded: bodies without a joint."""
+
+    def weld(b):
+        while b != "world" and b in welded:
+            b = parent[b]
+        return b
+
+    out, seen = [], set()
+    for i, g1 in enumerate(geoms):
+        for g2 in geoms[i + 1:]:
+            if not ((g1["contype"] & g2["conaffinity"]) or (g2["contype"] & g1["conaffinity"])):
+                continue
+            w1, w2 = weld(g1["body"]), weld(g2["body"])
+            if w1 == w2:
+                continue
+            p1 = weld(parent[w1]) if w1 != "world" else "world"
+            p2 = weld(parent[w2]) if w2 != "world" else "world"
+            if filterparent and w1 != "world" and w2 != "world" and (w1 == p2 or w2 == p1):
+                continue
+            if frozenset((w1, w2)) in excludes:
+                continue
+            out.append([g1["name"], g2["name"]])
+            seen.add(frozenset((g1["name"], g2["name"])))
+    for a, b in explicit:
+        if frozenset((a, b)) not in seen:
+            out.append([a, b])
+            seen.add(frozenset((a, b)))
+    return out
+
+
 def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | None = None,
               base_clearance: float | None = None, template: dict | None = None) -> dict:
     """Parse an MJCF file (path or XML text) into the descriptor compile_model() takes.
@@ -250,6 +291,11 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
     fromgeom = comp.get("inertiafromgeom", "auto") if comp is not None else "auto"
     grp = [int(x) for x in comp.get("inertiagrouprange", "0 5").split()] if comp is not None else [0, 5]
     defaults = _Defaults(root.find("default"))
+    flag = root.find("option/flag")
+    filterparent = flag is None or flag.get("filterparent", "enable") != "disable"
+    parent_of: dict[str, str] = {}
+    welded: set[str] = set()
+    colliding: list[dict] = []  # every robot geom with contype or conaffinity, for self_pairs
 
     servo_classes = dict(servo_classes if servo_classes is not None else tmpl.get("servo_classes", {}))
     tmpl_servo = {b["joint"]["name"]: b["joint"].get("servo") for b in tmpl["bodies"] if "joint" in b}
@@ -297,12 +343,15 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
         if not name:
             raise ValueError("every body needs a name")
         b: dict = {"name": name, "parent": parent, "pos": _floats(el.get("pos", "0 0 0"), 3)}
+        parent_of[name] = parent
         q = orientation(el, el.attrib)
         if q != [1.0, 0.0, 0.0, 0.0]:
             b["quat"] = q
         joints = [c for c in el if c.tag in ("joint", "freejoint")]
         if len(joints) > 1:
             raise ValueError(f"body {name}: one joint per body is supported (got {len(joints)})")
+        if not joints:
+            welded.add(name)
         for j in joints:
             ja = defaults.attrs(j, cls) if j.tag == "joint" else dict(j.attrib)
             jt = "free" if j.tag == "freejoint" else ja.get("type", "hinge")
@@ -366,17 +415,20 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
         for c in el:
             if c.tag == "geom":
                 ga = defaults.attrs(c, cls)
-                if int(ga.get("contype", "1")) == 0 and int(ga.get("conaffinity", "1")) == 0:
+                ct, ca = int(ga.get("contype", "1")), int(ga.get("conaffinity", "1"))
+                if ct == 0 and ca == 0:
                     continue  # visual only
                 gt = ga.get("type", "sphere")
+                gname = ga.get("name", f"{name}_geom{len(colliding)}")
+                colliding.append({"name": gname, "body": name, "type": gt, "contype": ct, "conaffinity": ca})
                 if gt not in COLLIDER_TYPES:
                     # the engine collides boxes, capsules, cylinders, spheres and ellipsoids with the floor; other colliding
                     # geoms are listed so a caller can see what the model leaves out (the count cap,
                     # MAX_COLLIDERS, is applied after the touch sensors pick their geoms, below)
-                    desc.setdefault("skipped_geoms", []).append({"name": ga.get("name", ""), "body": name, "type": gt})
+                    desc.setdefault("skipped_geoms", []).append({"name": gname, "body": name, "type": gt})
                     continue
                 nsz = COLLIDER_TYPES[gt]
-                gd = {"name": ga.get("name", f"{name}_geom{len(desc['geoms'])}"), "body": name, "type": gt}
+                gd = {"name": gname, "body": name, "type": gt}
                 gq = orientation(c, ga)
                 if "fromto" in ga:
                     if gt == "sphere":
@@ -414,12 +466,14 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
     wb = root.find("worldbody")
     if wb is None:
         raise ValueError("no <worldbody>")
+    floor_ct = floor_ca = 1
     for c in wb:
         if c.tag == "body":
             parse_body(c, "world", c.get("childclass", "main"))
         elif c.tag == "geom":
             ga = defaults.attrs(c, "main")
             if ga.get("type") == "plane":
+                floor_ct, floor_ca = int(ga.get("contype", "1")), int(ga.get("conaffinity", "1"))
                 fl = desc["floor"]
                 if "friction" in ga:
                     fr = _floats(ga["friction"])
@@ -429,6 +483,26 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                         fl[k] = _floats(ga[k])
                 if "margin" in ga:
                     fl["margin"] = float(ga["margin"])
+    # floor colliders are the geoms that pass the contype / conaffinity test against the floor
+    touches_floor = {g["name"] for g in colliding
+                     if (g["contype"] & floor_ca) or (floor_ct & g["conaffinity"])}
+    desc["geoms"] = [g for g in desc["geoms"] if g["name"] in touches_floor]
+    if "skipped_geoms" in desc:
+        desc["skipped_geoms"] = [g for g in desc["skipped_geoms"] if g["name"] in touches_floor]
+        if not desc["skipped_geoms"]:
+            del desc["skipped_geoms"]
+    # robot-robot pairs (the engine has none): <contact><exclude body1 body2> / <pair geom1 geom2>
+    excludes, explicit = set(), []
+    for ce in root.findall("contact"):
+        for ex in ce.findall("exclude"):
+            excludes.add(frozenset((ex.get("body1"), ex.get("body2"))))
+        names = {g["name"] for g in colliding}
+        for pr in ce.findall("pair"):
+            if pr.get("geom1") in names and pr.get("geom2") in names:
+                explicit.append((pr.get("geom1"), pr.get("geom2")))
+    sp = self_pairs(colliding, parent_of, welded, excludes, explicit, filterparent)
+    if sp:
+        desc["self_pairs"] = sp
     # actuators: a motor (or gain-1 general actuator) per hinge; ctrl order is the joint order
     # the engine requires (JOINT_BIASES, train.py:61-82), whatever the actuator order here
     act = root.find("actuator")
@@ -555,7 +629,10 @@ def to_mjcf(desc: dict) -> str:
         for g in geoms.get(b["name"], []):
             gp = f' pos="{_fmt(g["pos"])}"' if "pos" in g else ""
             gq = f' quat="{_fmt(g["quat"])}"' if "quat" in g else ""
-            lines.append(f'{ind}  <geom name="{g["name"]}" type="{g.get("type", "box")}" size="{_fmt(g["size"])}"{gp}{gq}/>')
+            # contype 1 / conaffinity 0: the floor (1 / 1) collides with every collider and no two
+            # colliders collide with each other, which is what the engine simulates
+            lines.append(f'{ind}  <geom name="{g["name"]}" type="{g.get("type", "box")}" size="{_fmt(g["size"])}"{gp}{gq} '
+                         f'contype="1" conaffinity="0"/>')
         for s in sites.get(b["name"], []):
             sq = f' quat="{_fmt(s["quat"])}"' if "quat" in s else ""
             lines.append(f'{ind}  <site name="{s["name"]}" pos="{_fmt(s.get("pos", [0, 0, 0]))}"{sq}/>')

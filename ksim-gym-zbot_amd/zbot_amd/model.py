@@ -193,14 +193,18 @@ def load_description(path: str | None = None) -> dict:
         return json.load(f)
 
 
-def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) -> CompiledModel:
+def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
+                  drop_self_contacts: bool = False) -> CompiledModel:
     """Compile a JSON robot description into a ZbModel (+ host float64 view).
 
     A description from zbot_amd.mjcf.load_mjcf lists the source's colliding geoms the engine does
     not collide with the floor (it collides up to 4 boxes, capsules and spheres) in
     desc["skipped_geoms"]. They are counted into ZbModel.nskip_geom, and zb_create rejects such a
     model (ZB_EMODEL) rather than simulating it without those contacts. drop_colliders=True
-    compiles it without them, knowingly (nskip_geom 0)."""
+    compiles it without them, knowingly (nskip_geom 0). Likewise desc["self_pairs"], the robot's
+    own geom pairs the source model collides (the engine has floor contacts only), are counted
+    into ZbModel.nskip_pair and refused by zb_create; drop_self_contacts=True compiles the model
+    without them (nskip_pair 0)."""
     if desc is None or isinstance(desc, str):
         desc = load_description(desc)
 
@@ -381,6 +385,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False) 
     m.nbody, m.nq, m.nv, m.nu = nbody, nq, nv, nu
     m.ngeom = len(geoms)
     m.nskip_geom = 0 if drop_colliders else len(desc.get("skipped_geoms", []))
+    m.nskip_pair = 0 if drop_self_contacts else len(desc.get("self_pairs", []))
     m.max_depth = max_depth
     opt = desc.get("option", {})
     g = opt.get("gravity", [0.0, 0.0, -9.81])

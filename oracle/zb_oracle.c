@@ -1769,7 +1769,7 @@ static const FieldOff model_fields[] = {
     OFF(ZbModel, site_body), OFF(ZbModel, site_pos), OFF(ZbModel, site_quat), OFF(ZbModel, site_imu),
     OFF(ZbModel, site_left_foot), OFF(ZbModel, site_right_foot), OFF(ZbModel, body_base), OFF(ZbModel, body_left_foot),
     OFF(ZbModel, body_right_foot), OFF(ZbModel, geom_left_foot), OFF(ZbModel, geom_right_foot),
-    OFF(ZbModel, max_body_depth), OFF(ZbModel, mrow_size), OFF(ZbModel, nskip_geom), OFF(ZbModel, pad_tab), OFF(ZbModel, body_nchild),
+    OFF(ZbModel, max_body_depth), OFF(ZbModel, mrow_size), OFF(ZbModel, nskip_geom), OFF(ZbModel, nskip_pair), OFF(ZbModel, body_nchild),
     OFF(ZbModel, body_child), OFF(ZbModel, depth_maxchild), OFF(ZbModel, dof_desc), OFF(ZbModel, dof_ancpk),
     OFF(ZbModel, dof_rowmask), OFF(ZbModel, dof_act), OFF(ZbModel, dof_rowoff), OFF(ZbModel, geom_lastdof),
     OFF(ZbModel, nlevel), OFF(ZbModel, pad_lvl), OFF(ZbModel, level_nmem), OFF(ZbModel, level_mem),

@@ -26,10 +26,10 @@ def limbs_desc() -> dict:
         for b in root.iter("body"):
             if b.get("name") == "right_knee_pitch_link":
                 b.append(ET.fromstring('<geom name="right_shin" type="box" size="0.015 0.02 0.05" pos="0 0 -0.05" '
-                                       'euler="0.2 0 0.1"/>'))
+                                       'euler="0.2 0 0.1" contype="1" conaffinity="0"/>'))
             if b.get("name") == "left_gripper_roll_link":
                 b.append(ET.fromstring('<geom name="left_hand" type="capsule" size="0.012" '
-                                       'fromto="0 0 0 0.01 0.0 -0.06"/>'))
+                                       'fromto="0 0 0 0.01 0.0 -0.06" contype="1" conaffinity="0"/>'))
 
     return _variant(edit)
 
@@ -46,7 +46,8 @@ def round_desc() -> dict:
                 g.set("quat", "0.7071067811865476 0 0.7071067811865476 0")
         for b in root.iter("body"):
             if b.get("name") == "head":
-                b.append(ET.fromstring('<geom name="head_ball" type="sphere" size="0.05" pos="0 0 0.02"/>'))
+                b.append(ET.fromstring('<geom name="head_ball" type="sphere" size="0.05" pos="0 0 0.02" contype="1" '
+                                       'conaffinity="0"/>'))
 
     return _variant(edit)
 
@@ -64,10 +65,10 @@ def cyl_desc() -> dict:
         for b in root.iter("body"):
             if b.get("name") == "left_knee_pitch_link":
                 b.append(ET.fromstring('<geom name="left_shin" type="cylinder" size="0.018" '
-                                       'fromto="0 0 -0.02 0.01 0.005 -0.09"/>'))
+                                       'fromto="0 0 -0.02 0.01 0.005 -0.09" contype="1" conaffinity="0"/>'))
             if b.get("name") == "right_gripper_roll_link":
                 b.append(ET.fromstring('<geom name="right_hand" type="ellipsoid" size="0.012 0.02 0.035" '
-                                       'pos="0 0 -0.03" euler="0.3 -0.2 0.5"/>'))
+                                       'pos="0 0 -0.03" euler="0.3 -0.2 0.5" contype="1" conaffinity="0"/>'))
 
     return _variant(edit)
 

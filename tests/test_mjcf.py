@@ -458,7 +458,8 @@ def test_skipped_colliders_are_rejected_by_zb_create():
             if "knee" in b.get("name"):
                 shape = ('size="0.015 0.02 0.04" pos="0 0 -0.04"' if gtype == "ellipsoid"
                          else 'mesh="shin"' if gtype == "mesh" else 'size="0.015" fromto="0 0 0 0 0 -0.08"')
-                b.append(ET.fromstring(f'<geom name="shin_col" type="{gtype}" {shape} mass="0"/>'))
+                b.append(ET.fromstring(f'<geom name="shin_col" type="{gtype}" {shape} mass="0" contype="1" '
+                                       'conaffinity="0"/>'))
                 break
         return load_mjcf(ET.tostring(root, encoding="unicode"))
 
@@ -505,3 +506,84 @@ def test_touch_sensor_colliders_win_the_cap():
     assert [g["name"] for g in b["geoms"]] == ["g0", "g1", "g2", "sole"]
     assert [g["name"] for g in b["skipped_geoms"]] == ["g3"]
     assert [s.get("touch_geom") for s in b["sites"]] == ["sole"]
+
+
+def _pairs_doc(body_geoms, extra="", option=""):
+    """A free base with two hinged legs (thigh -> shin) and a jointless foot welded to each shin."""
+    g = {k: body_geoms.get(k, "") for k in ("base", "lt", "ls", "lf", "rt", "rs", "rf")}
+    inert = "<inertial mass='0.1' diaginertia='1e-4 1e-4 1e-4'/>"
+    leg = ("<body name='{s}t' pos='0 {y} -0.05'><joint name='{s}hip' axis='0 1 0'/>" + inert + "{gt}"
+           "<body name='{s}s' pos='0 0 -0.1'><joint name='{s}knee' axis='0 1 0'/>" + inert + "{gs}"
+           "<body name='{s}f' pos='0 0 -0.1'>" + inert + "{gf}</body></body></body>")
+    return ("<mujoco>" + option + "<worldbody><geom name='floor' type='plane' size='0 0 1'/>"
+            "<body name='base' pos='0 0 0.3'><freejoint/>" + inert + g["base"]
+            + leg.format(s="l", y=0.05, gt=g["lt"], gs=g["ls"], gf=g["lf"])
+            + leg.format(s="r", y=-0.05, gt=g["rt"], gs=g["rs"], gf=g["rf"])
+            + "</body></worldbody>" + extra + "</mujoco>")
+
+
+def test_self_contact_pairs_follow_mujocos_filter():
+    """The robot's own geom pairs MuJoCo collides (contype / conaffinity, weld bodies, the parent
+    filter, <exclude>, <pair>) are listed in desc["self_pairs"]; the engine has floor contacts only."""
+    from zbot_amd.mjcf import load_mjcf
+
+    box = "<geom name='{n}' type='box' size='0.01 0.01 0.01'{a}/>"
+    feet = {"lf": box.format(n="lfoot", a=""), "rf": box.format(n="rfoot", a="")}
+    # default contype = conaffinity = 1: the two feet collide with each other
+    d = load_mjcf(_pairs_doc(feet))
+    assert d["self_pairs"] == [["lfoot", "rfoot"]]
+    assert [g["name"] for g in d["geoms"]] == ["lfoot", "rfoot"]
+    # contype 1 / conaffinity 0 on both: each still meets the floor (1 / 1), not each other
+    floor_only = {k: box.format(n=n, a=" contype='1' conaffinity='0'") for k, n in (("lf", "lfoot"), ("rf", "rfoot"))}
+    d = load_mjcf(_pairs_doc(floor_only))
+    assert "self_pairs" not in d and len(d["geoms"]) == 2
+    # <exclude> between the feet's weld bodies (the shins: the feet have no joint)
+    d = load_mjcf(_pairs_doc(feet, "<contact><exclude body1='ls' body2='rs'/></contact>"))
+    assert "self_pairs" not in d
+    # the parent filter: a shin geom and its thigh's geom never collide; the foot is welded to the
+    # shin, so the foot and the thigh are a weld body and its parent too
+    d = load_mjcf(_pairs_doc({"lt": box.format(n="lthigh", a=""), "lf": box.format(n="lfoot", a="")}))
+    assert "self_pairs" not in d
+    d = load_mjcf(_pairs_doc({"lt": box.format(n="lthigh", a=""), "lf": box.format(n="lfoot", a="")},
+                             option="<option><flag filterparent='disable'/></option>"))
+    assert d["self_pairs"] == [["lthigh", "lfoot"]]
+    # a base geom and a shin geom (grandparent): a pair
+    d = load_mjcf(_pairs_doc({"base": box.format(n="torso", a=""), "ls": box.format(n="lshin", a="")}))
+    assert d["self_pairs"] == [["torso", "lshin"]]
+    # contype 2 / conaffinity 2: not the floor's (1 / 1), so no floor contact, but each other's
+    two = {k: box.format(n=n, a=" contype='2' conaffinity='2'") for k, n in (("lf", "lfoot"), ("rf", "rfoot"))}
+    d = load_mjcf(_pairs_doc({**two, "base": box.format(n="torso", a=" contype='1' conaffinity='0'")}))
+    assert [g["name"] for g in d["geoms"]] == ["torso"] and d["self_pairs"] == [["lfoot", "rfoot"]]
+    # an explicit <pair> counts whatever the bits say
+    d = load_mjcf(_pairs_doc(floor_only, "<contact><pair geom1='lfoot' geom2='rfoot'/></contact>"))
+    assert d["self_pairs"] == [["lfoot", "rfoot"]]
+
+
+def test_self_contacts_are_rejected_by_zb_create():
+    """A model whose own geoms collide with each other is refused (ZB_EMODEL, nskip_pair) rather
+    than simulated without those contacts; drop_self_contacts=True compiles it knowingly."""
+    import ctypes as C
+    import xml.etree.ElementTree as ET
+
+    from zbot_amd import compile_model, default_config
+    from zbot_amd import engine as E
+
+    root = ET.fromstring(to_mjcf(load_description()))
+    for g in root.iter("geom"):
+        if g.get("name") in ("right_foot_sole", "left_foot_sole"):
+            del g.attrib["conaffinity"]  # MuJoCo's default 1: the soles collide with each other
+    desc = load_mjcf(ET.tostring(root, encoding="unicode"))
+    assert desc["self_pairs"] == [["right_foot_sole", "left_foot_sole"]] or \
+        desc["self_pairs"] == [["left_foot_sole", "right_foot_sole"]]
+    L = E.load_library()
+    h = C.c_void_p()
+    cm = compile_model(desc)
+    assert cm.cmodel.nskip_pair == 1
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc == -4 and b"pairs of its own geoms" in L.zb_last_error()
+    cm = compile_model(desc, drop_self_contacts=True)
+    assert cm.cmodel.nskip_pair == 0
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc != -4, L.zb_last_error()
+    if rc == 0:
+        L.zb_destroy(h)
