@@ -15,7 +15,8 @@
  *     (root only) or hinge; other bodies are welded (no joint);
  *   - nbody <= ZB_MAX_BODY, nv <= ZB_MAX_DOF, dof-chain depth <= ZB_MAX_DEPTH;
  *   - collision = floor plane (world geom) vs up to ZB_MAX_GEOM per-body boxes,
- *     capsules, cylinders or spheres (the two foot soles first by convention);
+ *     capsules, cylinders, spheres or ellipsoids (the two foot soles first by
+ *     convention); no robot-robot contacts (nskip_pair = 0);
  *   - actuators = motors on hinge joints (joint transmission, gear).
  * All floats are fp32; all vectors are padded to 4 so rows are 16-B aligned.
  */

@@ -198,7 +198,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
     """Compile a JSON robot description into a ZbModel (+ host float64 view).
 
     A description from zbot_amd.mjcf.load_mjcf lists the source's colliding geoms the engine does
-    not collide with the floor (it collides up to 4 boxes, capsules and spheres) in
+    not collide with the floor (it collides up to 4 boxes, capsules, cylinders, spheres and ellipsoids) in
     desc["skipped_geoms"]. They are counted into ZbModel.nskip_geom, and zb_create rejects such a
     model (ZB_EMODEL) rather than simulating it without those contacts. drop_colliders=True
     compiles it without them, knowingly (nskip_geom 0). Likewise desc["self_pairs"], the robot's
@@ -481,7 +481,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
     for gi, gd in enumerate(geoms):
         gt = gd.get("type", "box")
         if gt not in gtypes:
-            raise ValueError(f"geom {gd['name']}: type {gt!r} (box, capsule, cylinder and sphere collide with the floor)")
+            raise ValueError(f"geom {gd['name']}: type {gt!r} (box, capsule, cylinder, sphere and ellipsoid collide with the floor)")
         code, nsize = gtypes[gt]
         if len(gd["size"]) < nsize or any(not (v > 0) for v in gd["size"][:nsize]):
             raise ValueError(f"geom {gd['name']}: a {gt} needs {nsize} positive sizes")
