@@ -1,6 +1,7 @@
 """Floor colliders beyond the two box soles on the GPU (the general-collider kernels, XG): a right
-shin box and a left hand capsule beside the soles ("limbs"), and capsule feet with a head sphere
-("round"), in states where the colliders touch the floor (tests/collider_util.py), against the
+shin box and a left hand capsule beside the soles ("limbs"), capsule feet with a head sphere
+("round"), and a cylinder right foot, a cylinder shin and an ellipsoid hand beside the left box sole
+("cyl", round 4), in states where the colliders touch the floor (tests/collider_util.py), against the
 oracle on the same model and state."""
 
 import numpy as np
