@@ -96,6 +96,16 @@ COLLIDER_TOL_CG = {
 }
 
 
+# The cyl variant's cylinder right foot lands flat in the first step (three rim contacts, ncon 3):
+# a disk resting on the floor, where MuJoCo's plane-cylinder rule turns the contact triangle with
+# the direction of a vanishing tilt. The fp32 and fp64 oracles then leave the solver 15-25
+# iterations apart over the second step (fp32 51-68, fp64 29-45) and disagree by up to 1.7e-5 in
+# qpos in 56 of 64 envs, so the fp64 slack (MaxErr ref64) would cover nearly every env. There the
+# GPU is held to the fp32 oracle without it: every env within the same bounds (r04 v17 measured
+# qpos 3.0e-7, qvel 5.3e-6 with Newton; qpos 3.1e-6, qvel 2.3e-4 with CG).
+NO_FP64_SLACK = {"cyl"}
+
+
 @pytest.mark.parametrize("solver", ["newton", "cg"])
 def test_one_step_matches_oracle(torch_gpu, variant, oracle_mod, solver):
     torch = torch_gpu
@@ -120,7 +130,7 @@ def test_one_step_matches_oracle(torch_gpu, variant, oracle_mod, solver):
         gs = eng.get_state().cpu().numpy()
         np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
         for key, got, want in one_step_outputs(gs, out, env.state, ref):
-            err.add(key, got, want, *tols[key], ref64=ref64[key])
+            err.add(key, got, want, *tols[key], ref64=None if name in NO_FP64_SLACK else ref64[key])
     err.report()
 
 
