@@ -1545,7 +1545,7 @@ __device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, floa
 
 /* The collider of team lane l in contact-row bank `bank`: geom 2 bank + l / 16 (XG), or sole l / 16
    of the two-sole kernels. gb: its body; false when the model has no such geom. */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& gb) {
   MP m = c.m;
   const int gl = c.l >> 4;
@@ -1572,7 +1572,7 @@ __device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& g
  * direction n +- mu t (t1 = +y, t2 = n x t1 = -x for boxes and spheres: mju_makeFrame(+z)) and the
  * friction; returns the signed distance, 1e30 where the slot holds no contact. Recomputed by the
  * sensors instead of being held in registers through the solver. */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, const BodyK& B, int bank, float pos[3],
                                                float dir[3], float& mu) {
   MP m = c.m;
@@ -1586,8 +1586,10 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
 #pragma unroll
   for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
   const int ty = XG ? m->geom_type[g] : ZB_GEOM_BOX;
-  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE, cyl = XG && ty == ZB_GEOM_CYLINDER,
-             ell = XG && ty == ZB_GEOM_ELLIPSOID;
+  /* XG 2: the instantiation for models with cylinders or ellipsoids (zb_host.cpp needs_xg), so that
+     the others carry no code for them */
+  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE,
+             cyl = XG == 2 && ty == ZB_GEOM_CYLINDER, ell = XG == 2 && ty == ZB_GEOM_ELLIPSOID;
   /* the lane's point relative to the geom centre, geom frame -> body frame -> world */
   float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
   float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
@@ -1595,68 +1597,62 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
   float p[3], dist;
   bool slot_ok;
   float t1x = 0.f, t1y = 1.f;
-  if (cyl) {
-    /* mjc_PlaneCylinder (oracle collision()): the axis a turned toward the plane, v the radius
-       vector in the disk planes toward it; slot 0 the near disk's deepest point c + v + a, 1 the far
-       disk's c + v - a, 2 / 3 the near disk's points 120 degrees away, c + a - v / 2 +- v1; none
-       unless slot 0 is within the margin */
-    const float ez[3] = {0.f, 0.f, 1.f}, ex[3] = {1.f, 0.f, 0.f};
-    float ab[3], a[3], eb[3], xw[3], cw[3];
-    quat_rotate(ab, gq, ez);
-    quat_rotate(a, xqs, ab);
-    quat_rotate(eb, gq, ex);
-    quat_rotate(xw, xqs, eb);
+  if (cyl || ell) {
+    /* the geom's world rotation R from one quaternion product (body then geom), and its centre */
+    const float qw0 = xqs[0] * gq[0] - xqs[1] * gq[1] - xqs[2] * gq[2] - xqs[3] * gq[3];
+    const float qw1 = xqs[0] * gq[1] + xqs[1] * gq[0] + xqs[2] * gq[3] - xqs[3] * gq[2];
+    const float qw2 = xqs[0] * gq[2] - xqs[1] * gq[3] + xqs[2] * gq[0] + xqs[3] * gq[1];
+    const float qw3 = xqs[0] * gq[3] + xqs[1] * gq[2] - xqs[2] * gq[1] + xqs[3] * gq[0];
+    const float R00 = 1.f - 2.f * (qw2 * qw2 + qw3 * qw3), R01 = 2.f * (qw1 * qw2 - qw0 * qw3), R02 = 2.f * (qw1 * qw3 + qw0 * qw2);
+    const float R10 = 2.f * (qw1 * qw2 + qw0 * qw3), R11 = 1.f - 2.f * (qw1 * qw1 + qw3 * qw3), R12 = 2.f * (qw2 * qw3 - qw0 * qw1);
+    const float R20 = 2.f * (qw1 * qw3 - qw0 * qw2), R21 = 2.f * (qw2 * qw3 + qw0 * qw1), R22 = 1.f - 2.f * (qw1 * qw1 + qw2 * qw2);
+    float cw[3];
     quat_rotate(cw, xqs, gp);
     const float c0 = xp[0] + cw[0], c1 = xp[1] + cw[1], c2 = xp[2] + cw[2];
-    float prja = a[2];
-    if (prja > 0.f) {
+    if (cyl) {
+      /* mjc_PlaneCylinder (oracle collision()): the axis a (R's z column) turned toward the plane,
+         v the radius vector in the disk planes toward it; slot 0 the near disk's deepest point
+         c + v + a, 1 the far disk's c + v - a, 2 / 3 the near disk's points 120 degrees away,
+         c + a - v / 2 +- v1; none unless slot 0 is within the margin */
+      const float sg = R22 > 0.f ? -1.f : 1.f;
+      float a[3] = {sg * R02, sg * R12, sg * R22};
+      float prja = a[2];
+      float v[3] = {a[0] * prja, a[1] * prja, a[2] * prja - 1.f};
+      const float len = sqrtf(dot3(v, v));
+      const bool par = !(len >= MINVAL); /* the disks parallel to the plane: the geom's x axis */
+      const float sv = par ? s0 : s0 / len;
+      v[0] = (par ? R00 : v[0]) * sv;
+      v[1] = (par ? R10 : v[1]) * sv;
+      v[2] = (par ? R20 : v[2]) * sv;
+      const float prjv = v[2];
 #pragma unroll
-      for (int k = 0; k < 3; k++) a[k] = -a[k];
-      prja = -prja;
+      for (int k = 0; k < 3; k++) a[k] *= s1;
+      prja *= s1;
+      const float d1 = c2 + prja + prjv;
+      float v1[3];
+      cross3(v1, v, a);
+      const float n1 = sqrtf(dot3(v1, v1));
+      const float sc = n1 > 0.f ? s0 * 0.8660254037844386f / n1 : 0.f;
+      const float sa = slot == 1 ? -1.f : 1.f;                    /* +a, except the far disk */
+      const float svv = slot >= 2 ? -0.5f : 1.f;                  /* +v, -v / 2 on the triangle */
+      const float s1v = slot == 2 ? sc : (slot == 3 ? -sc : 0.f); /* +- v1 on the triangle */
+      p[0] = c0 + svv * v[0] + sa * a[0] + s1v * v1[0];
+      p[1] = c1 + svv * v[1] + sa * a[1] + s1v * v1[1];
+      p[2] = c2 + svv * v[2] + sa * a[2] + s1v * v1[2];
+      dist = slot == 0 ? d1 : (slot == 1 ? c2 - prja + prjv : c2 + prja - 0.5f * prjv);
+      slot_ok = d1 <= m->floor_margin;
+    } else {
+      /* mjc_PlaneEllipsoid (oracle collision()): sn = s .* (R' n) (R's z row), the support point
+         R (-s .* sn / |sn|) from the centre */
+      const float sn0 = s0 * R20, sn1 = s1 * R21, sn2 = s2 * R22;
+      const float inv = 1.f / sqrtf(sn0 * sn0 + sn1 * sn1 + sn2 * sn2);
+      const float l0 = -s0 * sn0 * inv, l1 = -s1 * sn1 * inv, l2 = -s2 * sn2 * inv;
+      p[0] = c0 + R00 * l0 + R01 * l1 + R02 * l2;
+      p[1] = c1 + R10 * l0 + R11 * l1 + R12 * l2;
+      p[2] = c2 + R20 * l0 + R21 * l1 + R22 * l2;
+      dist = p[2];
+      slot_ok = slot == 0;
     }
-    float v[3] = {a[0] * prja, a[1] * prja, a[2] * prja - 1.f};
-    const float len = sqrtf(dot3(v, v));
-    const bool par = !(len >= MINVAL); /* the disks parallel to the plane: the geom's x axis */
-    const float sv = par ? s0 : s0 / len;
-#pragma unroll
-    for (int k = 0; k < 3; k++) v[k] = (par ? xw[k] : v[k]) * sv;
-    const float prjv = v[2];
-#pragma unroll
-    for (int k = 0; k < 3; k++) a[k] *= s1;
-    prja *= s1;
-    const float d1 = c2 + prja + prjv;
-    float v1[3];
-    cross3(v1, v, a);
-    const float n1 = sqrtf(dot3(v1, v1));
-    const float sc = n1 > 0.f ? s0 * 0.8660254037844386f / n1 : 0.f;
-    const float sa = slot == 1 ? -1.f : 1.f;                    /* +a, except the far disk */
-    const float svv = slot >= 2 ? -0.5f : 1.f;                  /* +v, -v / 2 on the triangle */
-    const float s1v = slot == 2 ? sc : (slot == 3 ? -sc : 0.f); /* +- v1 on the triangle */
-    p[0] = c0 + svv * v[0] + sa * a[0] + s1v * v1[0];
-    p[1] = c1 + svv * v[1] + sa * a[1] + s1v * v1[1];
-    p[2] = c2 + svv * v[2] + sa * a[2] + s1v * v1[2];
-    dist = slot == 0 ? d1 : (slot == 1 ? c2 - prja + prjv : c2 + prja - 0.5f * prjv);
-    slot_ok = d1 <= m->floor_margin;
-  } else if (ell) {
-    /* mjc_PlaneEllipsoid (oracle collision()): n = +z taken into the geom frame (body, then geom
-       rotation inverted), sn = s .* n_g, the support point -s .* sn / |sn| back to the world */
-    const float ez[3] = {0.f, 0.f, 1.f};
-    const float xqc[4] = {xqs[0], -xqs[1], -xqs[2], -xqs[3]}, gqc[4] = {gq[0], -gq[1], -gq[2], -gq[3]};
-    float nb[3], ng[3];
-    quat_rotate(nb, xqc, ez);
-    quat_rotate(ng, gqc, nb);
-    const float sn0 = s0 * ng[0], sn1 = s1 * ng[1], sn2 = s2 * ng[2];
-    const float inv = 1.f / sqrtf(sn0 * sn0 + sn1 * sn1 + sn2 * sn2);
-    const float loc[3] = {-s0 * sn0 * inv, -s1 * sn1 * inv, -s2 * sn2 * inv};
-    float w[3], t[3];
-    quat_rotate(w, gq, loc);
-    const float gl[3] = {gp[0] + w[0], gp[1] + w[1], gp[2] + w[2]};
-    quat_rotate(t, xqs, gl);
-    p[0] = xp[0] + t[0];
-    p[1] = xp[1] + t[1];
-    p[2] = xp[2] + t[2];
-    dist = p[2];
-    slot_ok = slot == 0;
   } else {
     float v[3];
     if (box) {
@@ -1711,7 +1707,7 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
 }
 
 /* the contact rows of one bank: collision, then the row of lane l (J at Jrow) */
-template <bool XG, typename CR, typename JP>
+template <int XG, typename CR, typename JP>
 __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const BodyK& B, const float cm[3], int bank,
                                              CR& r, JP Jrow) {
   MP m = c.m;
@@ -1769,7 +1765,7 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
 }
 
 /* collision + contact rows (lane r; XG: both banks) + dof rows (lane j) */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
                                  Rows& r) {
   MP m = c.m;
@@ -1865,7 +1861,7 @@ __device__ __forceinline__ float eval_one(float jar, float D, float& force, int&
 }
 
 /* row costs at given jar values (no state change); jx: the second bank's contact row (XG) */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jl_, float jx) {
   float f;
   int a;
@@ -1924,7 +1920,7 @@ __device__ __forceinline__ float colsum16(JP Jrow, float fr) {
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
 /* returns this lane's cost share; the caller reduces it over the team (alone, or together with
    the Newton loop's other per-iteration sums in one tsum_n) */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, const float jr[CAP], float qacc,
                                                        float qs, float fs, float Ma, float& grad) {
   const int ddep = vopq(c.ddep);
@@ -1984,7 +1980,7 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
   grad = Ma - fs - qc;
   return cost;
 }
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, const float jr[CAP], float qacc, float qs,
                                                   float fs, float Ma, float& grad) {
   return tsum(update_constraint_lane<XG>(c, r, jr, qacc, qs, fs, Ma, grad));
@@ -2063,7 +2059,7 @@ __device__ __forceinline__ void add_rows(uint32_t tb, JP J, const float* da, int
  * H of the previous build is updated with the rows whose activity changed
  * (+-D_r J_r J_r') -- MuJoCo's Newton also only re-assembles on a change of
  * the active set, and the change is usually a handful of rows. XG: both banks. */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo,
                                                 int pa2) {
   const int ddep = vopq(c.ddep);
@@ -2156,7 +2152,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float jr[CAP], float search, float Ma, float fs,
                                              float grad, float& Mv) {
   CP cfg = c.cfg;
@@ -2249,7 +2245,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
 }
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters,
                                               bool live) {
   CP cfg = c.cfg;
@@ -2349,7 +2345,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
    the smooth factor of M that forward() left in L[] / Dk / Di (DinvM: this lane's 1/D), with
    Polak-Ribiere beta = max(0, g . (Mg - Mg_prev) / max(MINVAL, g_prev . Mg_prev)). No Hessian is
    built or factored. Returns qacc (dof lane). */
-template <bool XG>
+template <int XG>
 __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters, bool live,
                                           float DinvM) {
   CP cfg = c.cfg;
@@ -2458,7 +2454,7 @@ __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
 
 /* ------------------------------- full forward ------------------------------ */
 /* mj_forward (+ sensors if requested). Leaves qacc in ls.qacc, kinematics in B. */
-template <int SOLVER, bool XG>
+template <int SOLVER, int XG>
 __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, BodyK& B, Rows& r, bool with_sensors,
                                         Sensors& sen, int& iters) {
   MP m = c.m;
@@ -3115,7 +3111,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 #ifndef ZB_WAVES_PER_EU
 #define ZB_WAVES_PER_EU 2
 #endif
-template <int SOLVER, bool XG>
+template <int SOLVER, int XG>
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   /* Chunked step (a.nchunk > 1, one control step): the launch has npair * nchunk workgroups, each
@@ -3330,7 +3326,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
 #endif
 }
 
-template <int SOLVER, bool XG>
+template <int SOLVER, int XG>
 __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
@@ -3366,7 +3362,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
 }
 
 /* single forward on the stored (qpos, qvel), ctrl = action row; dumps internals */
-template <int SOLVER, bool XG>
+template <int SOLVER, int XG>
 __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   const int e = blockIdx.x * NTEAM + team;
@@ -3450,12 +3446,12 @@ int step_resident_blocks(int device, int xg, int solver) {
   int per_cu = 0, cus = 0;
   /* the instantiation the handle launches: CG and Newton differ in registers and LDS */
   hipError_t e;
+#define ZB_OCC(S, X) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<S, X>, 64, 0)
   if (solver == ZB_SOLVER_CG)
-    e = xg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_CG, true>, 64, 0)
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_CG, false>, 64, 0);
+    e = xg == 2 ? ZB_OCC(ZB_SOLVER_CG, 2) : xg ? ZB_OCC(ZB_SOLVER_CG, 1) : ZB_OCC(ZB_SOLVER_CG, 0);
   else
-    e = xg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, true>, 64, 0)
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<ZB_SOLVER_NEWTON, false>, 64, 0);
+    e = xg == 2 ? ZB_OCC(ZB_SOLVER_NEWTON, 2) : xg ? ZB_OCC(ZB_SOLVER_NEWTON, 1) : ZB_OCC(ZB_SOLVER_NEWTON, 0);
+#undef ZB_OCC
   if (e != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
   return per_cu * cus;
@@ -3465,11 +3461,13 @@ int step_resident_blocks(int device, int xg, int solver) {
 #define ZB_LAUNCH_VARIANT(K, grid, block, s, args)                                                        \
   do {                                                                                                    \
     if ((args).solver == ZB_SOLVER_CG) {                                                                  \
-      if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_CG, true>), grid, block, 0, s, args);                \
-      else hipLaunchKernelGGL((K<ZB_SOLVER_CG, false>), grid, block, 0, s, args);                         \
+      if ((args).xg == 2) hipLaunchKernelGGL((K<ZB_SOLVER_CG, 2>), grid, block, 0, s, args);              \
+      else if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_CG, 1>), grid, block, 0, s, args);              \
+      else hipLaunchKernelGGL((K<ZB_SOLVER_CG, 0>), grid, block, 0, s, args);                             \
     } else {                                                                                              \
-      if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, true>), grid, block, 0, s, args);            \
-      else hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, false>), grid, block, 0, s, args);                     \
+      if ((args).xg == 2) hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, 2>), grid, block, 0, s, args);          \
+      else if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, 1>), grid, block, 0, s, args);          \
+      else hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, 0>), grid, block, 0, s, args);                         \
     }                                                                                                     \
   } while (0)
 

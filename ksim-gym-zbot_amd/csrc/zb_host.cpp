@@ -154,8 +154,11 @@ int check_model(const ZbModel* m) {
   return ZB_OK;
 }
 
-bool needs_xg(const ZbModel* m) {
-  return !(m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX);
+int needs_xg(const ZbModel* m) {
+  if (m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX) return 0;
+  for (int g = 0; g < m->ngeom; g++)
+    if (m->geom_type[g] == ZB_GEOM_CYLINDER || m->geom_type[g] == ZB_GEOM_ELLIPSOID) return 2;
+  return 1;
 }
 
 int check_cfg(const ZbEnvConfig* c) {
