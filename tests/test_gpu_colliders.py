@@ -98,11 +98,12 @@ COLLIDER_TOL_CG = {
 
 # The cyl variant's cylinder right foot lands flat in the first step (three rim contacts, ncon 3):
 # a disk resting on the floor, where MuJoCo's plane-cylinder rule turns the contact triangle with
-# the direction of a vanishing tilt. The fp32 and fp64 oracles then leave the solver 15-25
-# iterations apart over the second step (fp32 51-68, fp64 29-45) and disagree by up to 1.7e-5 in
-# qpos in 56 of 64 envs, so the fp64 slack (MaxErr ref64) would cover nearly every env. There the
-# GPU is held to the fp32 oracle without it: every env within the same bounds (r04 v17 measured
-# qpos 3.0e-7, qvel 5.3e-6 with Newton; qpos 3.1e-6, qvel 2.3e-4 with CG).
+# the direction of a vanishing tilt. The fp32 and fp64 oracles then disagree by up to 1.7e-5 in
+# qpos over the second step in 56 of 64 envs (the limbs variant: 2.4e-7 in none;
+# scripts/cyl_flat_probe.py, profiles/r04_cyl_flat_probe.log), so the fp64 slack (MaxErr ref64)
+# would cover nearly every env. There the GPU is held to the fp32 oracle without it: every env
+# within the same bounds (r04 v17 measured qpos 3.0e-7, qvel 5.3e-6 with Newton; qpos 3.1e-6,
+# qvel 2.3e-4 with CG).
 NO_FP64_SLACK = {"cyl"}
 
 
