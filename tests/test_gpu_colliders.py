@@ -157,3 +157,59 @@ def test_rollout_launch_equals_steps(torch_gpu, variant, oracle_mod):
     b.rollout(A, reward_sum=torch.zeros(n, device="cuda"))
     torch.cuda.synchronize()
     assert np.array_equal(a.get_state().cpu().numpy(), b.get_state().cpu().numpy())
+
+
+@pytest.mark.parametrize("name", list(DESCS))
+def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
+    """48 control steps of 64 envs from reset with pushes and wide actions (std 0.5), so robots
+    stumble and fall and the colliders beyond the soles meet the floor: the engine against the fp32
+    oracle run alongside. As the golden rollouts (test_gpu_parity.test_golden_rollout): the first 8
+    rewards under the one-step contract (the fp64 oracle stepping from the fp32 oracle's state gives
+    the slack at a discontinuity; none for the cyl variant, NO_FP64_SLACK), done flags exact over
+    the first 16 steps, then the ensemble contract (golden_ensemble_check). Asserts that some
+    collider outside the soles touched the floor in the oracle's rollout."""
+    torch = torch_gpu
+    from test_gpu_parity import GOLDEN_EXACT_STEPS, GOLDEN_TOL, MaxErr, golden_ensemble_check
+
+    from zbot_amd.engine import HipEngine
+
+    cm = compile_model(DESCS[name]())
+    cfg = default_config(push=True)
+    n, steps, seed = 64, 48, 13
+    acts = np.stack([oracle_mod.synthetic_actions(cm.cmodel, seed, n, 0, t, std=0.5) for t in range(steps)])
+    e32 = oracle_mod.OracleEnv(cm.cmodel, cfg, n, seed=seed)
+    e64 = oracle_mod.OracleEnv(cm.cmodel, cfg, n, seed=seed, precision="f64")
+    e32.reset()
+    ref_r, ref_d, r64s = [], [], []
+    extra = np.zeros(cm.cmodel.ngeom, int)
+    for t in range(steps):
+        if t < 8:
+            e64.state[:] = e32.state
+            e64.rand[:] = e32.rand
+            r64s.append(e64.step(acts[t])["reward"].copy())
+        o = e32.step(acts[t])
+        ref_r.append(o["reward"].copy())
+        ref_d.append(o["done"].copy())
+        for e in range(0, n, 4):
+            cons = U.contacts(cm, e32.state[e, :27].astype(np.float64))
+            extra += np.array([len(c) > 0 for c in cons])
+    soles = {cm.geom_names.index(s) for s in ("right_foot_sole", "left_foot_sole")}
+    assert any(extra[g] > 0 for g in range(cm.cmodel.ngeom) if g not in soles), extra
+    g = {"reward": np.stack(ref_r), "done": np.stack(ref_d), "final_state": e32.state.copy()}
+    eng = HipEngine(cm, cfg, n, seed=seed)
+    eng.reset()
+    rew, done = [], []
+    for t in range(steps):
+        o = eng.step(torch.from_numpy(acts[t]).cuda())
+        rew.append(o["reward"].cpu().numpy().copy())
+        done.append(o["done"].cpu().numpy().copy())
+    rew, done = np.stack(rew), np.stack(done)
+    np.testing.assert_array_equal(done[:GOLDEN_EXACT_STEPS], g["done"][:GOLDEN_EXACT_STEPS])
+    err = MaxErr(f"colliders {name} rollout from reset")
+    for t in range(8):
+        err.add(f"reward[{t}]", rew[t], g["reward"][t], GOLDEN_TOL["reward"],
+                ref64=None if name in NO_FP64_SLACK else r64s[t])
+    print(f"\n[colliders {name} rollout] steps with a contact per collider (every 4th env): "
+          + ", ".join(f"{cm.geom_names[k]} {int(extra[k])}" for k in range(cm.cmodel.ngeom)))
+    golden_ensemble_check(f"colliders {name}", rew, done, eng.get_state().cpu().numpy(), g)
+    err.report()
