@@ -162,12 +162,15 @@ def test_rollout_launch_equals_steps(torch_gpu, variant, oracle_mod):
 @pytest.mark.parametrize("name", list(DESCS))
 def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
     """48 control steps of 64 envs from reset with pushes and wide actions (std 0.5), so robots
-    stumble and fall and the colliders beyond the soles meet the floor: the engine against the fp32
-    oracle run alongside. As the golden rollouts (test_gpu_parity.test_golden_rollout): the first 8
-    rewards under the one-step contract (the fp64 oracle stepping from the fp32 oracle's state gives
-    the slack at a discontinuity; none for the cyl variant, NO_FP64_SLACK), done flags exact over
-    the first 16 steps, then the ensemble contract (golden_ensemble_check). Asserts that some
-    collider outside the soles touched the floor in the oracle's rollout."""
+    stumble, fall and reset: the general-collider instantiations (levels 1 and 2) over a rollout,
+    against the fp32 oracle run alongside. As the golden rollouts (test_gpu_parity.
+    test_golden_rollout): the first 8 rewards under the one-step contract (the fp64 oracle stepping
+    from the fp32 oracle's state gives the slack at a discontinuity; none for the cyl variant,
+    NO_FP64_SLACK), done flags exact over the first 16 steps, then the ensemble contract
+    (golden_ensemble_check). Prints how often each collider touched the floor in the oracle's
+    rollout (every 4th env): the soles (and the cylinder foot) carry the robots; shins, hands and
+    head rarely touch before NotUpright ends the episode, so the one-step tests from touching states
+    above are the ones that load every collider."""
     torch = torch_gpu
     from test_gpu_parity import GOLDEN_EXACT_STEPS, GOLDEN_TOL, MaxErr, golden_ensemble_check
 
@@ -193,8 +196,7 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
         for e in range(0, n, 4):
             cons = U.contacts(cm, e32.state[e, :27].astype(np.float64))
             extra += np.array([len(c) > 0 for c in cons])
-    soles = {cm.geom_names.index(s) for s in ("right_foot_sole", "left_foot_sole")}
-    assert any(extra[g] > 0 for g in range(cm.cmodel.ngeom) if g not in soles), extra
+    names = [gd["name"] for gd in cm.desc["geoms"]]  # U.contacts order (the descriptor's)
     g = {"reward": np.stack(ref_r), "done": np.stack(ref_d), "final_state": e32.state.copy()}
     eng = HipEngine(cm, cfg, n, seed=seed)
     eng.reset()
@@ -210,6 +212,6 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
         err.add(f"reward[{t}]", rew[t], g["reward"][t], GOLDEN_TOL["reward"],
                 ref64=None if name in NO_FP64_SLACK else r64s[t])
     print(f"\n[colliders {name} rollout] steps with a contact per collider (every 4th env): "
-          + ", ".join(f"{cm.geom_names[k]} {int(extra[k])}" for k in range(cm.cmodel.ngeom)))
+          + ", ".join(f"{names[k]} {int(extra[k])}" for k in range(len(names))))
     golden_ensemble_check(f"colliders {name}", rew, done, eng.get_state().cpu().numpy(), g)
     err.report()
