@@ -107,6 +107,19 @@ def test_limbs_asset_is_the_test_variant():
     assert bytes(a) == bytes(b)
 
 
+def test_cyl_asset_is_the_test_variant():
+    """assets/zbot_like_cyl.xml (bench.py --model) is collider_util.cyl_desc written out."""
+    import os
+
+    from zbot_amd.mjcf import load_mjcf, to_mjcf
+    from zbot_amd.model import DEFAULT_ASSET
+
+    path = os.path.join(os.path.dirname(DEFAULT_ASSET), "zbot_like_cyl.xml")
+    with open(path) as f:
+        assert f.read() == to_mjcf(U.cyl_desc()) + "\n"
+    assert bytes(compile_model(load_mjcf(path)).cmodel) == bytes(compile_model(U.cyl_desc()).cmodel)
+
+
 def test_cylinder_known_answers():
     """Known answers for the cylinder rule (mjc_PlaneCylinder; pins the numpy restatement that
     test_oracle_contact_sets_match_mujoco_rules checks the oracle against). Radius 0.02, half-length
