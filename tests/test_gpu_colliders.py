@@ -219,3 +219,40 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
           + ", ".join(f"{names[k]} {int(extra[k])}" for k in range(len(names))))
     golden_ensemble_check(f"colliders {name}", rew, done, eng.get_state().cpu().numpy(), g)
     err.report()
+
+
+@pytest.mark.parametrize("name", list(DESCS))
+def test_full_size_properties(torch_gpu, name):
+    """Each collider variant at the C2 size (8192 envs, pushes and randomization on, 8 steps from
+    reset, two env groups): finite, unit quaternions, no invalid flag, bit-reproducible, and
+    shard-invariant (two half-size handles with env_offset give the same bits as one handle, and the
+    two-group EnvGroups the same bits again)."""
+    torch = torch_gpu
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    cm = compile_model(DESCS[name]())
+    cfg = default_config(push=True, randomize=True)
+    n = 8192
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    acts = [bias + 0.2 * torch.randn(n, 20, device="cuda", generator=g) for _ in range(8)]
+
+    def run(h, lo=0, hi=n):
+        h.reset()
+        for a in acts:
+            out = h.step(a[lo:hi].contiguous())
+        return h.get_state(), out
+
+    st, out = run(HipEngine(cm, cfg, n, seed=9))
+    assert torch.isfinite(st[:, :58]).all() and torch.isfinite(out["obs_critic"]).all()
+    assert torch.allclose(st[:, 3:7].norm(dim=1), torch.ones(n, device="cuda"), atol=2e-6)
+    assert (st[:, cs.S_NAN].view(torch.int32) == 0).all()
+    again, _ = run(HipEngine(cm, cfg, n, seed=9))
+    assert torch.equal(again, st)
+    halves = [run(HipEngine(cm, cfg, n // 2, env_offset=off, seed=9), off, off + n // 2)[0] for off in (0, n // 2)]
+    assert torch.equal(torch.cat(halves), st)
+    grouped = EnvGroups(cm, cfg, n, groups=2, seed=9)
+    gst, _ = run(grouped)
+    grouped.join()
+    assert torch.equal(gst, st)
