@@ -236,7 +236,9 @@ def self_pairs(geoms: list[dict], parent: dict[str, str], welded: set[str], excl
     the MJCF reference's "Contact" section): geoms g1, g2 with (contype1 & conaffinity2) or
     (contype2 & conaffinity1) nonzero, on different weld bodies (a body without a joint is welded to
     its parent), not a weld body and its weld parent (filterparent, unless the parent is the world),
-    not <contact><exclude>-d; plus the explicit <contact><pair>s. geoms: {"name", "body", "contype",
+    not <contact><exclude>-d (matched on the geoms' own bodies [U: MuJoCo's broadphase signature as
+    remembered; matching the weld bodies instead would exclude more, so this side reports more
+    pairs, never fewer]); plus the explicit <contact><pair>s. geoms: {"name", "body", "contype",
     "conaffinity"}; parent: body -> parent body; welded: bodies without a joint."""
 
     def weld(b):
@@ -256,7 +258,7 @@ def self_pairs(geoms: list[dict], parent: dict[str, str], welded: set[str], excl
             p2 = weld(parent[w2]) if w2 != "world" else "world"
             if filterparent and w1 != "world" and w2 != "world" and (w1 == p2 or w2 == p1):
                 continue
-            if frozenset((w1, w2)) in excludes:
+            if frozenset((g1["body"], g2["body"])) in excludes:
                 continue
             out.append([g1["name"], g2["name"]])
             seen.add(frozenset((g1["name"], g2["name"])))

@@ -537,9 +537,12 @@ def test_self_contact_pairs_follow_mujocos_filter():
     floor_only = {k: box.format(n=n, a=" contype='1' conaffinity='0'") for k, n in (("lf", "lfoot"), ("rf", "rfoot"))}
     d = load_mjcf(_pairs_doc(floor_only))
     assert "self_pairs" not in d and len(d["geoms"]) == 2
-    # <exclude> between the feet's weld bodies (the shins: the feet have no joint)
-    d = load_mjcf(_pairs_doc(feet, "<contact><exclude body1='ls' body2='rs'/></contact>"))
+    # <exclude> between the feet's bodies removes the pair; between their weld bodies (the shins:
+    # the feet have no joint) it does not (the geoms' own bodies are matched)
+    d = load_mjcf(_pairs_doc(feet, "<contact><exclude body1='lf' body2='rf'/></contact>"))
     assert "self_pairs" not in d
+    d = load_mjcf(_pairs_doc(feet, "<contact><exclude body1='ls' body2='rs'/></contact>"))
+    assert d["self_pairs"] == [["lfoot", "rfoot"]]
     # the parent filter: a shin geom and its thigh's geom never collide; the foot is welded to the
     # shin, so the foot and the thigh are a weld body and its parent too
     d = load_mjcf(_pairs_doc({"lt": box.format(n="lthigh", a=""), "lf": box.format(n="lfoot", a="")}))
