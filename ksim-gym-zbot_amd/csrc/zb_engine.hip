@@ -1726,6 +1726,28 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   r.Jv = 0.f;
   r.D = 0.f;
   r.aref = 0.f;
+  if (XG && bank == 1) {
+    /* the second bank (shins, hands: usually off the floor) first by a bound: no point of a geom
+       lies lower than its body's origin minus |geom_pos| minus the geom's bounding radius (box: the
+       half-diagonal; capsule: radius + half-length; cylinder: the rim's distance from the centre,
+       sqrt(r^2 + h^2); ellipsoid: the largest semi-axis; sphere: the radius). While no lane of the
+       wave can reach the margin (+1 mm against rounding), the bank has no row: the same state as
+       the full test below finds, without its shuffles and rotations */
+    const float zb = tsh(B.xp[2], gb);
+    const float gx = m->geom_pos[g][0], gy = m->geom_pos[g][1], gz = m->geom_pos[g][2];
+    const float s0 = m->geom_size[g][0], s1 = m->geom_size[g][1], s2 = m->geom_size[g][2];
+    const int ty = m->geom_type[g];
+    const float rb = ty == ZB_GEOM_BOX ? sqrtf(s0 * s0 + s1 * s1 + s2 * s2)
+                     : ty == ZB_GEOM_CAPSULE ? s0 + s1
+                     : ty == ZB_GEOM_CYLINDER ? sqrtf(s0 * s0 + s1 * s1)
+                     : ty == ZB_GEOM_ELLIPSOID ? fmaxf(s0, fmaxf(s1, s2)) : s0;
+    const bool reach = gvalid && zb - sqrtf(gx * gx + gy * gy + gz * gz) - rb <= m->floor_margin + 1e-3f;
+    if (__ballot(reach) == 0ull) {
+      r.nrow = 0;
+      r.exmask = 0u;
+      return;
+    }
+  }
   float Jc[CAP];
 #pragma unroll
   for (int e = 0; e < CAP; e++) Jc[e] = 0.f;

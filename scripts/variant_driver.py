@@ -1,6 +1,6 @@
 """Fixed C2 workload on one library build (diagnostic only): reset + N zb_step launches.
 
-    python scripts/variant_driver.py evariants/libeng_x.so [steps]
+    [MODEL=path.xml] python scripts/variant_driver.py evariants/libeng_x.so [steps]
 Used under rocprofv3 --pmc by scripts/pmc_variants.sh to count the step kernel's instructions.
 """
 import os
@@ -14,7 +14,12 @@ from zbot_amd.engine import HipEngine  # noqa: E402
 
 lib = os.path.abspath(sys.argv[1])
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-cm = compile_model()
+if os.environ.get("MODEL"):  # an MJCF file, e.g. the limbs asset (the general-collider kernels)
+    from zbot_amd.mjcf import load_mjcf  # noqa: E402
+
+    cm = compile_model(load_mjcf(os.environ["MODEL"]))
+else:
+    cm = compile_model()
 g = torch.Generator(device="cuda")
 g.manual_seed(0)
 bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
