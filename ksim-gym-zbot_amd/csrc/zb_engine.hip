@@ -1883,7 +1883,7 @@ __device__ __forceinline__ float eval_one(float jar, float D, float& force, int&
 }
 
 /* row costs at given jar values (no state change); jx: the second bank's contact row (XG) */
-template <int XG>
+template <int XG, bool XA = true>
 __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jl_, float jx) {
   float f;
   int a;
@@ -1896,7 +1896,7 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
     const float k2 = eval_one(jl_, r.Dl, f, a);
     cost += r.hl ? k2 : 0.f;
   }
-  if constexpr (XG) {
+  if constexpr (XG && XA) {
     const float k3 = eval_one(jx, r.x.D, f, a);
     cost += r.x.ex ? k3 : 0.f;
   }
@@ -1942,7 +1942,7 @@ __device__ __forceinline__ float colsum16(JP Jrow, float fr) {
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
 /* returns this lane's cost share; the caller reduces it over the team (alone, or together with
    the Newton loop's other per-iteration sums in one tsum_n) */
-template <int XG>
+template <int XG, bool XA = true>
 __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, const float jr[CAP], float qacc,
                                                        float qs, float fs, float Ma, float& grad) {
   const int ddep = vopq(c.ddep);
@@ -1973,7 +1973,7 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
   if (r.ex) L->rowF[c.l] = r.f;
   L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
   float sx0 = 0.f, sx1 = 0.f;
-  if (XG && r.x.any) {
+  if (XG && XA && r.x.any) {
     float f3;
     int a3;
     const float k3 = eval_one(r.x.jar, r.x.D, f3, a3);
@@ -2002,10 +2002,10 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
   grad = Ma - fs - qc;
   return cost;
 }
-template <int XG>
+template <int XG, bool XA = true>
 __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, const float jr[CAP], float qacc, float qs,
                                                   float fs, float Ma, float& grad) {
-  return tsum(update_constraint_lane<XG>(c, r, jr, qacc, qs, fs, Ma, grad));
+  return tsum(update_constraint_lane<XG, XA>(c, r, jr, qacc, qs, fs, Ma, grad));
 }
 
 /* G_f = sum_{r in foot f} D_r J_r J_r' (depth-indexed 12x12) for both feet of
@@ -2081,7 +2081,7 @@ __device__ __forceinline__ void add_rows(uint32_t tb, JP J, const float* da, int
  * H of the previous build is updated with the rows whose activity changed
  * (+-D_r J_r J_r') -- MuJoCo's Newton also only re-assembles on a change of
  * the active set, and the change is usually a handful of rows. XG: both banks. */
-template <int XG>
+template <int XG, bool XA = true>
 __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo,
                                                 int pa2) {
   const int ddep = vopq(c.ddep);
@@ -2093,7 +2093,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     Hd = load_mrow(c, H);
     tb = 0u;
     jdj_mfma<false>();
-    if (XG && r.x.any) {
+    if (XG && XA && r.x.any) {
       /* the second bank's D (rowDA is free once the first bank's J'DJ has read it) */
       tsync();
       L->rowDA[c.l] = (r.x.ex && r.x.act) ? r.x.D : 0.f;
@@ -2118,7 +2118,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
          so they need no mask */
       for (int e = 0; e < CAP; e++) H[e] += g0[e] + g1[e];
       Hd += d0 + d1;
-      if (XG && r.x.any) {
+      if (XG && XA && r.x.any) {
         const float* GX = &L->Hs[0][0] + ddep * CAP;
         const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
         const float* G2 = f2 ? GX : &L->L[31][0];
@@ -2137,7 +2137,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     const float dl = r.ex ? ((r.act ? r.D : 0.f) - (pa ? r.D : 0.f)) : 0.f;
     L->rowF[c.l] = dl; /* rowF is free until the next update_constraint */
     tb = team_ballot(dl != 0.f) & c.rowmask;
-    if (XG && r.x.any) {
+    if (XG && XA && r.x.any) {
       dl2 = r.x.ex ? ((r.x.act ? r.x.D : 0.f) - (pa2 ? r.x.D : 0.f)) : 0.f;
       ch2 = team_ballot(dl2 != 0.f); /* team-uniform: some row of the bank changed */
       tb2 = ch2 & c.rowmask2;        /* per dof lane: the changed rows on its chain */
@@ -2164,7 +2164,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     tsync();
     if (c.l < NV) add_rows(tb2, (const gfloat_t*)xrows(L), L->rowF, ddep, H, Hd);
   }
-  if (XG && full && r.x.any) tsync(); /* the second bank's G rows in Hs[] are read before H is stored there */
+  if (XG && XA && full && r.x.any) tsync(); /* the second bank's G rows in Hs[] are read before H is stored there */
   st_row(&L->Hs[c.l][0], H);
   L->Hsd[c.l] = Hd;
   tsync();
@@ -2174,7 +2174,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
 }
 
 /* exact line search along `search`; returns alpha (team-uniform) and Mv/Jv */
-template <int XG>
+template <int XG, bool XA = true>
 __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float jr[CAP], float search, float Ma, float fs,
                                              float grad, float& Mv) {
   CP cfg = c.cfg;
@@ -2182,7 +2182,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   /* leaves search in vec[V_TMP]; J rows are zero where no contact: no branch around the loads */
   float unused_;
   Mv = mul_m_dot(c, r, jr, search, V_TMP, r.Jv, -1, unused_);
-  if constexpr (XG) r.x.Jv = r.x.any ? row_dot_x(c, r, V_TMP) : 0.f;
+  if constexpr (XG && XA) r.x.Jv = r.x.any ? row_dot_x(c, r, V_TMP) : 0.f;
   tsync();
   /* the quadratic's coefficients and the slope/curvature at alpha = 0 in one reduction:
      d1(0) = search . grad (the gradient update_constraint left for the current active
@@ -2215,8 +2215,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   /* the iteration loop in two copies, with and without the joint-limit row (LIM): a branch on
      r.anyl inside the evaluation is if-converted by the compiler into selects around the row's
      arithmetic, which then runs in every evaluation */
-  auto iterate = [&](auto lim) -> float {
+  auto iterate = [&](auto lim, auto xany) -> float {
     constexpr bool LIM = decltype(lim)::value;
+    constexpr bool XANY = decltype(xany)::value; /* XG: the second bank has rows in the wave */
     auto eval = [&](float alpha, float& e1, float& e2) {
       /* branch-free; rows that do not exist or are inactive add exact zeros */
       float g1, g2;
@@ -2240,8 +2241,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
         g1 += DlJ * fminf(x, 0.f);
         g2 += x < 0.f ? DlJ2 : 0.f;
       }
-      if (XG && r.x.any) {
-        /* second-bank contact row */
+      if constexpr (XANY) {
+        /* second-bank contact row (the copy without it runs while the bank has no row in the wave;
+           a branch on r.x.any here was if-converted as the joint-limit one was) */
         const float x = r.x.jar + alpha * r.x.Jv;
         g1 += DXJ * fminf(x, 0.f);
         g2 += x < 0.f ? DXJ2 : 0.f;
@@ -2263,11 +2265,12 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
     }
     return alpha;
   };
-  return r.anyl ? iterate(BoolC<true>{}) : iterate(BoolC<false>{});
+  /* XA: the caller's instantiation for a wave whose second bank has rows (solve_newton / solve_cg) */
+  return r.anyl ? iterate(BoolC<true>{}, BoolC<XG != 0 && XA>{}) : iterate(BoolC<false>{}, BoolC<XG != 0 && XA>{});
 }
 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
-template <int XG>
+template <int XG, bool XA = true>
 __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters,
                                               bool live) {
   CP cfg = c.cfg;
@@ -2286,13 +2289,13 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   jw -= r.aref;
   js -= r.aref;
   float jwx = 0.f, jsx = 0.f;
-  if (XG && r.x.any) {
+  if (XG && XA && r.x.any) {
     jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
     jsx = row_dot_x(c, r, V_TMP2) - r.x.aref;
   }
   tsync();
-  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
-                  rows_cost<XG>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
+                  rows_cost<XG, XA>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
   tsum_n<2>(cws);
   const float cw = cws[0], cs = cws[1];
   if (cw > cs) {
@@ -2309,9 +2312,9 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   r.jl = r.sl * x - r.al;
   float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
-  float cost = update_constraint<XG>(c, r, jr, x, qs, fs, Ma, grad);
+  float cost = update_constraint<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
-  float Dinv = hessian_factor<XG>(c, r, true, 0, 0, 0, 0);
+  float Dinv = hessian_factor<XG, XA>(c, r, true, 0, 0, 0, 0);
   STAMP(S_HESS0);
   float search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
@@ -2319,7 +2322,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   while (live && it < cfg->iterations) {
     float Mv;
     STAMP(S_CHECK);
-    float alpha = line_search<XG>(c, r, jr, search, Ma, fs, grad, Mv);
+    float alpha = line_search<XG, XA>(c, r, jr, search, Ma, fs, grad, Mv);
     STAMP(S_LS);
     if (alpha == 0.f) break;
     x += alpha * search;
@@ -2333,7 +2336,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
        value, so the bits of separate tsum calls): cost, |grad|^2 and the active-set change */
     float red[3];
-    red[0] = update_constraint_lane<XG>(c, r, jr, x, qs, fs, Ma, grad);
+    red[0] = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
     red[2] = (r.act != pa || r.actf != pf || (XG && r.x.act != pa2)) ? 1.f : 0.f;
     if (r.anyl && r.actl != plo) red[2] = 1.f;
@@ -2350,7 +2353,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = red[2] > 0.f;
-    if (changed) Dinv = hessian_factor<XG>(c, r, false, pa, pf, plo, pa2);
+    if (changed) Dinv = hessian_factor<XG, XA>(c, r, false, pa, pf, plo, pa2);
     STAMP(S_HESS);
     const float mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
@@ -2367,7 +2370,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
    the smooth factor of M that forward() left in L[] / Dk / Di (DinvM: this lane's 1/D), with
    Polak-Ribiere beta = max(0, g . (Mg - Mg_prev) / max(MINVAL, g_prev . Mg_prev)). No Hessian is
    built or factored. Returns qacc (dof lane). */
-template <int XG>
+template <int XG, bool XA = true>
 __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters, bool live,
                                           float DinvM) {
   CP cfg = c.cfg;
@@ -2384,13 +2387,13 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   jw -= r.aref;
   js -= r.aref;
   float jwx = 0.f, jsx = 0.f;
-  if (XG && r.x.any) {
+  if (XG && XA && r.x.any) {
     jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
     jsx = row_dot_x(c, r, V_TMP2) - r.x.aref;
   }
   tsync();
-  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
-                  rows_cost<XG>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
+                  rows_cost<XG, XA>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
   tsum_n<2>(cws);
   if (cws[0] > cws[1]) {
     x = qs;
@@ -2405,13 +2408,13 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   r.jl = r.sl * x - r.al;
   const float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
-  float cost = update_constraint<XG>(c, r, jr, x, qs, fs, Ma, grad);
+  float cost = update_constraint<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
   float mg = solve_ldl(c, grad, DinvM);
   float search = -mg;
   int it = 0;
   while (live && it < cfg->iterations) {
     float Mv;
-    const float alpha = line_search<XG>(c, r, jr, search, Ma, fs, grad, Mv);
+    const float alpha = line_search<XG, XA>(c, r, jr, search, Ma, fs, grad, Mv);
     if (alpha == 0.f) break;
     x += alpha * search;
     Ma += alpha * Mv;
@@ -2421,7 +2424,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     if (r.anyl) r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
     float red[2];
-    red[0] = update_constraint_lane<XG>(c, r, jr, x, qs, fs, Ma, grad);
+    red[0] = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
     tsum_n<2>(red);
     cost = red[0];
@@ -2526,8 +2529,14 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   qacc = qs;
   if (__ballot(nrows > 0) != 0ull) {
     int it2 = 0;
-    const float qn = SOLVER == ZB_SOLVER_CG ? solve_cg<XG>(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM)
-                                            : solve_newton<XG>(c, r, qs, fs, ls.w, it2, nrows > 0);
+    /* XG: the solver in two copies, with and without the second bank's terms (wave-uniform
+       r.x.any; branches on it inside the loops were if-converted into every evaluation) */
+    auto solve = [&](auto xa) -> float {
+      constexpr bool XA = decltype(xa)::value;
+      return SOLVER == ZB_SOLVER_CG ? solve_cg<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM)
+                                    : solve_newton<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0);
+    };
+    const float qn = (XG != 0 && r.x.any) ? solve(BoolC<true>{}) : solve(BoolC<false>{});
     if (nrows > 0) {
       qacc = qn;
       iters += it2;
