@@ -359,15 +359,16 @@ def bench_c1(cm, dev, rank: int, world: int, seed: int, n: int = 64, T: int = 12
 
 
 def bench_general_colliders(cfg, n: int, steps: int, warmup: int, dev, rank: int, world: int, seed: int,
-                            groups: int) -> dict:
-    """C2 on the limbs model (assets/zbot_like_limbs.xml: shin boxes and hand capsules collide with
+                            groups: int, asset: str = "zbot_like_limbs.xml") -> dict:
+    """C2 on the limbs model (assets/zbot_like_limbs.xml: a shin box and a hand capsule collide with
     the floor besides the soles), which runs the general-collider kernel instantiation (DESIGN.md
-    §4j); same groups and actions as the headline."""
+    §4j); same groups and actions as the headline. asset="zbot_like_cyl.xml": the cylinder foot,
+    cylinder shin and ellipsoid hand model (the third instantiation)."""
     from zbot_amd import compile_model  # noqa: PLC0415
     from zbot_amd.engine import EnvGroups, HipEngine  # noqa: PLC0415
     from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
 
-    path = os.path.join(ROOT, "ksim-gym-zbot_amd", "assets", "zbot_like_limbs.xml")
+    path = os.path.join(ROOT, "ksim-gym-zbot_amd", "assets", asset)
     cm = compile_model(load_mjcf(path))
     if groups > 1:
         eng = EnvGroups(cm, cfg, n, groups=groups, env_offset=rank * n, device=dev.index, seed=seed)
@@ -379,7 +380,7 @@ def bench_general_colliders(cfg, n: int, steps: int, warmup: int, dev, rank: int
     wall = _timed_steps(lambda t: eng.step(acts[t % 64], extras=False), steps, warmup, dev, world)
     eng.check()
     return {
-        "workload": f"C2 on the limbs model ({os.path.relpath(path, ROOT)}: {len(cm.geom_names)} floor colliders "
+        "workload": f"C2 on {os.path.relpath(path, ROOT)} ({len(cm.geom_names)} floor colliders "
                     f"{cm.geom_names}), {n} envs/GPU, {groups} env groups, {steps} timed steps (after {warmup})",
         "env_steps_per_s": world * n * steps / wall,
         "ms_per_step": 1e3 * wall / steps,
@@ -543,8 +544,8 @@ def main() -> None:
     ap.add_argument("--no-c2-rollout", action="store_true",
                     help="skip the C2-as-stated leg (one 256-step rollout with resets inside, timed whole)")
     ap.add_argument("--no-extra-legs", action="store_true",
-                    help="skip the ksim_env (ZbotWalkingEnv.step), train_defaults (512 x 200) and general_colliders "
-                         "(limbs model) legs")
+                    help="skip the ksim_env (ZbotWalkingEnv.step), train_defaults (512 x 200), c1_gpu, "
+                         "general_colliders (limbs model) and cylinder_colliders (cyl model) legs")
     ap.add_argument("--inloop-critic", type=int, default=0,
                     help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
                          "(1 one-wave, 2 two-wave, 3 four-wave; DESIGN.md §4f); 0 = the 8-wave critic afterwards")
@@ -637,6 +638,8 @@ def main() -> None:
         extra_legs["c1_gpu"] = bench_c1(cm, dev, rank, world, args.seed)
         extra_legs["general_colliders"] = bench_general_colliders(cfg, n, args.steps, args.warmup, dev, rank, world,
                                                                   args.seed, G)
+        extra_legs["cylinder_colliders"] = bench_general_colliders(cfg, n, args.steps, args.warmup, dev, rank, world,
+                                                                   args.seed, G, "zbot_like_cyl.xml")
 
     eng.reset()
     for t in range(args.warmup):
