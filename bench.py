@@ -3,6 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--config c1|c2|c3|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
+--gpus N is authoritative: without torchrun (WORLD_SIZE unset) and N > 1, bench.py spawns the N
+rank processes itself; under torchrun WORLD_SIZE must equal N; with nccl (RCCL) N GPUs must be
+visible. Any mismatch exits with status 2 before a GPU call. The line reports `ranks_seen`.
+
 A "step" is one zb_step over all E envs of a GPU (20 physics substeps each,
 Newton solver 8 / 8 line-search iterations, observations, rewards, auto-reset)
 — the hot path of ksim's step_engine for train.py's ZbotWalkingTask
@@ -515,7 +519,81 @@ def bench_rollout_pipeline(eng, n: int, T: int, reps: int, dev, world: int, inlo
     }
 
 
-def main() -> None:
+def _free_port() -> int:
+    import socket  # noqa: PLC0415
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_entry(local_rank: int, world: int, port: int, argv: list) -> None:
+    """One spawned rank of a self-launched `bench.py --gpus N`: the torch.distributed.run environment
+    (rank = local rank on this one node), then the same main() as under torchrun."""
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    main(argv)
+
+
+def launch_ranks(world: int, argv: list) -> int:
+    """`bench.py --gpus N` without torchrun: start N rank processes (spawn: fresh interpreters; this
+    parent makes no GPU call, it only counts devices, which does not initialise HIP on this image)
+    and wait for all of them. Returns the exit status (non-zero if any rank failed)."""
+    import torch.multiprocessing as mp  # noqa: PLC0415
+
+    try:
+        mp.start_processes(_rank_entry, args=(world, _free_port(), argv), nprocs=world, join=True,
+                           start_method="spawn")
+    except Exception as e:  # ProcessRaisedException / ProcessExitedException: a rank failed
+        print(f"bench.py: a rank failed: {e}", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def check_world(args) -> tuple[int, bool]:
+    """The world size bench.py will run at, and whether this process must launch the ranks itself.
+    --gpus N is authoritative: under torchrun WORLD_SIZE must equal it, and the nccl backend (RCCL:
+    one rank per GPU) needs N visible devices. Exits with status 2 on a mismatch, before any GPU call."""
+    import torch  # noqa: PLC0415
+
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None and int(env) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env} but --gpus {args.gpus}: launch exactly --gpus ranks", file=sys.stderr)
+        sys.exit(2)
+    if args.gpus < 1:
+        print(f"bench.py: --gpus {args.gpus} < 1", file=sys.stderr)
+        sys.exit(2)
+    if args.gpus > 1 and args.dist_backend == "nccl" and not args.launch_probe:
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} with the nccl backend (RCCL, one rank per GPU) but only {ndev} "
+                  "device(s) are visible", file=sys.stderr)
+            sys.exit(2)
+    return args.gpus, env is None and args.gpus > 1
+
+
+def launch_probe(world: int, backend: str) -> None:
+    """--launch-probe: the multi-rank launch alone, no GPU work (CPU-testable with gloo): every rank
+    joins the process group and all_gathers its rank; rank 0 prints the ranks it saw."""
+    import torch  # noqa: PLC0415
+    import torch.distributed as dist  # noqa: PLC0415
+
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend)
+    seen = [None] * world
+    if dist.is_initialized():
+        dist.all_gather_object(seen, rank)
+    else:
+        seen = [rank]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_seen": dist.get_world_size() if dist.is_initialized() else 1,
+                          "ranks": seen, "pid_parent": os.getppid(), "torch": torch.__version__}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def main(argv: list | None = None) -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
@@ -556,7 +634,19 @@ def main() -> None:
                     help="initialise the process group even at WORLD_SIZE 1 (under torch.distributed.run with one "
                          "rank): the barriers, the max-over-ranks timer and the statistics all_gather then run "
                          "through RCCL on a one-GPU box")
-    args = ap.parse_args()
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="run only the multi-rank launch (process group + all_gather of the ranks), no GPU work")
+    argv = sys.argv[1:] if argv is None else argv
+    args = ap.parse_args(argv)
+
+    # --gpus N is authoritative (before any GPU call): torchrun's WORLD_SIZE must equal it, and
+    # without torchrun this process starts the N ranks itself
+    world, self_launch = check_world(args)
+    if self_launch:
+        sys.exit(launch_ranks(world, argv))
+    if args.launch_probe:
+        launch_probe(world, args.dist_backend)
+        return
 
     import torch  # noqa: PLC0415
     import torch.distributed as dist  # noqa: PLC0415
@@ -566,7 +656,6 @@ def main() -> None:
     from zbot_amd.engine import EnvGroups, HipEngine  # noqa: PLC0415
     from zbot_amd.metrics import FP32_PEAK_TFLOPS, HBM_PEAK_GBS, bytes_per_env_step  # noqa: PLC0415
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
@@ -576,6 +665,9 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            print(f"bench.py: the process group has {dist.get_world_size()} ranks, --gpus {world}", file=sys.stderr)
+            sys.exit(2)
 
     conf = CONFIGS[args.config]
     n = args.envs or conf["envs"]
@@ -722,6 +814,7 @@ def main() -> None:
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
+            "ranks_seen": dist.get_world_size() if dist.is_initialized() else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,

@@ -4,7 +4,8 @@ RCCL needs one GPU per rank, so on the one-GPU test box two processes share cuda
 over gloo; the data path has no collective either way. Checks:
   * two ranks, each a HipEngine over its half of the global envs (env_offset = rank * n), give
     bit-identical per-env states to one process over all envs (RNG keyed by global env id);
-  * bench.py under torch.distributed.run with 2 ranks prints one JSON line with the whole-job value;
+  * bench.py under torch.distributed.run with 2 ranks prints one JSON line with the whole-job value,
+    and so does `bench.py --gpus 2` launched without torchrun (it starts its ranks itself);
   * RCCL itself at world size 1 (one GPU, one rank): the statistics reduction's all_gather and the
     barriers through the `nccl` backend, in a spawned rank and in bench.py --init-dist.
 """
@@ -97,6 +98,25 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert res["n_gpus"] == 2 and res["config"]["global_envs"] == 2048 and res["scaling"] == "weak"
     assert res["value"] > 0 and np.isfinite(res["value"])
     assert res["rollout_pipeline"]["env_steps_per_s"] > 0 and res["ppo_inputs"]["gae_kernel_ms"] > 0
+    assert res["ranks_seen"] == 2
+
+
+def test_bench_self_launch_two_ranks():
+    # `bench.py --gpus 2` without torchrun starts its two ranks itself (spawn, from a parent that
+    # made no GPU call); gloo rehearsal: both ranks share cuda:0 on the one-GPU box
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "3",
+           "--warmup", "1", "--envs", "1024", "--no-cpu-baseline", "--no-extra-legs", "--no-policy", "--no-pipeline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["ranks_seen"] == 2 and res["process_group"] == "gloo"
+    assert res["config"]["global_envs"] == 2048 and res["value"] > 0
 
 
 def _run_rccl_rank(rank, world, port, outdir):
