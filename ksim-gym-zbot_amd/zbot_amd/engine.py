@@ -398,9 +398,11 @@ class EnvGroups:
             raise ZbError(f"action must be [{self.n}, {cs.NJ}], got {tuple(a.shape)}")
         self.fork()
         for s in self.streams:
-            # the group streams read `a` after step() returns (no join): keep its block from being
-            # reused on the caller's stream before they are done with it
-            a.record_stream(s)
+            # the group streams read `a` (and write reward / done) after step() returns (no join):
+            # keep those blocks from being reused on the caller's stream before they are done
+            for t in (a, reward, done):
+                if t is not None:
+                    t.record_stream(s)
         for g, (e, s, (lo, hi)) in enumerate(self.groups()):
             with self.torch.cuda.stream(s):
                 if events is not None:
@@ -435,7 +437,14 @@ class EnvGroups:
 
     def feet_airtime_exact(self, reward0=None, terms0=None, curriculum: float = 1.0) -> None:
         """HipEngine.feet_airtime_exact per group, on the group's stream after its last step;
-        reward0 [n] / terms0 [n, 12] are the rollout's row-0 buffers (nullable). Pending like step()."""
+        reward0 [n] / terms0 [n, 12] are the rollout's row-0 buffers (nullable). Pending like step().
+        The group streams first wait for the caller's stream (fork): the row-0 buffers may have been
+        written there after the last step() (e.g. a trajectory stacked after the loop)."""
+        self.fork()
+        for s in self.streams:
+            for t in (reward0, terms0):
+                if t is not None:
+                    t.record_stream(s)
         for g, (e, s, (lo, hi)) in enumerate(self.groups()):
             with self.torch.cuda.stream(s):
                 e.feet_airtime_exact(None if reward0 is None else reward0[lo:hi],

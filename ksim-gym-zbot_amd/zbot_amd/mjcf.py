@@ -298,6 +298,7 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
     parent_of: dict[str, str] = {}
     welded: set[str] = set()
     colliding: list[dict] = []  # every robot geom with contype or conaffinity, for self_pairs
+    robot_geoms: set[str] = set()  # every named robot geom, visual-only ones included (<contact><pair>)
 
     servo_classes = dict(servo_classes if servo_classes is not None else tmpl.get("servo_classes", {}))
     tmpl_servo = {b["joint"]["name"]: b["joint"].get("servo") for b in tmpl["bodies"] if "joint" in b}
@@ -418,8 +419,10 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
             if c.tag == "geom":
                 ga = defaults.attrs(c, cls)
                 ct, ca = int(ga.get("contype", "1")), int(ga.get("conaffinity", "1"))
+                if "name" in ga:
+                    robot_geoms.add(ga["name"])
                 if ct == 0 and ca == 0:
-                    continue  # visual only
+                    continue  # visual only (an explicit <pair> still collides it, below)
                 gt = ga.get("type", "sphere")
                 gname = ga.get("name", f"{name}_geom{len(colliding)}")
                 colliding.append({"name": gname, "body": name, "type": gt, "contype": ct, "conaffinity": ca})
@@ -498,9 +501,9 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
     for ce in root.findall("contact"):
         for ex in ce.findall("exclude"):
             excludes.add(frozenset((ex.get("body1"), ex.get("body2"))))
-        names = {g["name"] for g in colliding}
+        # MuJoCo collides an explicit pair whatever the geoms' contype / conaffinity
         for pr in ce.findall("pair"):
-            if pr.get("geom1") in names and pr.get("geom2") in names:
+            if pr.get("geom1") in robot_geoms and pr.get("geom2") in robot_geoms:
                 explicit.append((pr.get("geom1"), pr.get("geom2")))
     sp = self_pairs(colliding, parent_of, welded, excludes, explicit, filterparent)
     if sp:

@@ -17,8 +17,6 @@ clone them if they must survive the next step).
 
 from __future__ import annotations
 
-from dataclasses import dataclass
-
 from . import cstructs as cs
 from .config import default_config
 from .constants import JOINT_BIASES, REWARDS
@@ -86,10 +84,11 @@ class StepResult:
     """One step's outputs under ksim's names (views into the engine's output buffers).
 
     With env groups (ZbotWalkingEnv(groups=G > 1)) the buffers are still being written on the group
-    streams when step() returns. The first read of any field makes the caller's current stream wait
-    for every group (EnvGroups.join; no host synchronisation), so a loop that only steps, as an
-    open-loop rollout does, never serialises the groups, and a loop that reads the outputs sees
-    them complete."""
+    streams when step() returns. Every read of a field makes the stream that is current at that read
+    wait for every group (EnvGroups.join: one stream-wait per group, no host synchronisation), so a
+    loop that only steps, as an open-loop rollout does, never serialises the groups, and a read under
+    any stream context (e.g. `with torch.cuda.stream(side)`) sees the outputs complete on that stream.
+    It is not a dataclass (reads are properties); as_dict() gives the fields as a plain dict."""
 
     FIELDS = ("obs", "actor_inputs", "critic_inputs", "reward", "reward_terms", "done", "success")
 
@@ -100,9 +99,12 @@ class StepResult:
 
     def _get(self, k):
         if self._join is not None:
-            self._join()
-            self._join = None
+            self._join()  # on every read: the join orders only the stream current at this read
         return self._v[k]
+
+    def as_dict(self) -> dict:
+        """Every field (joined on the current stream), for callers that used dataclasses.asdict."""
+        return {k: self._get(k) for k in self.FIELDS}
 
     obs = property(lambda self: self._get("obs"))
     actor_inputs = property(lambda self: self._get("actor_inputs"))

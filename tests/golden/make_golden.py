@@ -34,6 +34,9 @@ CASES = {
 }
 
 
+EXACT_STEPS = 16  # tests/test_gpu_parity.py GOLDEN_EXACT_STEPS: the per-env state is also kept at this step
+
+
 def run_case(name, n, steps, seed, push, randomize, std, solver="newton"):
     cm = compile_model()
     cfg = default_config(push=push, randomize=randomize, solver=solver)
@@ -46,7 +49,10 @@ def run_case(name, n, steps, seed, push, randomize, std, solver="newton"):
         actions.append(a)
         rewards.append(out["reward"])
         dones.append(out["done"])
-    return dict(
+        if t + 1 == EXACT_STEPS:
+            state_exact = env.state.copy()
+    extra = {"state_at_exact": state_exact} if steps > EXACT_STEPS else {}
+    return dict(**extra,
         reset_obs_actor=oa0, reset_obs_critic=oc0, actions=np.stack(actions), reward=np.stack(rewards),
         done=np.stack(dones), final_state=env.state.copy(), final_rand=env.rand.copy(),
         final_obs_actor=out["obs_actor"], final_obs_critic=out["obs_critic"], final_terms=out["reward_terms"],

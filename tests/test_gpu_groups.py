@@ -192,3 +192,34 @@ def test_converted_actions_outlive_step_without_join(torch_gpu, cmodel):
     grp.join()
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_bits(grp.get_state()), _bits(one.get_state()))
+
+
+def test_airtime_patch_orders_after_caller_writes(torch_gpu, cmodel):
+    """the row-0 FeetAirtime patch runs on the group streams; a trajectory buffer the
+    caller fills on its own stream after the last step() (here: stacked behind a long sleep kernel)
+    must be written before the patch adds to it. One handle on one stream is the reference."""
+    torch = torch_gpu
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    n, T = 300, 12
+    cfg = default_config(push=True)
+    acts = _actions(torch, cmodel, T, n, 5)
+    out = {}
+    for name, eng in (("one", HipEngine(cmodel, cfg, n, seed=11)), ("grp", EnvGroups(cmodel, cfg, n, groups=3, seed=11))):
+        eng.reset()
+        eng.mark_rollout_start()
+        rows = []
+        for t in range(T):
+            o = eng.step(acts[t])
+            eng.join()
+            rows.append(o["reward"].clone())
+        torch.cuda._sleep(50_000_000)  # the caller's stream is busy: the stack below lands late
+        traj = torch.stack(rows)
+        eng.feet_airtime_exact(traj[0], None)
+        eng.join()
+        torch.cuda.synchronize()
+        out[name] = traj.cpu().numpy()
+        out[name + "_causal0"] = rows[0].cpu().numpy()
+    np.testing.assert_array_equal(out["grp"].view(np.uint32), out["one"].view(np.uint32))
+    # the patch changed row 0 for the envs whose feet touched down over the rollout
+    assert not np.array_equal(out["one"][0], out["one_causal0"])

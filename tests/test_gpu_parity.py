@@ -395,10 +395,13 @@ def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
     np.testing.assert_allclose(out["obs_actor"].cpu().numpy(), g["reset_obs_actor"], atol=1e-4)
     np.testing.assert_allclose(out["obs_critic"].cpu().numpy(), g["reset_obs_critic"], atol=1e-3, rtol=1e-4)
     rew, done = [], []
+    state_ex = None
     for t in range(steps):
         o = eng.step(torch.from_numpy(g["actions"][t]).cuda())
         rew.append(o["reward"].cpu().numpy().copy())
         done.append(o["done"].cpu().numpy().copy())
+        if t + 1 == GOLDEN_EXACT_STEPS:
+            state_ex = eng.get_state().cpu().numpy()
     rew, done = np.stack(rew), np.stack(done)
     ex = min(steps, GOLDEN_EXACT_STEPS)
     np.testing.assert_array_equal(done[:ex], g["done"][:ex])
@@ -407,11 +410,16 @@ def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
     e32 = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=seed)
     e64 = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=seed, precision="f64")
     e32.reset()
-    for t in range(8):
+    switch = np.zeros(n, bool)  # envs with a step at a discontinuity (fp32 / fp64 one-step qpos gap)
+    for t in range(min(steps, GOLDEN_EXACT_STEPS)):
         e64.state[:] = e32.state
         e64.rand[:] = e32.rand
         r64 = e64.step(g["actions"][t])["reward"]
         r32 = e32.step(g["actions"][t])["reward"]
+        qtol = (ONE_STEP_TOL_CG if solver == "cg" else ONE_STEP_TOL)["qpos"][0]
+        switch |= np.abs(e64.state[:, :27] - e32.state[:, :27]).max(1) > qtol
+        if t >= 8:
+            continue
         np.testing.assert_allclose(r32, g["reward"][t], rtol=1e-6, atol=1e-6)  # the replay is the fixture
         err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"], ref64=r64)
         for e in err.take_over():
@@ -421,6 +429,18 @@ def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
     if steps <= GOLDEN_EXACT_STEPS:
         err.add("final_base_pos", gs[:, :3], g["final_state"][:, :3], tol["final_base_pos"])
     else:
+        # the per-env pin at the end of the exact window: the base position at step 16
+        # against the fixture's oracle state there, every env but those whose trajectory crossed a
+        # discontinuity on the way (at most MaxErr.max_ill; their fp32 and fp64 steps part, so the
+        # two fp32 implementations may follow either side from there)
+        np.testing.assert_array_equal(e32.state[:, :27], g["state_at_exact"][:, :27])  # replay = fixture
+        keep = ~switch
+        print(f"[golden {name}] step {GOLDEN_EXACT_STEPS}: {int(switch.sum())} envs crossed a discontinuity "
+              f"{np.flatnonzero(switch).tolist()}, max |base pos err| over the rest "
+              f"{np.abs(state_ex[keep, :3] - g['state_at_exact'][keep, :3]).max():.2e}")
+        assert switch.sum() <= err.max_ill
+        err.add(f"base_pos[{GOLDEN_EXACT_STEPS}]", state_ex[keep, :3], g["state_at_exact"][keep, :3],
+                tol["final_base_pos"])
         golden_ensemble_check(name, rew, done, gs, g)
     err.add("final_rand", eng.get_rand().cpu().numpy(), g["final_rand"], 1e-6)
     err.report()

@@ -560,6 +560,12 @@ def test_self_contact_pairs_follow_mujocos_filter():
     # an explicit <pair> counts whatever the bits say
     d = load_mjcf(_pairs_doc(floor_only, "<contact><pair geom1='lfoot' geom2='rfoot'/></contact>"))
     assert d["self_pairs"] == [["lfoot", "rfoot"]]
+    # ... even between visual-only geoms (contype = conaffinity = 0): MuJoCo still collides the pair
+    vis = {k: box.format(n=n, a=" contype='0' conaffinity='0'") for k, n in (("lf", "lfoot"), ("rf", "rfoot"))}
+    d = load_mjcf(_pairs_doc(vis, "<contact><pair geom1='lfoot' geom2='rfoot'/></contact>"))
+    assert d["self_pairs"] == [["lfoot", "rfoot"]] and d["geoms"] == []
+    d = load_mjcf(_pairs_doc(vis))
+    assert "self_pairs" not in d
 
 
 def test_self_contacts_are_rejected_by_zb_create():
