@@ -391,6 +391,68 @@ def bench_general_colliders(cfg, n: int, steps: int, warmup: int, dev, rank: int
     }
 
 
+def bench_variant(cm, cfg, label: str, flops_file: str, n: int, steps: int, warmup: int, dev, rank: int, world: int,
+                  seed: int, groups: int) -> dict:
+    """C2 with one of the [U] physics switches flipped: the solver (CG instead of
+    Newton) or mj_Euler's implicit joint damping (ZB_F_EULERDAMP). Same envs, groups, actions and
+    timing as the headline (per-launch HIP events on each group's stream), with its own roofline:
+    the same algorithmic bytes, and the counted FLOPs of that configuration (scripts/count_flops.py)."""
+    import torch  # noqa: PLC0415
+    from zbot_amd.engine import EnvGroups, HipEngine  # noqa: PLC0415
+    from zbot_amd.metrics import FP32_PEAK_TFLOPS, HBM_PEAK_GBS, bytes_per_env_step  # noqa: PLC0415
+
+    G = max(1, groups)
+    eng = (EnvGroups(cm, cfg, n, groups=G, env_offset=rank * n, device=dev.index, seed=seed) if G > 1 else
+           HipEngine(cm, cfg, n, env_offset=rank * n, device=dev.index, seed=seed))
+    acts = _synthetic_actions(n, 64, dev, 1234 + rank, 0.05)
+    eng.reset()
+    stream = torch.cuda.current_stream(dev)
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(G)]
+          for _ in range(steps)]
+    for evt in ev:
+        for a, b in evt:
+            a.record(stream)
+            b.record(stream)
+
+    def step(t):
+        k = t - warmup
+        if G > 1:
+            eng.step(acts[t % 64], extras=False, events=ev[k] if k >= 0 else None)
+        else:
+            if k >= 0:
+                ev[k][0][0].record(stream)
+            eng.step(acts[t % 64], extras=False)
+            if k >= 0:
+                ev[k][0][1].record(stream)
+        if G > 1 and t == warmup + steps - 1:
+            eng.join()
+
+    wall = _timed_steps(step, steps, warmup, dev, world)
+    eng.check()
+    avg_ms = sum(a.elapsed_time(b) for evt in ev for a, b in evt) / (steps * G)
+    wall_ms = 1e3 * wall / steps
+    rate_ms = avg_ms if G == 1 else max(avg_ms, wall_ms)
+    bpe = bytes_per_env_step(extras=False, terms=True)
+    hbm = bpe * n / (rate_ms * 1e-3) / 1e9
+    out = {
+        "workload": f"C2 with {label}: {n} envs/GPU, {G} env groups, {steps} timed steps (after {warmup})",
+        "env_steps_per_s": world * n * steps / wall,
+        "ms_per_step": wall_ms,
+        "avg_solver_iters_per_env_step": eng.solver_iters().float().mean().item(),
+        "roofline": {"bound": "hbm", "achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm / HBM_PEAK_GBS,
+                     "kernel_avg_ms": avg_ms, "rate_ms": rate_ms, "algorithmic_bytes_per_env_step": bpe},
+    }
+    fpath = os.path.join(ROOT, "profiles", flops_file)
+    if os.path.exists(fpath):
+        with open(fpath) as f:
+            fl = json.load(f)["as_run"]["flops_per_env_step"]
+        tf = fl * n / (rate_ms * 1e-3) / 1e12
+        out["roofline_fp32"] = {"bound": "fp32-valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                "frac": tf / FP32_PEAK_TFLOPS, "algorithmic_flop_per_env_step": fl,
+                                "flops_file": os.path.relpath(fpath, ROOT)}
+    return out
+
+
 def bench_policy_in_loop(eng, n: int, steps: int, dev, rank: int, grouped=None) -> dict:
     """The GRU actor in the rollout loop: per control step the actor samples
     every env's action from its observation on the f32 matrix cores, then zb_step advances the
@@ -623,7 +685,8 @@ def main(argv: list | None = None) -> None:
                     help="skip the C2-as-stated leg (one 256-step rollout with resets inside, timed whole)")
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the ksim_env (ZbotWalkingEnv.step), train_defaults (512 x 200), c1_gpu, "
-                         "general_colliders (limbs model) and cylinder_colliders (cyl model) legs")
+                         "general_colliders (limbs model), cylinder_colliders (cyl model), the other solver's "
+                         "(cg_solver / newton_solver) and the eulerdamp legs")
     ap.add_argument("--inloop-critic", type=int, default=0,
                     help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
                          "(1 one-wave, 2 two-wave, 3 four-wave; DESIGN.md §4f); 0 = the 8-wave critic afterwards")
@@ -732,6 +795,17 @@ def main(argv: list | None = None) -> None:
                                                                   args.seed, G)
         extra_legs["cylinder_colliders"] = bench_general_colliders(cfg, n, args.steps, args.warmup, dev, rank, world,
                                                                    args.seed, G, "zbot_like_cyl.xml")
+        # the [U] physics switches timed both ways: the other solver, and implicit damping
+        other = "cg" if args.solver == "newton" else "newton"
+        extra_legs[f"{other}_solver"] = bench_variant(
+            cm, default_config(solver=other), f"the {other.upper() if other == 'cg' else 'Newton'} solver (ZbEnvConfig.solver)",
+            "r03_flops_count_cg.json" if other == "cg" else "r03_flops_count.json", n, args.steps, args.warmup, dev,
+            rank, world, args.seed, G)
+        extra_legs["eulerdamp"] = bench_variant(
+            cm, default_config(solver=args.solver, eulerdamp=True),
+            f"mj_Euler's implicit joint damping (ZB_F_EULERDAMP), {args.solver} solver",
+            "r05_flops_count_eulerdamp.json" if args.solver == "newton" else "r05_flops_count_cg_eulerdamp.json", n,
+            args.steps, args.warmup, dev, rank, world, args.seed, G)
 
     eng.reset()
     for t in range(args.warmup):

@@ -113,6 +113,9 @@ extern "C" {
 #define ZB_F_PUSH        2u   /* PushEvent (train.py:1459-1468), config 3 */
 #define ZB_F_RANDOMIZE   4u   /* physics randomizers (train.py:1441-1454), config 5 */
 #define ZB_F_AUTORESET   8u   /* reset done envs inside zb_step (ksim auto-reset) */
+#define ZB_F_EULERDAMP  16u   /* mj_Euler's implicit joint damping, qacc_e = (M + dt diag(damping))^-1 (qfrc_smooth +
+                                 qfrc_constraint): MuJoCo's default (mjDSBL_EULERDAMP clear). Off here: ksim
+                                 sets the disable bit on its MJX model [U]. train.py:1777-1781 */
 
 typedef struct ZbEnvConfig {
   int32_t  struct_bytes;

@@ -136,7 +136,7 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMalloc(&h->itpart, n * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(h->itpart, 0, n * sizeof(int32_t));
   if (e == hipSuccess && zb::needs_xg(model)) e = hipMalloc(&h->xj, (n + 1) * ZB_XJ_STRIDE * sizeof(float));
-  h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device, zb::needs_xg(model), cfg->solver));
+  h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device, zb::needs_xg(model), cfg->solver, (cfg->flags & ZB_F_EULERDAMP) ? 1 : 0));
 #if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
   {
     /* phase stamps: ZB_NSTAMP per env; wave times: 4 words per (chunk, pair), up to one chunk per
@@ -193,6 +193,7 @@ static zb::StepArgs base_args(ZbHandle* h) {
   a.itpart = h->itpart;
   a.solver = h->cfg.solver;
   a.xg = zb::needs_xg(&h->hmodel);
+  a.ed = (h->cfg.flags & ZB_F_EULERDAMP) ? 1 : 0;
   a.xj = h->xj;
   return a;
 }
@@ -323,7 +324,7 @@ int zb_set_step_chunks(ZbHandle* h, int k) {
   if (k == 0) {
     int rc = use_device(h);
     if (rc) return rc;
-    h->nchunk = choose_chunks(h->n, h->cfg.n_substeps, zb::step_resident_blocks(h->device, zb::needs_xg(&h->hmodel), h->cfg.solver));
+    h->nchunk = choose_chunks(h->n, h->cfg.n_substeps, zb::step_resident_blocks(h->device, zb::needs_xg(&h->hmodel), h->cfg.solver, (h->cfg.flags & ZB_F_EULERDAMP) ? 1 : 0));
   } else {
     h->nchunk = k > h->cfg.n_substeps ? h->cfg.n_substeps : k;
   }

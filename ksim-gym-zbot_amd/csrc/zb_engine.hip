@@ -626,6 +626,7 @@ struct LaneS {
   float ctrl;           /* actuator ctrl of this dof lane */
   float qacc;           /* last constrained qacc */
   float actforce;       /* actuator force (gear*clamped ctrl) */
+  float fq;             /* qfrc_smooth + qfrc_constraint of the last solve (implicit damping only) */
 };
 /* per-substep body outputs */
 struct BodyK {
@@ -2272,7 +2273,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
 template <int XG, bool XA = true>
 __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters,
-                                              bool live) {
+                                              bool live, float& ftot) {
   CP cfg = c.cfg;
   MP m = c.m;
   EnvL* L = c.L;
@@ -2360,6 +2361,9 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     search = -mg;
   }
   iters += it;
+  /* qfrc_smooth + qfrc_constraint at the returned qacc (grad = Ma - qfrc_smooth - J'f), for
+     mj_Euler's implicit damping */
+  ftot = Ma - grad;
   __builtin_amdgcn_s_setprio(0);
   return x;
 }
@@ -2372,7 +2376,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
    built or factored. Returns qacc (dof lane). */
 template <int XG, bool XA = true>
 __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters, bool live,
-                                          float DinvM) {
+                                          float DinvM, float& ftot) {
   CP cfg = c.cfg;
   MP m = c.m;
   EnvL* L = c.L;
@@ -2439,6 +2443,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     search = -mg + beta * search;
   }
   iters += it;
+  ftot = Ma - grad; /* as solve_newton */
   __builtin_amdgcn_s_setprio(0);
   return x;
 }
@@ -2527,22 +2532,26 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
      build runs on the matrix cores and needs every lane); an env without
      rows leaves the Newton loop at once and keeps qacc_smooth */
   qacc = qs;
+  float ftot = fs; /* qfrc_smooth (+ qfrc_constraint below) */
   if (__ballot(nrows > 0) != 0ull) {
     int it2 = 0;
+    float ft = 0.f;
     /* XG: the solver in two copies, with and without the second bank's terms (wave-uniform
        r.x.any; branches on it inside the loops were if-converted into every evaluation) */
     auto solve = [&](auto xa) -> float {
       constexpr bool XA = decltype(xa)::value;
-      return SOLVER == ZB_SOLVER_CG ? solve_cg<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM)
-                                    : solve_newton<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0);
+      return SOLVER == ZB_SOLVER_CG ? solve_cg<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM, ft)
+                                    : solve_newton<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, ft);
     };
     const float qn = (XG != 0 && r.x.any) ? solve(BoolC<true>{}) : solve(BoolC<false>{});
     if (nrows > 0) {
       qacc = qn;
+      ftot = ft;
       iters += it2;
     }
   }
   ls.qacc = (c.l < NV) ? qacc : 0.f;
+  ls.fq = (c.l < NV) ? ftot : 0.f;
   STAMP(S_CHECK);
   if (!with_sensors) return;
   /* ------------------- sensors (mj_rnePostConstraint etc.) ------------------ */
@@ -2642,10 +2651,28 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   STAMP(S_SENS);
 }
 
+/* ------------------------- implicit damping (EULERDAMP) --------------------- */
+/* mj_Euler with EULERDAMP enabled (MuJoCo's default; MJX forward.euler): the joint damping is
+   integrated implicitly, qacc_e = (M + dt diag(B))^-1 (qfrc_smooth + qfrc_constraint), and qvel
+   advances with qacc_e; qacc itself (sensors, qacc_warmstart) stays the solver's. M's rows are
+   still in L->M (the solvers only read them); the factor lands in L[] / Dk / Di, which the next
+   forward() rewrites. Wave-uniform: factor_ldl's Schur complement runs on the matrix cores. */
+__device__ __forceinline__ float implicit_damping(const Ctx& c, const LaneS& ls) {
+  tsync(); /* the solve's last reads of L[] are done before the factor overwrites it */
+  float X[CAP];
+  float Xd = load_mrow(c, X);
+  const float damp = keepf(c.L->par[P_DAMP][c.l & 31]);
+  Xd += (c.l < NV) ? c.cfg->dt * damp : 0.f;
+  const float Dinv = factor_ldl<true>(c, X, Xd, c.L->M);
+  return solve_ldl(c, ls.fq, Dinv);
+}
+
 /* ------------------------------ Euler integrate ----------------------------- */
-__device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls) {
+/* mj_Euler / mj_advance. ED: qvel advances with the implicit-damping qacc_e (implicit_damping). */
+template <bool ED>
+__device__ __forceinline__ void integrate(const Ctx& c, EnvS& s, LaneS& ls, float qacc_e) {
   const float dt = c.cfg->dt;
-  float vn = ls.v + dt * ls.qacc;
+  float vn = ls.v + dt * (ED ? qacc_e : ls.qacc);
   float v0 = tsh(vn, 0), v1 = tsh(vn, 1), v2 = tsh(vn, 2), w0 = tsh(vn, 3), w1 = tsh(vn, 4), w2 = tsh(vn, 5);
   if (c.l < NV) {
     ls.w = ls.qacc; /* mj_advance: qacc_warmstart */
@@ -3142,7 +3169,7 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
 #ifndef ZB_WAVES_PER_EU
 #define ZB_WAVES_PER_EU 2
 #endif
-template <int SOLVER, int XG>
+template <int SOLVER, int XG, int ED>
 __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   const int team = threadIdx.x / TEAM;
   /* Chunked step (a.nchunk > 1, one control step): the launch has npair * nchunk workgroups, each
@@ -3250,7 +3277,10 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       forward<SOLVER, XG>(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, it_pass);
       if (!ghost) iters += it_pass;
       if (!resetting && !ghost) {
-        integrate(c, s, ls);
+        /* wave-uniform: both teams integrate, or both run the reset / ghost pass */
+        float qacc_e = 0.f;
+        if constexpr (ED != 0) qacc_e = implicit_damping(c, ls);
+        integrate<ED != 0>(c, s, ls, qacc_e);
         STAMP(S_INT);
         if (++ss < cfg->n_substeps) {
           if (ss < ss_end) continue;
@@ -3473,15 +3503,17 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   }
 }
 
-int step_resident_blocks(int device, int xg, int solver) {
+int step_resident_blocks(int device, int xg, int solver, int ed) {
   int per_cu = 0, cus = 0;
   /* the instantiation the handle launches: CG and Newton differ in registers and LDS */
   hipError_t e;
-#define ZB_OCC(S, X) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<S, X>, 64, 0)
+#define ZB_OCC(S, X, D) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<S, X, D>, 64, 0)
+#define ZB_OCC2(S, D) (xg == 2 ? ZB_OCC(S, 2, D) : xg ? ZB_OCC(S, 1, D) : ZB_OCC(S, 0, D))
   if (solver == ZB_SOLVER_CG)
-    e = xg == 2 ? ZB_OCC(ZB_SOLVER_CG, 2) : xg ? ZB_OCC(ZB_SOLVER_CG, 1) : ZB_OCC(ZB_SOLVER_CG, 0);
+    e = ed ? ZB_OCC2(ZB_SOLVER_CG, 1) : ZB_OCC2(ZB_SOLVER_CG, 0);
   else
-    e = xg == 2 ? ZB_OCC(ZB_SOLVER_NEWTON, 2) : xg ? ZB_OCC(ZB_SOLVER_NEWTON, 1) : ZB_OCC(ZB_SOLVER_NEWTON, 0);
+    e = ed ? ZB_OCC2(ZB_SOLVER_NEWTON, 1) : ZB_OCC2(ZB_SOLVER_NEWTON, 0);
+#undef ZB_OCC2
 #undef ZB_OCC
   if (e != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
@@ -3502,6 +3534,33 @@ int step_resident_blocks(int device, int xg, int solver) {
     }                                                                                                     \
   } while (0)
 
+/* the step kernel's instantiation: solver x collider set x implicit damping (ZB_F_EULERDAMP) */
+#define ZB_LAUNCH_STEP(grid, block, s, args)                                                              \
+  do {                                                                                                    \
+    const int xg_ = (args).xg;                                                                            \
+    if ((args).ed) {                                                                                      \
+      if ((args).solver == ZB_SOLVER_CG) {                                                                \
+        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 2, 1>), grid, block, 0, s, args);     \
+        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 1, 1>), grid, block, 0, s, args);     \
+        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 0, 1>), grid, block, 0, s, args);              \
+      } else {                                                                                            \
+        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 2, 1>), grid, block, 0, s, args); \
+        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 1, 1>), grid, block, 0, s, args); \
+        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 0, 1>), grid, block, 0, s, args);          \
+      }                                                                                                   \
+    } else {                                                                                              \
+      if ((args).solver == ZB_SOLVER_CG) {                                                                \
+        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 2, 0>), grid, block, 0, s, args);     \
+        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 1, 0>), grid, block, 0, s, args);     \
+        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 0, 0>), grid, block, 0, s, args);              \
+      } else {                                                                                            \
+        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 2, 0>), grid, block, 0, s, args); \
+        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 1, 0>), grid, block, 0, s, args); \
+        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 0, 0>), grid, block, 0, s, args);          \
+      }                                                                                                   \
+    }                                                                                                     \
+  } while (0)
+
 hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   if (a.nchunk < 1 || (a.nchunk > 1 && (a.nsteps != 1 || !a.sched || !a.itpart))) return hipErrorInvalidValue;
@@ -3512,7 +3571,7 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   const StepArgs& b = a;
 #endif
   dim3 grid((unsigned)((b.n_envs + NTEAM - 1) / NTEAM * b.nchunk)), block(64);
-  ZB_LAUNCH_VARIANT(step_kernel, grid, block, s, b);
+  ZB_LAUNCH_STEP(grid, block, s, b);
   return hipGetLastError();
 }
 /* ksim's FeetAirtimeReward over one trajectory (train.py:503-546), row 0. The fused step

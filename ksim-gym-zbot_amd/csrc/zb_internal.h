@@ -60,10 +60,11 @@ struct StepArgs {
   int solver;               /* ZB_SOLVER_NEWTON / ZB_SOLVER_CG: which kernel instantiation runs */
   int xg;                   /* general colliders (zb_host.h needs_xg): 0 two-sole, 1 two banks, 2 two banks + cylinders / ellipsoids */
   float* xj;                /* xg: [n + 1, ZB_XJ_STRIDE] second-bank Jacobian rows (the last block: ghost teams) */
+  int ed;                   /* ZB_F_EULERDAMP: the step kernel integrates the joint damping implicitly */
 };
 
 /* workgroups of step_kernel resident on the device at once (occupancy x CUs) */
-int step_resident_blocks(int device, int xg, int solver);
+int step_resident_blocks(int device, int xg, int solver, int ed);
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s);
 hipError_t launch_reset(const StepArgs& a, hipStream_t s);

@@ -27,9 +27,14 @@ def default_config(
     ctrl_dt: float = CTRL_DT,
     max_episode_sec: float = 80.0,
     solver: str = "newton",
+    eulerdamp: bool = False,
 ) -> cs.ZbEnvConfig:
     """solver: "newton" (MuJoCo's default, mj_solNewton) or "cg" (mj_solCG, which MJX training setups
-    commonly select for speed); which one ksim 0.1.99 sets on the model is [U]."""
+    commonly select for speed); which one ksim 0.1.99 sets on the model is [U].
+
+    eulerdamp: mj_Euler's implicit joint damping (MuJoCo's default, mjDSBL_EULERDAMP clear): qvel
+    advances with (M + dt diag(damping))^-1 (qfrc_smooth + qfrc_constraint). Off by default: ksim
+    sets the disable bit on its MJX model [U], so the damping is explicit."""
     if solver not in ("newton", "cg"):
         raise ValueError(f"solver must be 'newton' or 'cg', got {solver!r}")
     c = cs.ZbEnvConfig()
@@ -43,6 +48,8 @@ def default_config(
         flags |= cs.F_RANDOMIZE
     if autoreset:
         flags |= cs.F_AUTORESET
+    if eulerdamp:
+        flags |= cs.F_EULERDAMP
     c.flags = flags
     c.n_substeps = int(round(ctrl_dt / dt))  # ksim: round(ctrl_dt / dt) physics steps per control step
     c.iterations = iterations  # train.py:1779
@@ -89,4 +96,5 @@ def config_flags(c: cs.ZbEnvConfig) -> dict:
         "push": bool(c.flags & cs.F_PUSH),
         "randomize": bool(c.flags & cs.F_RANDOMIZE),
         "autoreset": bool(c.flags & cs.F_AUTORESET),
+        "eulerdamp": bool(c.flags & cs.F_EULERDAMP),
     }

@@ -103,6 +103,7 @@ F_OBS_NOISE = 1
 F_PUSH = 2
 F_RANDOMIZE = 4
 F_AUTORESET = 8
+F_EULERDAMP = 16  # ZB_F_EULERDAMP: mj_Euler's implicit joint damping
 
 
 def _f(n: int, m: int = 0) -> type:

@@ -1042,7 +1042,10 @@ static void forward(const ZbModel* m, ZbData* d, real dt, const ZbEnvConfig* cfg
   make_constraint(m, d, dt);
   smooth_forces(m, d);
   if (d->nefc == 0) {
-    for (int i = 0; i < m->nv; i++) d->qacc[i] = d->qacc_smooth[i];
+    for (int i = 0; i < m->nv; i++) {
+      d->qacc[i] = d->qacc_smooth[i];
+      d->qfrc_constraint[i] = 0;
+    }
   } else if (cfg->solver == ZB_SOLVER_CG) {
     solve_cg(m, d, cfg);
   } else {
@@ -1105,9 +1108,28 @@ static void sensors(const ZbModel* m, ZbData* d) {
 }
 
 /* -------------------------------- mj_Euler ---------------------------------- */
-static void integrate(const ZbModel* m, ZbData* d, real dt) {
+/* eulerdamp (ZB_F_EULERDAMP, MuJoCo's default when mjDSBL_EULERDAMP is clear; engine_forward.c
+   mj_Euler, MJX forward.py euler): the joint damping is integrated implicitly,
+   qacc_e = (M + dt diag(dof_damping))^-1 (qfrc_smooth + qfrc_constraint), by the same tree L'DL as
+   mj_factorM / mj_solveM, and qvel advances with qacc_e. d->qacc (sensors, the warmstart saved by
+   mj_advance) stays the solver's. Without it qvel advances with qacc (explicit damping, inside
+   qfrc_smooth's passive force). */
+static void integrate(const ZbModel* m, ZbData* d, real dt, int eulerdamp) {
   int nv = m->nv;
-  for (int j = 0; j < nv; j++) d->qvel[j] += dt * d->qacc[j];
+  real qacc_e[NDOF];
+  if (eulerdamp) {
+    real H[NDOF][NDOF], Hinv[NDOF];
+    memcpy(H, d->qM, sizeof(H));
+    for (int j = 0; j < nv; j++) {
+      H[j][j] += dt * d->dof_damping[j];
+      qacc_e[j] = d->qfrc_smooth[j] + d->qfrc_constraint[j];
+    }
+    factor_m(m, H, Hinv);
+    solve_m(m, H, Hinv, qacc_e);
+  } else {
+    for (int j = 0; j < nv; j++) qacc_e[j] = d->qacc[j];
+  }
+  for (int j = 0; j < nv; j++) d->qvel[j] += dt * qacc_e[j];
   for (int i = 1; i < m->nbody; i++) {
     int qa = m->body_qposadr[i], da = m->body_dofadr[i];
     if (m->body_jnttype[i] == ZB_JNT_FREE) {
@@ -1413,7 +1435,7 @@ static void physics_substep(const ZbModel* m, ZbData* d, const ZbEnvConfig* cfg,
   if (with_sensors) sensors(m, d);
   if (do_integrate) { /* mj_advance saves qacc for warmstart, then integrates */
     for (int j = 0; j < m->nv; j++) d->qacc_warm[j] = d->qacc[j];
-    integrate(m, d, dt);
+    integrate(m, d, dt, (cfg->flags & ZB_F_EULERDAMP) != 0);
   }
 }
 

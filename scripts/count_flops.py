@@ -56,14 +56,16 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--out", default="")
     ap.add_argument("--solver", default="newton", choices=["newton", "cg"])
+    ap.add_argument("--eulerdamp", action="store_true", help="mj_Euler's implicit joint damping (ZB_F_EULERDAMP)")
     args = ap.parse_args()
     cm = compile_model()
     res = {"workload": f"C2 standing task, {args.envs} envs x {args.steps} env-steps after 20 warm-up steps, "
-                       f"JOINT_BIASES + 0.05 N(0,1) actions (zbo_synthetic_actions), {args.solver} 8 / 8",
+                       f"JOINT_BIASES + 0.05 N(0,1) actions (zbo_synthetic_actions), {args.solver} 8 / 8"
+                       + (", implicit joint damping (eulerdamp)" if args.eulerdamp else ""),
            "note": "FMA counted as a multiply and an add; compares listed apart and not in the FLOPs",
-           "solver": args.solver}
-    res["as_run"] = count(cm, default_config(solver=args.solver), args.envs, args.steps)
-    fixed = default_config(solver=args.solver)
+           "solver": args.solver, "eulerdamp": args.eulerdamp}
+    res["as_run"] = count(cm, default_config(solver=args.solver, eulerdamp=args.eulerdamp), args.envs, args.steps)
+    fixed = default_config(solver=args.solver, eulerdamp=args.eulerdamp)
     fixed.tolerance = -1.0
     fixed.ls_tolerance = -1.0
     res["fixed_iterations"] = count(cm, fixed, args.envs, args.steps)

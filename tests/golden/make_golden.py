@@ -31,15 +31,19 @@ CASES = {
     # round 4: CG at C1's ensemble size, with pushes (the GPU test compares its first 8 rewards and
     # the 64-step ensemble statistics)
     "c2_cg_64x64_seed4": dict(n=64, steps=64, seed=4, push=True, randomize=False, std=0.1, solver="cg"),
+    # round 5: mj_Euler's implicit joint damping (ZB_F_EULERDAMP), with each solver
+    "c2_eulerdamp_seed5": dict(n=16, steps=16, seed=5, push=False, randomize=False, std=0.05, eulerdamp=True),
+    "c5_cg_eulerdamp_seed6": dict(n=16, steps=16, seed=6, push=True, randomize=True, std=0.1, solver="cg",
+                                  eulerdamp=True),
 }
 
 
 EXACT_STEPS = 16  # tests/test_gpu_parity.py GOLDEN_EXACT_STEPS: the per-env state is also kept at this step
 
 
-def run_case(name, n, steps, seed, push, randomize, std, solver="newton"):
+def run_case(name, n, steps, seed, push, randomize, std, solver="newton", eulerdamp=False):
     cm = compile_model()
-    cfg = default_config(push=push, randomize=randomize, solver=solver)
+    cfg = default_config(push=push, randomize=randomize, solver=solver, eulerdamp=eulerdamp)
     env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
     oa0, oc0, _ = env.reset()
     rewards, dones, actions = [], [], []

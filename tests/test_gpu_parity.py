@@ -252,12 +252,48 @@ def print_budget_envs(err, t, eng, env, ref64, gs):
 @pytest.mark.parametrize("solver", ["newton", "cg"])
 @pytest.mark.parametrize("push,randomize", [(False, False), (True, False), (False, True), (True, True)])
 def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize, solver):
+    _one_step_parity(torch_gpu, cmodel, oracle_mod, default_config(push=push, randomize=randomize, solver=solver),
+                     f"one-step {solver} push={push} randomize={randomize}", solver)
+
+
+@pytest.mark.parametrize("solver", ["newton", "cg"])
+@pytest.mark.parametrize("push,randomize", [(False, False), (True, True)])
+def test_one_step_parity_eulerdamp(torch_gpu, cmodel, oracle_mod, push, randomize, solver):
+    """ZB_F_EULERDAMP (mj_Euler's implicit joint damping, the step kernel's ED instantiation) under
+    the same one-step contract as the explicit form; the two forms part by more than the bounds."""
+    cfg = default_config(push=push, randomize=randomize, solver=solver, eulerdamp=True)
+    _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, f"one-step eulerdamp {solver} push={push} "
+                     f"randomize={randomize}", solver)
+
+
+def test_eulerdamp_changes_the_step(torch_gpu, cmodel, oracle_mod):
+    """The flag reaches the kernel: from the same state the implicit and explicit steps differ in
+    qvel by far more than the one-step bound, and the oracle agrees on the difference."""
     torch = torch_gpu
-    cfg = default_config(push=push, randomize=randomize, solver=solver)
+    n = 64
+    on, off = default_config(eulerdamp=True), default_config()
+    env = warm_states(oracle_mod, cmodel, off, n, steps=12)
+    qv = {}
+    for name, cfg in (("on", on), ("off", off)):
+        eng = engine(cmodel, cfg, n, seed=7)
+        eng.set_state(torch.from_numpy(env.state.copy()))
+        eng.step(torch.from_numpy(oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100)).cuda())
+        qv[name] = eng.get_state().cpu().numpy()[:, 32:58]
+        o = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=7)
+        o.state[:] = env.state
+        o.step(oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100))
+        qv[name + "_ref"] = o.state[:, 32:58].copy()
+    d_gpu, d_ref = qv["on"] - qv["off"], qv["on_ref"] - qv["off_ref"]
+    print(f"\n[eulerdamp] max |qvel(on) - qvel(off)| engine {np.abs(d_gpu).max():.3e} oracle {np.abs(d_ref).max():.3e}")
+    assert np.abs(d_gpu).max() > 50 * ONE_STEP_TOL["qvel"][0]
+    np.testing.assert_allclose(d_gpu, d_ref, atol=2 * ONE_STEP_TOL["qvel"][0] + 0.05 * np.abs(d_ref).max())
+
+
+def _one_step_parity(torch, cmodel, oracle_mod, cfg, name, solver):
     n = 64
     env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
     eng = engine(cmodel, cfg, n, seed=7)
-    err = MaxErr(f"one-step {solver} push={push} randomize={randomize}")
+    err = MaxErr(name)
     for t in range(3):
         eng.set_state(torch.from_numpy(env.state.copy()))
         eng.set_rand(torch.from_numpy(env.rand.copy()))
@@ -374,7 +410,8 @@ def golden_ensemble_check(name, rew, done, final_state, g, k=5.0):
     assert abs(z.mean() - z_ref.mean()) <= k * se_z
 
 
-@pytest.mark.parametrize("name", ["c1_64x128_seed0", "c5_push_seed1", "c2_cg_seed2", "c2_cg_64x64_seed4"])
+@pytest.mark.parametrize("name", ["c1_64x128_seed0", "c5_push_seed1", "c2_cg_seed2", "c2_cg_64x64_seed4",
+                                  "c2_eulerdamp_seed5", "c5_cg_eulerdamp_seed6"])
 def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
     """The engine from reset against a committed oracle rollout. The first 8 rewards follow the
     one-step contract (MaxErr): the fp32 oracle is replayed along the fixture (it reproduces it),
@@ -388,7 +425,8 @@ def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
     g = dict(np.load(os.path.join(GOLDEN, f"{name}.npz")))
     n, steps, seed = int(g["cfg_n"]), int(g["cfg_steps"]), int(g["cfg_seed"])
     solver = str(g["cfg_solver"]) if "cfg_solver" in g else "newton"
-    cfg = default_config(push=bool(g["cfg_push"]), randomize=bool(g["cfg_randomize"]), solver=solver)
+    cfg = default_config(push=bool(g["cfg_push"]), randomize=bool(g["cfg_randomize"]), solver=solver,
+                         eulerdamp=bool(g["cfg_eulerdamp"]) if "cfg_eulerdamp" in g else False)
     eng = engine(cmodel, cfg, n, seed=seed)
     out = eng.reset()
     torch.cuda.synchronize()

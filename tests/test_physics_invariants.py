@@ -162,3 +162,47 @@ def test_f32_oracle_tracks_f64(oracle_mod, cmodel):
         b.step(act)
     np.testing.assert_allclose(a.state[:, :27], b.state[:, :27], atol=2e-5)
     np.testing.assert_allclose(a.state[:, 32:58], b.state[:, 32:58], atol=5e-3)
+
+
+def test_eulerdamp_is_mj_euler_implicit_damping(oracle_mod, cmodel):
+    """ZB_F_EULERDAMP (mj_Euler with mjDSBL_EULERDAMP clear): one substep advances qvel by
+    dt (M + dt diag(B))^-1 (qfrc_smooth + qfrc_constraint). In the air only the frictionloss rows
+    act; with the fp64 Newton solve converged, qfrc_smooth + qfrc_constraint = M qacc, so the step is
+    checked against an independent numpy solve of (M + dt B) x = M qacc."""
+    rng = np.random.default_rng(11)
+    q = _random_qpos(cmodel, rng)
+    q[2] = 2.0
+    qv = np.concatenate([rng.normal(0, 0.3, 6), rng.normal(0, 2.0, 20)]).astype(np.float32)
+    ctrl = rng.normal(0, 0.5, 20).astype(np.float32)
+    dt = 0.001
+    on, off = default_config(eulerdamp=True), default_config()
+    assert on.flags & cs.F_EULERDAMP and not off.flags & cs.F_EULERDAMP
+    p = oracle_mod.constraint_problem(cmodel.cmodel, on, q, qv, ctrl=ctrl, precision="f64")
+    M, qacc = p["qM"].astype(np.float64), p["qacc"].astype(np.float64)
+    B = np.array([cmodel.cmodel.dof_damping[i] for i in range(26)])
+    assert (B[6:] > 0).all()
+    expect = qv + dt * np.linalg.solve(M + dt * np.diag(B), M @ qacc)
+    _, v_on, w_on = oracle_mod.simulate(cmodel.cmodel, on, q, qv, 1, ctrl=ctrl, precision="f64")
+    _, v_off, w_off = oracle_mod.simulate(cmodel.cmodel, off, q, qv, 1, ctrl=ctrl, precision="f64")
+    np.testing.assert_allclose(v_on, expect, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(v_off, qv + dt * qacc, rtol=0, atol=2e-6)
+    # the implicit form differs from the explicit one by about dt^2 B M^-1 (B qacc): visible on the hinges
+    assert np.abs(v_on - v_off)[6:].max() > 20 * 2e-6
+    # qacc_warmstart is the solver's qacc either way (mj_advance)
+    np.testing.assert_array_equal(w_on, w_off)
+
+
+def test_eulerdamp_stable_past_the_explicit_limit(oracle_mod, cmodel):
+    """With the joint damping raised until dt B / M_jj > 2 on the hinges, explicit Euler diverges and
+    the implicit form stays bounded (the reason MuJoCo integrates damping implicitly by default)."""
+    m = _model_copy(cmodel.cmodel)
+    for i in range(6, 26):
+        m.dof_damping[i] = 3000.0 * m.dof_damping[i] / max(m.dof_damping[i], 1e-9)
+    q = cmodel.reset_qpos().astype(np.float32)
+    q[2] = 2.0
+    qv = np.zeros(26, np.float32)
+    qv[6:] = 1.0
+    _, v_on, _ = oracle_mod.simulate(m, default_config(eulerdamp=True), q, qv, 50, precision="f64")
+    _, v_off, _ = oracle_mod.simulate(m, default_config(), q, qv, 50, precision="f64")
+    assert np.isfinite(v_on).all() and np.abs(v_on[6:]).max() < 1.0
+    assert not (np.isfinite(v_off).all() and np.abs(v_off[6:]).max() < 1e3)
