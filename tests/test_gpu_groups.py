@@ -207,6 +207,8 @@ def test_airtime_patch_orders_after_caller_writes(torch_gpu, cmodel):
     out = {}
     for name, eng in (("one", HipEngine(cmodel, cfg, n, seed=11)), ("grp", EnvGroups(cmodel, cfg, n, groups=3, seed=11))):
         eng.reset()
+        for t in range(10):  # the feet are down at the rollout's first step (its contact bits are set)
+            eng.step(acts[t])
         eng.mark_rollout_start()
         rows = []
         for t in range(T):
