@@ -16,7 +16,9 @@
  *   - nbody <= ZB_MAX_BODY, nv <= ZB_MAX_DOF, dof-chain depth <= ZB_MAX_DEPTH;
  *   - collision = floor plane (world geom) vs up to ZB_MAX_GEOM per-body boxes,
  *     capsules, cylinders, spheres or ellipsoids (the two foot soles first by
- *     convention); no robot-robot contacts (nskip_pair = 0);
+ *     convention); of the robot's own pairs only the two box soles against each
+ *     other (npair <= 1, box-box, with no other floor collider); any other
+ *     self pair is counted in nskip_pair and refused;
  *   - actuators = motors on hinge joints (joint transmission, gear).
  * All floats are fp32; all vectors are padded to 4 so rows are 16-B aligned.
  */
@@ -30,7 +32,7 @@ extern "C" {
 #endif
 
 #define ZB_MODEL_MAGIC   0x5A424F54u /* 'ZBOT' */
-#define ZB_MODEL_VERSION 6
+#define ZB_MODEL_VERSION 7
 
 #define ZB_MAX_BODY  32
 #define ZB_MAX_DOF   32
@@ -40,6 +42,7 @@ extern "C" {
 #define ZB_MAX_SITE  8
 #define ZB_MAX_ACT   32
 #define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-cylinder 4, plane-capsule 2, plane-sphere / -ellipsoid 1 */
+#define ZB_CON_PER_PAIR 4 /* box-box (the sole pair): at most 4 contacts */
 #define ZB_MAX_CON  (ZB_MAX_GEOM * ZB_CON_PER_GEOM)
 
 /* joint types (mjtJoint values where they exist) */
@@ -138,6 +141,18 @@ typedef struct ZbModel {
   float    floor_solimp[8];
   float    floor_margin;
   float    pad_floor[3];
+
+  /* the robot's own colliding pair the engine simulates (npair 0 or 1): the two box soles against
+     each other (box-box). The contact normal points from geom pair_geom[0] to pair_geom[1] (MuJoCo's
+     geom1 -> geom2). Parameters as MuJoCo mixes them for two geoms of equal priority
+     (mj_contactParam): friction the larger of the two per component, solref / solimp the mean
+     (solmix 1 each), margin the larger. */
+  int32_t  npair;
+  int32_t  pair_geom[2];
+  float    pair_margin;
+  float    pair_friction[4];
+  float    pair_solref[4];
+  float    pair_solimp[8];
 
   /* sites */
   int32_t  site_body[ZB_MAX_SITE];

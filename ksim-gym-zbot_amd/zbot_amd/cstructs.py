@@ -14,9 +14,10 @@ MAX_GEOM = 4
 MAX_SITE = 8
 MAX_ACT = 32
 CON_PER_GEOM = 4
+CON_PER_PAIR = 4  # box-box: the sole pair
 
 MODEL_MAGIC = 0x5A424F54
-MODEL_VERSION = 6
+MODEL_VERSION = 7
 
 JNT_NONE = -1
 JNT_FREE = 0
@@ -186,6 +187,12 @@ class ZbModel(C.Structure):
         ("floor_solimp", _f(8)),
         ("floor_margin", C.c_float),
         ("pad_floor", _f(3)),
+        ("npair", C.c_int32),
+        ("pair_geom", _i(2)),
+        ("pair_margin", C.c_float),
+        ("pair_friction", _f(4)),
+        ("pair_solref", _f(4)),
+        ("pair_solimp", _f(8)),
         ("site_body", _i(MAX_SITE)),
         ("site_pos", _f(MAX_SITE, 4)),
         ("site_quat", _f(MAX_SITE, 4)),

@@ -256,14 +256,50 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize, solver)
                      f"one-step {solver} push={push} randomize={randomize}", solver)
 
 
+# mj_Euler's implicit damping advances qvel with (M + dt B)^-1 (qfrc_smooth + qfrc_constraint): the
+# constraint force at the solver's LAST iterate, not its qacc. Where the solve is unconverged the force
+# residual (the gradient) enters the velocity, scaled by the contact stiffness, so rounding differences
+# along the solver path weigh more than in the explicit form (MuJoCo has the same sensitivity).
+# Newton: the explicit contract, except the solver exit-iteration env (engine and fp32 oracle leave the
+# loop a few iterations apart), which may be 50x off (measured r05: 33x, env 23: 66 vs 63 iterations);
+# with the early exit off the whole contract holds with no exception
+# (test_one_step_parity_eulerdamp_without_early_exit). CG (8 unconverged iterations): about 5x the
+# maximum error measured on MI355X (r05: qpos 1.7e-4, qvel 3.2e-3, planner 4.0e-3, obs_critic 1.1e-2,
+# obs_extra 0.76, reward 9.6e-4, terms 3.9e-4), up to 12 of 64 envs at a discontinuity (measured 8).
+ONE_STEP_TOL_CG_ED = {
+    "qpos": (1e-3, 0.0),
+    "qvel": (1.5e-2, 0.0),
+    "planner": (2e-2, 0.0),
+    "obs_actor": (1.5e-2, 0.0),
+    "obs_critic": (5e-2, 0.0),
+    "obs_extra": (4.0, 0.0),
+    "reward": (4e-3, 0.0),
+    "reward_terms": (2e-3, 0.0),
+}
+
+
 @pytest.mark.parametrize("solver", ["newton", "cg"])
 @pytest.mark.parametrize("push,randomize", [(False, False), (True, True)])
 def test_one_step_parity_eulerdamp(torch_gpu, cmodel, oracle_mod, push, randomize, solver):
-    """ZB_F_EULERDAMP (mj_Euler's implicit joint damping, the step kernel's ED instantiation) under
-    the same one-step contract as the explicit form; the two forms part by more than the bounds."""
+    """ZB_F_EULERDAMP (mj_Euler's implicit joint damping, the step kernel's ED instantiation): Newton
+    under the explicit form's contract with a wider exit-iteration budget, CG under ONE_STEP_TOL_CG_ED."""
     cfg = default_config(push=push, randomize=randomize, solver=solver, eulerdamp=True)
-    _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, f"one-step eulerdamp {solver} push={push} "
-                     f"randomize={randomize}", solver)
+    name = f"one-step eulerdamp {solver} push={push} randomize={randomize}"
+    if solver == "cg":
+        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, name, solver, tol=ONE_STEP_TOL_CG_ED,
+                         err_kw=dict(max_ill=12))
+    else:
+        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, name, solver, err_kw=dict(loose=50.0))
+
+
+def test_one_step_parity_eulerdamp_without_early_exit(torch_gpu, cmodel, oracle_mod):
+    """The cause of the implicit form's Newton budget, shown as for the explicit form: with the
+    solver tolerance at 0 the same states hold the explicit contract with no exception (budget 0)."""
+    for push, randomize in ((False, False), (True, True)):
+        cfg = default_config(push=push, randomize=randomize, eulerdamp=True)
+        cfg.tolerance = 0.0
+        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, f"one-step eulerdamp newton tolerance 0 push={push} "
+                         f"randomize={randomize}", "newton", err_kw=dict(budget=0, loose=1.0))
 
 
 def test_eulerdamp_changes_the_step(torch_gpu, cmodel, oracle_mod):
@@ -289,11 +325,11 @@ def test_eulerdamp_changes_the_step(torch_gpu, cmodel, oracle_mod):
     np.testing.assert_allclose(d_gpu, d_ref, atol=2 * ONE_STEP_TOL["qvel"][0] + 0.05 * np.abs(d_ref).max())
 
 
-def _one_step_parity(torch, cmodel, oracle_mod, cfg, name, solver):
+def _one_step_parity(torch, cmodel, oracle_mod, cfg, name, solver, tol=None, err_kw=None):
     n = 64
     env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
     eng = engine(cmodel, cfg, n, seed=7)
-    err = MaxErr(name)
+    err = MaxErr(name, **(err_kw or {}))
     for t in range(3):
         eng.set_state(torch.from_numpy(env.state.copy()))
         eng.set_rand(torch.from_numpy(env.rand.copy()))
@@ -303,9 +339,9 @@ def _one_step_parity(torch, cmodel, oracle_mod, cfg, name, solver):
         torch.cuda.synchronize()
         gs = eng.get_state().cpu().numpy()
         np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
-        tol = ONE_STEP_TOL_CG if solver == "cg" else ONE_STEP_TOL
+        tl = tol or (ONE_STEP_TOL_CG if solver == "cg" else ONE_STEP_TOL)
         for key, got, want in one_step_outputs(gs, out, env.state, ref):
-            err.add(key, got, want, *tol[key], ref64=ref64[key])
+            err.add(key, got, want, *tl[key], ref64=ref64[key])
         print_budget_envs(err, t, eng, env, ref64, gs)
         # integer bookkeeping is exact
         for w in (cs.S_EP_STEPS, cs.S_RNG_STEP, cs.S_EPISODE):
