@@ -29,6 +29,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "zb_internal.h"
 
 namespace zb {
@@ -1544,14 +1546,22 @@ __device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, floa
   aref = -bb * vel - kk * imp * pos;
 }
 
-/* The collider of team lane l in contact-row bank `bank`: geom 2 bank + l / 16 (XG), or sole l / 16
-   of the two-sole kernels. gb: its body; false when the model has no such geom. */
+/* The second contact-row bank's role by kernel instantiation (zb_host.cpp needs_xg): XG 1 / 2 the
+   general floor colliders (geoms 2-3; XG 2 with cylinders / ellipsoids), XG 3 the sole pair (the two
+   box soles against each other, pair_rows). XG 0: the two soles alone. */
+template <int XG>
+constexpr bool XFLOOR = XG == 1 || XG == 2;
+template <int XG>
+constexpr bool XPAIR = XG == 3;
+
+/* The collider of team lane l in contact-row bank `bank`: geom 2 bank + l / 16 (general colliders), or
+   sole l / 16 (the two-sole and sole-pair kernels). gb: its body; false when the model has no such geom. */
 template <int XG>
 __device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& gb) {
   MP m = c.m;
   const int gl = c.l >> 4;
-  g = XG ? 2 * bank + gl : gl;
-  const bool gvalid = XG ? g < m->ngeom : gl < NGEOM;
+  g = XFLOOR<XG> ? 2 * bank + gl : gl;
+  const bool gvalid = XFLOOR<XG> ? g < m->ngeom : gl < NGEOM;
   if (!gvalid) g = 0;
   gb = gvalid ? m->geom_body[g] : 0;
   return gvalid;
@@ -1586,10 +1596,10 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
   for (int k = 0; k < 4; k++) xqs[k] = tsh(B.xq[k], gb);
 #pragma unroll
   for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
-  const int ty = XG ? m->geom_type[g] : ZB_GEOM_BOX;
+  const int ty = XFLOOR<XG> ? m->geom_type[g] : ZB_GEOM_BOX;
   /* XG 2: the instantiation for models with cylinders or ellipsoids (zb_host.cpp needs_xg), so that
      the others carry no code for them */
-  const bool box = !XG || ty == ZB_GEOM_BOX, cap = XG && ty == ZB_GEOM_CAPSULE,
+  const bool box = !XFLOOR<XG> || ty == ZB_GEOM_BOX, cap = XFLOOR<XG> && ty == ZB_GEOM_CAPSULE,
              cyl = XG == 2 && ty == ZB_GEOM_CYLINDER, ell = XG == 2 && ty == ZB_GEOM_ELLIPSOID;
   /* the lane's point relative to the geom centre, geom frame -> body frame -> world */
   float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
@@ -1727,7 +1737,7 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   r.Jv = 0.f;
   r.D = 0.f;
   r.aref = 0.f;
-  if (XG && bank == 1) {
+  if (XFLOOR<XG> && bank == 1) {
     /* the second bank (shins, hands: usually off the floor) first by a bound: no point of a geom
        lies lower than its body's origin minus |geom_pos| minus the geom's bounding radius (box: the
        half-diagonal; capsule: radius + half-length; cylinder: the rim's distance from the centre,
@@ -1787,6 +1797,345 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   if (bank == 0 || bal != 0ull) st_row(Jrow, Jc);
 }
 
+/* the world frame of geom g (body frame then geom frame): centre cw, rotation R (row-major) */
+__device__ __forceinline__ void geom_world(const Ctx& c, const BodyK& B, int g, float cw[3], float R[9]) {
+  MP m = c.m;
+  const int gb = m->geom_body[g];
+  float xq[4], xp[3];
+#pragma unroll
+  for (int k = 0; k < 4; k++) xq[k] = tsh(B.xq[k], gb);
+#pragma unroll
+  for (int k = 0; k < 3; k++) xp[k] = tsh(B.xp[k], gb);
+  const float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
+  const float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
+  float q[4], t[3];
+  quat_mul(q, xq, gq);
+  quat2mat(R, q);
+  quat_rotate(t, xq, gp);
+#pragma unroll
+  for (int k = 0; k < 3; k++) cw[k] = xp[k] + t[k];
+}
+
+/* The sole pair's box-box contacts (ZbModel.npair; the oracle's box_box / pair_collision, whose
+   comment states the method): every lane runs the separating-axis test on team-uniform values; for a
+   face contact lane i < 24 holds candidate i of the clip in the oracle's order ((a) incident vertices
+   0-3, (b) edge crossings 4 + 4 edge + side, (c) rectangle corners 20-23), duplicates and the four-point
+   selection are team ballots and reductions. Lane l's contact is q = (l & 15) >> 2: its point, distance
+   (1e30 past the count) and the contact frame (n from geom1 to geom2, t1, t2 = n x t1: mju_makeFrame). */
+__device__ __forceinline__ float pair_contact(const Ctx& c, const BodyK& B, float pos[3], float n[3], float t1[3],
+                                              float t2[3]) {
+  MP m = c.m;
+  const int q = (c.l & 15) >> 2;
+  float c1[3], c2[3], R1[9], R2[9];
+  geom_world(c, B, m->pair_geom[0], c1, R1);
+  geom_world(c, B, m->pair_geom[1], c2, R2);
+  const float a[3] = {m->geom_size[m->pair_geom[0]][0], m->geom_size[m->pair_geom[0]][1], m->geom_size[m->pair_geom[0]][2]};
+  const float b[3] = {m->geom_size[m->pair_geom[1]][0], m->geom_size[m->pair_geom[1]][1], m->geom_size[m->pair_geom[1]][2]};
+  const float margin = m->pair_margin;
+  const float dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  n[0] = 0.f; n[1] = 0.f; n[2] = 1.f;
+  t1[0] = 0.f; t1[1] = 1.f; t1[2] = 0.f;
+  t2[0] = -1.f; t2[1] = 0.f; t2[2] = 0.f;
+  pos[0] = pos[1] = pos[2] = 0.f;
+  /* the bounding spheres first (the soles are usually far apart): wave-uniform skip */
+  const float ra = sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]), rb = sqrtf(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+  const bool near = sqrtf(dot3(dv, dv)) <= ra + rb + margin;
+  if (__ballot(near) == 0ull) return 1e30f;
+  /* the boxes' axes in the world: columns of the rotations */
+  float A[3][3], Bx[3][3];
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      A[k][r] = R1[3 * r + k];
+      Bx[k][r] = R2[3 * r + k];
+    }
+  float best = -1e30f, L[3] = {0.f, 0.f, 1.f};
+  int code = -1;
+  bool sep_found = false;
+#pragma unroll
+  for (int ax = 0; ax < 15; ax++) {
+    float l[3];
+    bool ok = true;
+    if (ax < 3) {
+      l[0] = A[ax][0]; l[1] = A[ax][1]; l[2] = A[ax][2];
+    } else if (ax < 6) {
+      l[0] = Bx[ax - 3][0]; l[1] = Bx[ax - 3][1]; l[2] = Bx[ax - 3][2];
+    } else {
+      const int i = (ax - 6) / 3, j = (ax - 6) % 3;
+      cross3(l, A[i], Bx[j]);
+      const float ln = sqrtf(dot3(l, l));
+      ok = ln >= 1e-6f;
+      const float inv = ok ? 1.f / ln : 0.f;
+      l[0] *= inv; l[1] *= inv; l[2] *= inv;
+    }
+    float rsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) rsum += a[k] * fabsf(dot3(A[k], l)) + b[k] * fabsf(dot3(Bx[k], l));
+    const float dl = dot3(dv, l);
+    const float sep = fabsf(dl) - rsum;
+    if (ok && sep > margin) sep_found = true;
+    const bool better = ok && (ax < 6 ? sep > best : sep > best + 0.05f * fabsf(best));
+    if (better) {
+      best = sep;
+      code = ax;
+      const float sg = dl < 0.f ? -1.f : 1.f;
+      L[0] = sg * l[0]; L[1] = sg * l[1]; L[2] = sg * l[2];
+    }
+  }
+  const bool contact = near && !sep_found;
+  n[0] = L[0]; n[1] = L[1]; n[2] = L[2];
+  {
+    /* mju_makeFrame(n) */
+    float y[3] = {0.f, 1.f, 0.f};
+    if (!(fabsf(n[1]) < 0.5f)) { y[1] = 0.f; y[2] = 1.f; }
+    const float d = dot3(n, y);
+#pragma unroll
+    for (int k = 0; k < 3; k++) t1[k] = y[k] - d * n[k];
+    const float inv = 1.f / sqrtf(dot3(t1, t1));
+#pragma unroll
+    for (int k = 0; k < 3; k++) t1[k] *= inv;
+    cross3(t2, n, t1);
+  }
+  float dist = 1e30f;
+  if (code >= 6) {
+    /* edge-edge: one contact */
+    const int i = (code - 6) / 3, j = (code - 6) % 3;
+    float p1[3] = {c1[0], c1[1], c1[2]}, p2[3] = {c2[0], c2[1], c2[2]};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float s1 = dot3(A[k], L) > 0.f ? a[k] : -a[k], s2 = dot3(Bx[k], L) > 0.f ? -b[k] : b[k];
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        p1[r] += k != i ? s1 * A[k][r] : 0.f;
+        p2[r] += k != j ? s2 * Bx[k][r] : 0.f;
+      }
+    }
+    const float w[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    const float ab = dot3(A[i], Bx[j]), d1 = dot3(A[i], w), d2 = dot3(Bx[j], w);
+    const float den = 1.f - ab * ab;
+    float t = den > 1e-12f ? (ab * d2 - d1) / den : 0.f;
+    t = fminf(fmaxf(t, -a[i]), a[i]);
+    float u = d2 + t * ab;
+    u = fminf(fmaxf(u, -b[j]), b[j]);
+#pragma unroll
+    for (int r = 0; r < 3; r++) pos[r] = 0.5f * (p1[r] + t * A[i][r] + p2[r] + u * Bx[j][r]);
+    dist = (contact && q == 0) ? best : 1e30f;
+    return dist;
+  }
+  /* face contact: reference box R (the axis's box), incident box I */
+  const bool ref2 = code >= 3;
+  const int k = ref2 ? code - 3 : (code < 0 ? 0 : code);
+  const int ku = (k + 1) % 3, kv = (k + 2) % 3;
+  float nr[3], o[3], u3[3], v3[3], I[3][3], is[3], cI[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    nr[r] = ref2 ? -L[r] : L[r];
+    o[r] = (ref2 ? c2[r] : c1[r]) + (ref2 ? b[k] : a[k]) * nr[r];
+    u3[r] = ref2 ? Bx[ku][r] : A[ku][r];
+    v3[r] = ref2 ? Bx[kv][r] : A[kv][r];
+    cI[r] = ref2 ? c1[r] : c2[r];
+  }
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    is[e] = ref2 ? a[e] : b[e];
+#pragma unroll
+    for (int r = 0; r < 3; r++) I[e][r] = ref2 ? A[e][r] : Bx[e][r];
+  }
+  const float hu = ref2 ? b[ku] : a[ku], hv = ref2 ? b[kv] : a[kv];
+  int jj = 0;
+  {
+    float bd = -1.f;
+#pragma unroll
+    for (int e = 0; e < 3; e++) {
+      const float v = fabsf(dot3(I[e], nr));
+      if (v > bd) { bd = v; jj = e; }
+    }
+  }
+  float Ij[3], Ia[3], Ib[3];
+  const int ja = (jj + 1) % 3, jb = (jj + 2) % 3;
+#pragma unroll
+  for (int r = 0; r < 3; r++) { Ij[r] = I[jj][r]; Ia[r] = I[ja][r]; Ib[r] = I[jb][r]; }
+  const float sIj = is[jj], sIa = is[ja], sIb = is[jb];
+  const float sgi = dot3(Ij, nr) > 0.f ? -1.f : 1.f;
+  float px[4], py[4], pz[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const float va = (e == 0 || e == 3) ? 1.f : -1.f, vb = e < 2 ? 1.f : -1.f;
+    float V[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) V[r] = cI[r] + sgi * sIj * Ij[r] + va * sIa * Ia[r] + vb * sIb * Ib[r] - o[r];
+    px[e] = dot3(V, u3);
+    py[e] = dot3(V, v3);
+    pz[e] = dot3(V, nr);
+  }
+  /* this lane's candidate */
+  const int i = c.l;
+  float cx = 0.f, cy = 0.f, cz = 0.f;
+  bool valid = false;
+  if (i < 4) {
+    const float x0 = i == 0 ? px[0] : i == 1 ? px[1] : i == 2 ? px[2] : px[3];
+    const float y0 = i == 0 ? py[0] : i == 1 ? py[1] : i == 2 ? py[2] : py[3];
+    const float z0 = i == 0 ? pz[0] : i == 1 ? pz[1] : i == 2 ? pz[2] : pz[3];
+    valid = fabsf(x0) <= hu && fabsf(y0) <= hv;
+    cx = x0; cy = y0; cz = z0;
+  } else if (i < 20) {
+    const int e = (i - 4) >> 2, sd = (i - 4) & 3, e1 = (e + 1) & 3;
+    const float xa = e == 0 ? px[0] : e == 1 ? px[1] : e == 2 ? px[2] : px[3];
+    const float ya = e == 0 ? py[0] : e == 1 ? py[1] : e == 2 ? py[2] : py[3];
+    const float za = e == 0 ? pz[0] : e == 1 ? pz[1] : e == 2 ? pz[2] : pz[3];
+    const float xb = e1 == 0 ? px[0] : e1 == 1 ? px[1] : e1 == 2 ? px[2] : px[3];
+    const float yb = e1 == 0 ? py[0] : e1 == 1 ? py[1] : e1 == 2 ? py[2] : py[3];
+    const float zb = e1 == 0 ? pz[0] : e1 == 1 ? pz[1] : e1 == 2 ? pz[2] : pz[3];
+    const bool isx = sd < 2;
+    const float X = (sd & 1) ? (isx ? hu : hv) : (isx ? -hu : -hv);
+    const float e0 = isx ? xa : ya, ee1 = isx ? xb : yb;
+    if ((e0 - X) * (ee1 - X) < 0.f) {
+      const float t = (X - e0) / (ee1 - e0);
+      const float oth = isx ? ya + t * (yb - ya) : xa + t * (xb - xa);
+      valid = fabsf(oth) <= (isx ? hv : hu);
+      cx = isx ? X : oth;
+      cy = isx ? oth : X;
+      cz = za + t * (zb - za);
+    }
+  } else if (i < 24) {
+    const int e = i - 20;
+    const float X = (e == 1 || e == 2) ? hu : -hu, Y = e >= 2 ? hv : -hv;
+    int pos_ = 0, neg_ = 0;
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      const int f1 = (f + 1) & 3;
+      const float cr = (px[f1] - px[f]) * (Y - py[f]) - (py[f1] - py[f]) * (X - px[f]);
+      pos_ += cr >= 0.f;
+      neg_ += cr <= 0.f;
+    }
+    valid = pos_ == 4 || neg_ == 4;
+    float ni[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) ni[r] = sgi * Ij[r];
+    const float nx = dot3(ni, u3), ny = dot3(ni, v3), nz = dot3(ni, nr);
+    cx = X;
+    cy = Y;
+    cz = pz[0] - (nx * (X - px[0]) + ny * (Y - py[0])) / nz;
+  }
+  const bool inm = contact && valid && cz <= margin;
+  /* duplicates: within 1e-6 in x and y of an earlier candidate within the margin */
+  bool dup = false;
+  for (int j = 0; j < 24; j++) {
+    const float xj = tsh(cx, j), yj = tsh(cy, j);
+    const int mj = tshi(inm ? 1 : 0, j);
+    dup = dup || (j < i && mj && fabsf(cx - xj) <= 1e-6f && fabsf(cy - yj) <= 1e-6f);
+  }
+  const bool keep = inm && !dup;
+  const uint32_t km = team_ballot(keep);
+  const int nk = __popc(km);
+  int sel[4] = {0, 0, 0, 0}, ns;
+  if (nk <= 4) {
+    uint32_t mm = km;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      sel[t] = mm ? __ffs(mm) - 1 : 0;
+      mm &= mm - 1u;
+    }
+    ns = nk;
+  } else {
+    /* MJX's manifold points from the deepest: first lane at each extreme (team-uniform indices) */
+    auto first_of = [&](float v, bool on) {
+      const float mx = tmaxf(on ? v : -1e30f);
+      return __ffs(team_ballot(on && v == mx)) - 1;
+    };
+    const int ia = first_of(-cz, keep);
+    const float xa = tsh(cx, ia), ya = tsh(cy, ia);
+    const int ib = first_of((cx - xa) * (cx - xa) + (cy - ya) * (cy - ya), keep);
+    const float xb = tsh(cx, ib), yb = tsh(cy, ib);
+    const int ic = first_of(fabsf((xb - xa) * (cy - ya) - (yb - ya) * (cx - xa)), keep);
+    const float xc = tsh(cx, ic), yc = tsh(cy, ic);
+    const float v1 = fabsf((xb - xc) * (yb - cy) - (yb - yc) * (xb - cx));
+    const float v2 = fabsf((xa - xc) * (ya - cy) - (ya - yc) * (xa - cx));
+    const float m1 = tmaxf(keep ? v1 : -1e30f), m2 = tmaxf(keep ? v2 : -1e30f);
+    const int id = m1 >= m2 ? __ffs(team_ballot(keep && v1 == m1)) - 1 : __ffs(team_ballot(keep && v2 == m2)) - 1;
+    const int cand[4] = {ia, ib, ic, id};
+    ns = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      bool d = false;
+#pragma unroll
+      for (int e = 0; e < t; e++) d = d || cand[e] == cand[t];
+      if (!d) {
+        sel[ns] = cand[t];
+        ns++;
+      }
+    }
+  }
+  const int mine = q == 0 ? sel[0] : q == 1 ? sel[1] : q == 2 ? sel[2] : sel[3];
+  const float x = tsh(cx, mine), y = tsh(cy, mine), z = tsh(cz, mine);
+#pragma unroll
+  for (int r = 0; r < 3; r++) pos[r] = o[r] + x * u3[r] + y * v3[r] + 0.5f * z * nr[r];
+  return (contact && q < ns) ? z : 1e30f;
+}
+
+/* The sole pair's contact rows (second bank of the XG 3 kernels): lane l = 16 h + 4 q + edge holds the
+   pyramid row (n +- mu t1, n +- mu t2) of contact q, half h: h = 0 the row's entries on geom2's limb
+   (+J of its body), h = 1 those on geom1's limb (-J of its body). The root dofs' columns of
+   J(body2) - J(body1) cancel exactly (mj_jacDifPair), so each half is a one-chain row of the limb dofs;
+   both halves carry the row's scalars (aref, D, jar, Jv, f), the cost counts them once (h = 0). */
+template <typename JP>
+__device__ __forceinline__ void pair_rows(const Ctx& c, const EnvS& s, const BodyK& B, const float cm[3], XRow& r,
+                                          JP Jrow) {
+  MP m = c.m;
+  CP cfg = c.cfg;
+  EnvL* L = c.L;
+  const int h = c.l >> 4, edge = c.l & 3;
+  const int g = m->pair_geom[1 - h];
+  const int gb = m->geom_body[g];
+  int kd = m->body_lastdof[gb];
+  if (kd < 0) kd = 0;
+  r.chd = tshi(c.chd, kd);
+  r.kdep = tshi(c.ddep, kd);
+  r.ex = false;
+  r.act = 0;
+  r.f = 0.f;
+  r.jar = 0.f;
+  r.Jv = 0.f;
+  r.D = 0.f;
+  r.aref = 0.f;
+  float pos[3], n[3], t1[3], t2[3];
+  const float dist = pair_contact(c, B, pos, n, t1, t2);
+  const float mu = m->pair_friction[0];
+  const float sg = (edge & 1) ? -mu : mu;
+  float dir[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) dir[k] = n[k] + sg * (edge < 2 ? t1[k] : t2[k]);
+  const float hs = h ? -1.f : 1.f;
+  float off[3] = {pos[0] - cm[0], pos[1] - cm[1], pos[2] - cm[2]}, sa[3];
+  cross3(sa, off, dir);
+  float Jc[CAP];
+  float vel = 0.f;
+#pragma unroll
+  for (int e = 0; e < CAP; e++) {
+    const int a = anc_lin(r.chd, e);
+    float v = sa[0] * L->cdof[a][0] + sa[1] * L->cdof[a][1] + sa[2] * L->cdof[a][2] + dir[0] * L->cdof[a][3] +
+              dir[1] * L->cdof[a][4] + dir[2] * L->cdof[a][5];
+    v = (e >= NROOT && e <= r.kdep) ? hs * v : 0.f;
+    Jc[e] = v;
+    vel += v * L->vec[V_QVEL][a];
+  }
+  vel += xor16f(vel); /* the row's velocity: both halves */
+  const bool ex = dist <= m->pair_margin;
+  if (ex) {
+    r.ex = true;
+    const int b1 = m->geom_body[m->pair_geom[0]], b2 = m->geom_body[m->pair_geom[1]];
+    const float dA = (m->body_invweight0[b1][0] + m->body_invweight0[b2][0]) * (1.f + mu * mu);
+    float Rr;
+    row_params(m->pair_solref, m->pair_solimp, dist, dA, vel, cfg->dt, r.D, Rr, r.aref);
+  }
+  const uint64_t bal = __ballot(r.ex);
+  const uint32_t tb = (uint32_t)(bal >> ((threadIdx.x & 63) & ~(TEAM - 1)));
+  r.nrow = __popc(tb);
+  r.exmask = tb;
+  if (bal != 0ull) st_row(Jrow, Jc);
+}
+
 /* collision + contact rows (lane r; XG: both banks) + dof rows (lane j) */
 template <int XG>
 __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
@@ -1796,7 +2145,8 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   const int l = c.l;
   contact_rows<XG>(c, s, B, cm, 0, r, &c.L->u.J[l][0]);
   if constexpr (XG) {
-    contact_rows<XG>(c, s, B, cm, 1, r.x, xrows(c.L) + l * CAP);
+    if constexpr (XPAIR<XG>) pair_rows(c, s, B, cm, r.x, xrows(c.L) + l * CAP);
+    else contact_rows<XG>(c, s, B, cm, 1, r.x, xrows(c.L) + l * CAP);
     /* the second bank's work is skipped, bit for bit, while no row of it exists in the wave (the
        usual case: shins and hands off the floor) */
     r.x.any = __ballot(r.x.ex) != 0ull;
@@ -1899,7 +2249,8 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
   }
   if constexpr (XG && XA) {
     const float k3 = eval_one(jx, r.x.D, f, a);
-    cost += r.x.ex ? k3 : 0.f;
+    /* the sole pair's row is held by two lanes (its halves): counted once */
+    cost += (r.x.ex && (!XPAIR<XG> || c.l < 16)) ? k3 : 0.f;
   }
   return cost;
 }
@@ -1978,7 +2329,7 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
     float f3;
     int a3;
     const float k3 = eval_one(r.x.jar, r.x.D, f3, a3);
-    cost += r.x.ex ? k3 : 0.f;
+    cost += (r.x.ex && (!XPAIR<XG> || c.l < 16)) ? k3 : 0.f; /* the pair's halves: once */
     r.x.f = r.x.ex ? f3 : r.x.f;
     r.x.act = r.x.ex ? a3 : r.x.act;
     const float cx = colsum16((const gfloat_t*)xrows(c.L) + c.l * CAP, r.x.ex ? r.x.f : 0.f);
@@ -2094,7 +2445,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     Hd = load_mrow(c, H);
     tb = 0u;
     jdj_mfma<false>();
-    if (XG && XA && r.x.any) {
+    if (XFLOOR<XG> && XA && r.x.any) {
       /* the second bank's D (rowDA is free once the first bank's J'DJ has read it) */
       tsync();
       L->rowDA[c.l] = (r.x.ex && r.x.act) ? r.x.D : 0.f;
@@ -2119,7 +2470,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
          so they need no mask */
       for (int e = 0; e < CAP; e++) H[e] += g0[e] + g1[e];
       Hd += d0 + d1;
-      if (XG && XA && r.x.any) {
+      if (XFLOOR<XG> && XA && r.x.any) {
         const float* GX = &L->Hs[0][0] + ddep * CAP;
         const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
         const float* G2 = f2 ? GX : &L->L[31][0];
@@ -2138,7 +2489,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     const float dl = r.ex ? ((r.act ? r.D : 0.f) - (pa ? r.D : 0.f)) : 0.f;
     L->rowF[c.l] = dl; /* rowF is free until the next update_constraint */
     tb = team_ballot(dl != 0.f) & c.rowmask;
-    if (XG && XA && r.x.any) {
+    if (XFLOOR<XG> && XA && r.x.any) {
       dl2 = r.x.ex ? ((r.x.act ? r.x.D : 0.f) - (pa2 ? r.x.D : 0.f)) : 0.f;
       ch2 = team_ballot(dl2 != 0.f); /* team-uniform: some row of the bank changed */
       tb2 = ch2 & c.rowmask2;        /* per dof lane: the changed rows on its chain */
@@ -2157,7 +2508,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     }
     Hd += dd;
   }
-  if (XG && ch2 != 0u) {
+  if (XFLOOR<XG> && ch2 != 0u) {
     /* the second bank's changed rows, their D through rowF after the first bank's: every lane of the
        team writes its row (team-uniform branch), a dof lane then adds the rows on its chain */
     tsync();
@@ -2165,7 +2516,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     tsync();
     if (c.l < NV) add_rows(tb2, (const gfloat_t*)xrows(L), L->rowF, ddep, H, Hd);
   }
-  if (XG && XA && full && r.x.any) tsync(); /* the second bank's G rows in Hs[] are read before H is stored there */
+  if (XFLOOR<XG> && XA && full && r.x.any) tsync(); /* the second bank's G rows in Hs[] are read before H is stored there */
   st_row(&L->Hs[c.l][0], H);
   L->Hsd[c.l] = Hd;
   tsync();
@@ -2183,7 +2534,11 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   /* leaves search in vec[V_TMP]; J rows are zero where no contact: no branch around the loads */
   float unused_;
   Mv = mul_m_dot(c, r, jr, search, V_TMP, r.Jv, -1, unused_);
-  if constexpr (XG && XA) r.x.Jv = r.x.any ? row_dot_x(c, r, V_TMP) : 0.f;
+  if constexpr (XG && XA) {
+    float jx = r.x.any ? row_dot_x(c, r, V_TMP) : 0.f;
+    if constexpr (XPAIR<XG>) jx += xor16f(jx); /* the pair's row: both halves */
+    r.x.Jv = jx;
+  }
   tsync();
   /* the quadratic's coefficients and the slope/curvature at alpha = 0 in one reduction:
      d1(0) = search . grad (the gradient update_constraint left for the current active
@@ -2193,7 +2548,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   float g20 = (r.ex && r.act) ? r.D * r.Jv * r.Jv : 0.f;
   g20 += (r.hf && r.actf) ? r.Df * jv0 * jv0 : 0.f;
   if (r.anyl) g20 += (r.hl && r.actl) ? r.Dl * jv0 * jv0 : 0.f;
-  if constexpr (XG) g20 += (r.x.ex && r.x.act) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
+  const bool xprim = !XPAIR<XG> || c.l < 16; /* the lane that counts the second bank's row (pair: half 0) */
+  if constexpr (XG) g20 += (r.x.ex && r.x.act && xprim) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
   float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
   tsum_n<4>(cc);
   const float c1 = cc[0], c2 = cc[1];
@@ -2209,7 +2565,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
     DlJ = r.hl ? r.Dl * sv : 0.f;
     DlJ2 = DlJ * sv;
   }
-  const float DXJ = (XG && r.x.ex) ? r.x.D * r.x.Jv : 0.f, DXJ2 = DXJ * r.x.Jv;
+  const float DXJ = (XG && r.x.ex && xprim) ? r.x.D * r.x.Jv : 0.f, DXJ2 = DXJ * r.x.Jv;
   float d1 = cc[2], d2 = c2 + cc[3];
   if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
   const float gtol = cfg->ls_tolerance * (-d1);
@@ -2270,6 +2626,66 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   return r.anyl ? iterate(BoolC<true>{}, BoolC<XG != 0 && XA>{}) : iterate(BoolC<false>{}, BoolC<XG != 0 && XA>{});
 }
 
+/* H p for the sole-pair kernels' Newton direction (hsolve_pair): M p, the floor rows' and dof rows'
+   D J J' p over the current active set (the terms of the factored tree Hessian H_t, hessian_factor),
+   plus the pair's active rows' D u u' p (u: the row over both limbs, held as two half rows). */
+__device__ __forceinline__ float hmul_pair(const Ctx& c, const Rows& r, const float jr[CAP], float p) {
+  const int ddep = vopq(c.ddep);
+  float jv, unused_;
+  const float Mp = mul_m_dot(c, r, jr, p, V_TMP, jv, -1, unused_);
+  float jx = row_dot_x(c, r, V_TMP);
+  jx += xor16f(jx);
+  const float w0 = (r.ex && r.act) ? r.D * jv : 0.f;
+  const float wx = (r.x.ex && r.x.act) ? r.x.D * jx : 0.f;
+  const float cs0 = colsum16_pre(jr, w0);
+  const float cs1 = colsum16((const gfloat_t*)xrows(c.L) + c.l * CAP, wx);
+  const float so = tsh(cs0, ddep), sx = tsh(cs0, 16 + ddep), s2 = tsh(cs1, ddep), s3 = tsh(cs1, 16 + ddep);
+  float y = 0.f;
+  if (c.l < NV) {
+    const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
+    const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
+    y = Mp + (f0 ? so : 0.f) + (f1 ? sx : 0.f) + (f2 ? s2 : 0.f) + (f3 ? s3 : 0.f);
+    if (r.hf && r.actf) y += r.Df * p;
+    if (r.anyl && r.hl && r.actl) y += r.Dl * p;
+  }
+  return y;
+}
+
+/* Newton direction H^-1 g of the sole-pair kernels. H = H_t + sum over the pair's active rows of
+   D u u': the pair's rows couple the two legs, which the tree factorization of H_t (hessian_factor)
+   cannot hold, so while any of them is active the system is solved by conjugate gradients
+   preconditioned with H_t. H_t^-1 H = I + H_t^-1 U D U' has at most 1 + rank(U) <= 13 distinct
+   eigenvalues (U spans the two limbs' dofs), so the iteration is exact in at most 13 steps in exact
+   arithmetic; it stops at a relative residual |r|^2 <= 1e-12 |g|^2 or after 16. Without an active pair
+   row it is the tree solve. [The oracle factors the dense H, mju_cholFactor; the two agree to the
+   residual.] Team-uniform loop (no matrix cores inside). */
+__device__ __forceinline__ float hsolve_pair(const Ctx& c, const Rows& r, const float jr[CAP], float g, float Dinv) {
+  const bool isd = c.l < NV;
+  float z = solve_ldl(c, g, Dinv);
+  if (team_ballot(r.x.ex && r.x.act) == 0u) return z;
+  float x = 0.f, rr = isd ? g : 0.f, p = isd ? z : 0.f;
+  float dd[2] = {isd ? rr * z : 0.f, isd ? g * g : 0.f};
+  tsum_n<2>(dd);
+  float rz = dd[0];
+  const float g2 = dd[1];
+  for (int it = 0; it < 16; it++) {
+    const float Hp = hmul_pair(c, r, jr, p);
+    const float pHp = tsum(isd ? p * Hp : 0.f);
+    if (!(pHp > 0.f)) break;
+    const float alpha = rz / pHp;
+    x += alpha * p;
+    rr -= alpha * Hp;
+    const float rn = tsum(isd ? rr * rr : 0.f);
+    if (!(rn > 1e-12f * g2)) break;
+    z = solve_ldl(c, rr, Dinv);
+    const float rzn = tsum(isd ? rr * z : 0.f);
+    const float beta = rzn / rz;
+    rz = rzn;
+    p = isd ? z + beta * p : 0.f;
+  }
+  return x;
+}
+
 /* constrained acceleration (mj_solNewton, primal). Returns qacc (dof lane). */
 template <int XG, bool XA = true>
 __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, float fs, float w, int& iters,
@@ -2291,8 +2707,14 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   js -= r.aref;
   float jwx = 0.f, jsx = 0.f;
   if (XG && XA && r.x.any) {
-    jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
-    jsx = row_dot_x(c, r, V_TMP2) - r.x.aref;
+    jwx = row_dot_x(c, r, V_TMP);
+    jsx = row_dot_x(c, r, V_TMP2);
+    if constexpr (XPAIR<XG>) {
+      jwx += xor16f(jwx);
+      jsx += xor16f(jsx);
+    }
+    jwx -= r.x.aref;
+    jsx -= r.x.aref;
   }
   tsync();
   float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
@@ -2317,7 +2739,9 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   STAMP(S_UPD0);
   float Dinv = hessian_factor<XG, XA>(c, r, true, 0, 0, 0, 0);
   STAMP(S_HESS0);
-  float search = -solve_ldl(c, grad, Dinv);
+  float search;
+  if constexpr (XPAIR<XG> && XA) search = -hsolve_pair(c, r, jr, grad, Dinv);
+  else search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
   int it = 0;
   while (live && it < cfg->iterations) {
@@ -2339,7 +2763,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     float red[3];
     red[0] = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
-    red[2] = (r.act != pa || r.actf != pf || (XG && r.x.act != pa2)) ? 1.f : 0.f;
+    red[2] = (r.act != pa || r.actf != pf || (XFLOOR<XG> && r.x.act != pa2)) ? 1.f : 0.f;
     if (r.anyl && r.actl != plo) red[2] = 1.f;
     tsum_n<3>(red);
     cost = red[0];
@@ -2356,7 +2780,9 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     const bool changed = red[2] > 0.f;
     if (changed) Dinv = hessian_factor<XG, XA>(c, r, false, pa, pf, plo, pa2);
     STAMP(S_HESS);
-    const float mg = solve_ldl(c, grad, Dinv);
+    float mg;
+    if constexpr (XPAIR<XG> && XA) mg = hsolve_pair(c, r, jr, grad, Dinv);
+    else mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
     search = -mg;
   }
@@ -2392,8 +2818,14 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   js -= r.aref;
   float jwx = 0.f, jsx = 0.f;
   if (XG && XA && r.x.any) {
-    jwx = row_dot_x(c, r, V_TMP) - r.x.aref;
-    jsx = row_dot_x(c, r, V_TMP2) - r.x.aref;
+    jwx = row_dot_x(c, r, V_TMP);
+    jsx = row_dot_x(c, r, V_TMP2);
+    if constexpr (XPAIR<XG>) {
+      jwx += xor16f(jwx);
+      jsx += xor16f(jsx);
+    }
+    jwx -= r.x.aref;
+    jsx -= r.x.aref;
   }
   tsync();
   float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
@@ -2561,7 +2993,20 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   float cpos[3], cdir[3], cmu;
   (void)contact_point<XG>(c, s, B, 0, cpos, cdir, cmu);
   float xpos[3], xdir[3];
-  if (XG && r.x.any) (void)contact_point<XG>(c, s, B, 1, xpos, xdir, cmu);
+  if constexpr (XPAIR<XG>) {
+    if (r.x.any) {
+      /* the pair's row direction n +- mu t; the half on geom1's limb (lanes 16-31) takes -F */
+      float n[3], t1[3], t2[3];
+      (void)pair_contact(c, B, xpos, n, t1, t2);
+      const int edge = c.l & 3;
+      const float sg = (edge & 1) ? -m->pair_friction[0] : m->pair_friction[0];
+      const float hs = (c.l >> 4) ? -1.f : 1.f;
+#pragma unroll
+      for (int k = 0; k < 3; k++) xdir[k] = hs * (n[k] + sg * (edge < 2 ? t1[k] : t2[k]));
+    }
+  } else if (XG && r.x.any) {
+    (void)contact_point<XG>(c, s, B, 1, xpos, xdir, cmu);
+  }
   const int rgeom = c.l >> 4;
   float tch0 = 0.f, tch1 = 0.f;
   for (int g = 0; g < (XG ? 2 * NGEOM : NGEOM); g++) {
@@ -2584,12 +3029,15 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     tsum_n<7>(ex7);
     float ext[6] = {ex7[0], ex7[1], ex7[2], ex7[3], ex7[4], ex7[5]};
     float fnt = ex7[6];
-    if (g < m->ngeom && c.l == m->geom_body[g]) {
+    /* the pair's halves: g = 2 geom2's body (+F), g = 3 geom1's (-F, in xdir); each foot's touch
+       sensor takes the pair's normal force (its geom is in the contact) */
+    const int gg = (XPAIR<XG> && b1) ? m->pair_geom[g == NGEOM ? 1 : 0] : g;
+    if (gg < m->ngeom && c.l == m->geom_body[gg]) {
 #pragma unroll
       for (int k = 0; k < 6; k++) fext[k] += ext[k];
     }
-    if (g == m->geom_left_foot) tch0 = fnt;
-    if (g == m->geom_right_foot) tch1 = fnt;
+    if (gg == m->geom_left_foot) tch0 += fnt;
+    if (gg == m->geom_right_foot) tch1 += fnt;
   }
   sen.touch[0] = tch0;
   sen.touch[1] = tch1;
@@ -3470,10 +3918,11 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = c.L->ci[l][k];
     for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
   }
-  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (XG && r.x.ex ? 1 : 0) + (r.hf ? 1 : 0) + (r.hl ? 1 : 0)));
+  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (XG && r.x.ex && (!XPAIR<XG> || l < 16) ? 1 : 0) + (r.hf ? 1 : 0) +
+                               (r.hl ? 1 : 0)));
   if (l == 0) {
     d[ZB_DBG_MISC + 0] = (float)nefc;
-    d[ZB_DBG_MISC + 1] = (float)((r.nrow + (XG ? r.x.nrow : 0)) / 4);
+    d[ZB_DBG_MISC + 1] = (float)((r.nrow + (XG ? r.x.nrow / (XPAIR<XG> ? 2 : 1) : 0)) / 4);
     d[ZB_DBG_MISC + 2] = sen.touch[0];
     d[ZB_DBG_MISC + 3] = sen.touch[1];
     for (int k = 0; k < 4; k++) d[ZB_DBG_MISC + 4 + k] = sen.fq[k];
@@ -3503,63 +3952,40 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   }
 }
 
+/* the kernel instantiation for a handle: solver x collider set (zb_host.cpp needs_xg: 0 two soles,
+   1 / 2 general floor colliders, 3 the sole pair) x implicit damping (ZB_F_EULERDAMP, step kernel
+   only). f(S, X, D) is called with std::integral_constant values. */
+template <typename F>
+__host__ void with_variant(int solver, int xg, int ed, F&& f) {
+  using std::integral_constant;
+  auto by_xg = [&](auto S, auto D) {
+    switch (xg) {
+      case 3: f(S, integral_constant<int, 3>{}, D); break;
+      case 2: f(S, integral_constant<int, 2>{}, D); break;
+      case 1: f(S, integral_constant<int, 1>{}, D); break;
+      default: f(S, integral_constant<int, 0>{}, D); break;
+    }
+  };
+  auto by_ed = [&](auto S) {
+    if (ed) by_xg(S, integral_constant<int, 1>{});
+    else by_xg(S, integral_constant<int, 0>{});
+  };
+  if (solver == ZB_SOLVER_CG) by_ed(integral_constant<int, ZB_SOLVER_CG>{});
+  else by_ed(integral_constant<int, ZB_SOLVER_NEWTON>{});
+}
+
 int step_resident_blocks(int device, int xg, int solver, int ed) {
   int per_cu = 0, cus = 0;
   /* the instantiation the handle launches: CG and Newton differ in registers and LDS */
-  hipError_t e;
-#define ZB_OCC(S, X, D) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<S, X, D>, 64, 0)
-#define ZB_OCC2(S, D) (xg == 2 ? ZB_OCC(S, 2, D) : xg ? ZB_OCC(S, 1, D) : ZB_OCC(S, 0, D))
-  if (solver == ZB_SOLVER_CG)
-    e = ed ? ZB_OCC2(ZB_SOLVER_CG, 1) : ZB_OCC2(ZB_SOLVER_CG, 0);
-  else
-    e = ed ? ZB_OCC2(ZB_SOLVER_NEWTON, 1) : ZB_OCC2(ZB_SOLVER_NEWTON, 0);
-#undef ZB_OCC2
-#undef ZB_OCC
+  hipError_t e = hipSuccess;
+  with_variant(solver, xg, ed, [&](auto S, auto X, auto D) {
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<decltype(S)::value, decltype(X)::value,
+                                                                          decltype(D)::value>, 64, 0);
+  });
   if (e != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
   return per_cu * cus;
 }
-
-/* the instantiation for the handle's solver and collider set */
-#define ZB_LAUNCH_VARIANT(K, grid, block, s, args)                                                        \
-  do {                                                                                                    \
-    if ((args).solver == ZB_SOLVER_CG) {                                                                  \
-      if ((args).xg == 2) hipLaunchKernelGGL((K<ZB_SOLVER_CG, 2>), grid, block, 0, s, args);              \
-      else if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_CG, 1>), grid, block, 0, s, args);              \
-      else hipLaunchKernelGGL((K<ZB_SOLVER_CG, 0>), grid, block, 0, s, args);                             \
-    } else {                                                                                              \
-      if ((args).xg == 2) hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, 2>), grid, block, 0, s, args);          \
-      else if ((args).xg) hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, 1>), grid, block, 0, s, args);          \
-      else hipLaunchKernelGGL((K<ZB_SOLVER_NEWTON, 0>), grid, block, 0, s, args);                         \
-    }                                                                                                     \
-  } while (0)
-
-/* the step kernel's instantiation: solver x collider set x implicit damping (ZB_F_EULERDAMP) */
-#define ZB_LAUNCH_STEP(grid, block, s, args)                                                              \
-  do {                                                                                                    \
-    const int xg_ = (args).xg;                                                                            \
-    if ((args).ed) {                                                                                      \
-      if ((args).solver == ZB_SOLVER_CG) {                                                                \
-        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 2, 1>), grid, block, 0, s, args);     \
-        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 1, 1>), grid, block, 0, s, args);     \
-        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 0, 1>), grid, block, 0, s, args);              \
-      } else {                                                                                            \
-        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 2, 1>), grid, block, 0, s, args); \
-        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 1, 1>), grid, block, 0, s, args); \
-        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 0, 1>), grid, block, 0, s, args);          \
-      }                                                                                                   \
-    } else {                                                                                              \
-      if ((args).solver == ZB_SOLVER_CG) {                                                                \
-        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 2, 0>), grid, block, 0, s, args);     \
-        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 1, 0>), grid, block, 0, s, args);     \
-        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_CG, 0, 0>), grid, block, 0, s, args);              \
-      } else {                                                                                            \
-        if (xg_ == 2) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 2, 0>), grid, block, 0, s, args); \
-        else if (xg_) hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 1, 0>), grid, block, 0, s, args); \
-        else hipLaunchKernelGGL((step_kernel<ZB_SOLVER_NEWTON, 0, 0>), grid, block, 0, s, args);          \
-      }                                                                                                   \
-    }                                                                                                     \
-  } while (0)
 
 hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
@@ -3571,7 +3997,9 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
   const StepArgs& b = a;
 #endif
   dim3 grid((unsigned)((b.n_envs + NTEAM - 1) / NTEAM * b.nchunk)), block(64);
-  ZB_LAUNCH_STEP(grid, block, s, b);
+  with_variant(b.solver, b.xg, b.ed, [&](auto S, auto X, auto D) {
+    hipLaunchKernelGGL((step_kernel<decltype(S)::value, decltype(X)::value, decltype(D)::value>), grid, block, 0, s, b);
+  });
   return hipGetLastError();
 }
 /* ksim's FeetAirtimeReward over one trajectory (train.py:503-546), row 0. The fused step
@@ -3615,13 +4043,17 @@ hipError_t launch_airtime_exact(const StepArgs& a, hipStream_t s) {
 hipError_t launch_reset(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  ZB_LAUNCH_VARIANT(reset_kernel, grid, block, s, a);
+  with_variant(a.solver, a.xg, 0, [&](auto S, auto X, auto) {
+    hipLaunchKernelGGL((reset_kernel<decltype(S)::value, decltype(X)::value>), grid, block, 0, s, a);
+  });
   return hipGetLastError();
 }
 hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
-  ZB_LAUNCH_VARIANT(debug_forward_kernel, grid, block, s, a);
+  with_variant(a.solver, a.xg, 0, [&](auto S, auto X, auto) {
+    hipLaunchKernelGGL((debug_forward_kernel<decltype(S)::value, decltype(X)::value>), grid, block, 0, s, a);
+  });
   return hipGetLastError();
 }
 

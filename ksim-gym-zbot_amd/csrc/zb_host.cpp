@@ -96,8 +96,9 @@ int check_model(const ZbModel* m) {
                            "collides the 2 box soles): compile_model(..., drop_colliders=True) to simulate without "
                            "them knowingly", m->nskip_geom);
   if (m->nskip_pair != 0)
-    return fail(ZB_EMODEL, "the source model collides %d pairs of its own geoms with each other; the engine has "
-                           "floor contacts only: compile_model(..., drop_self_contacts=True) to simulate without "
+    return fail(ZB_EMODEL, "the source model collides %d pairs of its own geoms with each other; the engine "
+                           "collides the robot with itself only as the two box soles against each other, with no "
+                           "other floor collider: compile_model(..., drop_self_contacts=True) to simulate without "
                            "them knowingly", m->nskip_pair);
   if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
@@ -112,6 +113,27 @@ int check_model(const ZbModel* m) {
       if (!(m->geom_size[g][k] > 0.f)) return fail(ZB_EMODEL, "geom %d: size[%d] must be positive", g, k);
   }
   if (m->max_depth > ZB_MAX_DEPTH) return fail(ZB_EMODEL, "dof depth %d > %d", m->max_depth, ZB_MAX_DEPTH);
+  if (m->npair < 0 || m->npair > 1) return fail(ZB_EMODEL, "npair=%d: the sole pair at most", m->npair);
+  if (m->npair == 1) {
+    /* the sole pair (zb_engine.hip pair_rows): the two box soles, the only floor colliders, on two
+       different limbs (its contact rows are one half-row per limb chain) */
+    const int g1 = m->pair_geom[0], g2 = m->pair_geom[1];
+    if (m->ngeom != 2 || !((g1 == 0 && g2 == 1) || (g1 == 1 && g2 == 0)))
+      return fail(ZB_EMODEL, "the sole pair needs exactly the two soles as colliders (ngeom=%d, pair %d-%d)",
+                  m->ngeom, g1, g2);
+    if (m->geom_type[0] != ZB_GEOM_BOX || m->geom_type[1] != ZB_GEOM_BOX)
+      return fail(ZB_EMODEL, "the sole pair collides two boxes (box-box)");
+    int head[2];
+    for (int k = 0; k < 2; k++) {
+      int d = m->body_lastdof[m->geom_body[k]];
+      if (d < 6) return fail(ZB_EMODEL, "sole %d hangs off the base: the pair needs both on limbs", k);
+      while (m->dof_parent[d] >= 6) d = m->dof_parent[d];
+      head[k] = d;
+    }
+    if (head[0] == head[1]) return fail(ZB_EMODEL, "the two soles of the pair are on one limb");
+    if (!(m->pair_friction[0] >= 0.f) || !(m->pair_solref[0] > 0.f) || !(m->pair_solimp[1] > 0.f))
+      return fail(ZB_EMODEL, "the sole pair's friction / solref / solimp are invalid");
+  }
   if (m->nu != ZB_NJ || m->nbody != ZB_NBODY_TASK)
     return fail(ZB_EMODEL, "task layout needs nu=%d nbody=%d (got %d, %d)", ZB_NJ, ZB_NBODY_TASK, m->nu, m->nbody);
   if (m->body_jnttype[1] != ZB_JNT_FREE) return fail(ZB_EMODEL, "body 1 must carry the free joint");
@@ -155,6 +177,7 @@ int check_model(const ZbModel* m) {
 }
 
 int needs_xg(const ZbModel* m) {
+  if (m->npair > 0) return 3; /* the two soles and their pair (the second bank holds the pair's rows) */
   if (m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX) return 0;
   for (int g = 0; g < m->ngeom; g++)
     if (m->geom_type[g] == ZB_GEOM_CYLINDER || m->geom_type[g] == ZB_GEOM_ELLIPSOID) return 2;
@@ -226,6 +249,15 @@ void build_topology(const ZbModel* m, int32_t t[zb::TP_NF][zb::TOPO_LANES]) {
     for (int g = 0; g < m->ngeom && g < 2 * TOPO_NGEOM; g++) {
       const int kd = m->body_lastdof[m->geom_body[g]];
       if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm[g / 2] |= 0xFFFFu << (16 * (g % 2));
+    }
+    if (m->npair > 0) {
+      /* the sole pair's rows (second bank): lanes 0-15 the half rows on geom2's limb (+J), lanes 16-31
+         those on geom1's limb (-J); the root dofs' columns cancel, so a limb dof only */
+      rm[1] = 0u;
+      for (int h = 0; h < 2; h++) {
+        const int kd = m->body_lastdof[m->geom_body[m->pair_geom[1 - h]]];
+        if (isd && l >= 6 && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm[1] |= 0xFFFFu << (16 * h);
+      }
     }
     t[TP_ROWMASK][l] = (int32_t)rm[0];
     t[TP_ROWMASK2][l] = (int32_t)rm[1];

@@ -434,6 +434,15 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                     continue
                 nsz = COLLIDER_TYPES[gt]
                 gd = {"name": gname, "body": name, "type": gt}
+                # contact parameters other than MuJoCo's defaults (the sole pair's mix, model.py)
+                for key, nk in (("friction", 3), ("solref", 2), ("solimp", 5)):
+                    if key in ga:
+                        vals = _floats(ga[key])
+                        dflt = {"friction": [1.0, 0.005, 0.0001], "solref": [0.02, 1.0],
+                                "solimp": [0.9, 0.95, 0.001, 0.5, 2.0]}[key]
+                        gd[key] = (vals + dflt[len(vals):])[:nk]
+                if "margin" in ga:
+                    gd["margin"] = float(ga["margin"])
                 gq = orientation(c, ga)
                 if "fromto" in ga:
                     if gt == "sphere":

@@ -385,7 +385,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
     m.nbody, m.nq, m.nv, m.nu = nbody, nq, nv, nu
     m.ngeom = len(geoms)
     m.nskip_geom = 0 if drop_colliders else len(desc.get("skipped_geoms", []))
-    m.nskip_pair = 0 if drop_self_contacts else len(desc.get("self_pairs", []))
+    m.nskip_pair = 0  # set with the sole pair below
     m.max_depth = max_depth
     opt = desc.get("option", {})
     g = opt.get("gravity", [0.0, 0.0, -9.81])
@@ -523,6 +523,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
     m.body_right_foot = names["Right_Foot"]
     m.geom_left_foot = geom_names.index(sites[m.site_left_foot]["touch_geom"])
     m.geom_right_foot = geom_names.index(sites[m.site_right_foot]["touch_geom"])
+    _compile_pairs(m, desc, geoms, geom_names, drop_self_contacts)
 
     _fill_tables(m, bodies, nbody, nv, dof_depth, dof_anc, dof_parent, [m.geom_body[g] for g in range(len(geoms))])
 
@@ -613,6 +614,43 @@ def _fill_tables(m, bodies, nbody, nv, dof_depth, dof_anc, dof_parent, geom_body
         m.level_nmem[lv] = len(mem)
         for k in range(8):
             m.level_mem[lv][k] = mem[k] if k < len(mem) else -1
+
+
+# MuJoCo's geom contact defaults (mjModel geom_friction / solref / solimp / margin)
+GEOM_FRICTION = (1.0, 0.005, 0.0001)
+GEOM_SOLREF = (0.02, 1.0)
+GEOM_SOLIMP = (0.9, 0.95, 0.001, 0.5, 2.0)
+
+
+def _compile_pairs(m, desc: dict, geoms: list, geom_names: list, drop: bool) -> None:
+    """The robot's own colliding pairs (desc["self_pairs"]): the engine simulates the two box soles
+    against each other (ZbModel.npair = 1; box-box) when that is the only pair and the soles are the
+    only floor colliders; any other pair is counted into nskip_pair, which zb_create refuses.
+    drop=True: none of them (npair = nskip_pair = 0). The pair's parameters are MuJoCo's mix for two
+    geoms of equal priority (mj_contactParam): friction the larger per component, solref / solimp the
+    mean (solmix 1 each), margin the larger [U: MuJoCo's mixing rule restated from its documentation]."""
+    m.npair = 0
+    pairs = [] if drop else [list(p) for p in desc.get("self_pairs", [])]
+    soles = {geom_names[m.geom_left_foot], geom_names[m.geom_right_foot]}
+    by_name = {g["name"]: g for g in geoms}
+    if (len(pairs) == 1 and set(pairs[0]) == soles and len(geoms) == 2
+            and all(by_name[n].get("type", "box") == "box" for n in soles)):
+        g1, g2 = (geom_names.index(n) for n in pairs[0])
+        m.npair = 1
+        m.pair_geom[0], m.pair_geom[1] = g1, g2
+        a, b = by_name[pairs[0][0]], by_name[pairs[0][1]]
+        fa, fb = a.get("friction", GEOM_FRICTION), b.get("friction", GEOM_FRICTION)
+        for k in range(3):
+            m.pair_friction[k] = max(float(fa[k]), float(fb[k]))
+        ra, rb = a.get("solref", GEOM_SOLREF), b.get("solref", GEOM_SOLREF)
+        for k in range(2):
+            m.pair_solref[k] = 0.5 * (float(ra[k]) + float(rb[k]))
+        ia, ib = a.get("solimp", GEOM_SOLIMP), b.get("solimp", GEOM_SOLIMP)
+        for k in range(5):
+            m.pair_solimp[k] = 0.5 * (float(ia[k]) + float(ib[k]))
+        m.pair_margin = max(float(a.get("margin", 0.0)), float(b.get("margin", 0.0)))
+        pairs = []
+    m.nskip_pair = len(pairs)
 
 
 def C_sizeof(t: type) -> int:  # noqa: N802

@@ -56,6 +56,8 @@ def lib(precision: str = "f32") -> C.CDLL:
     L.zbo_field_offset.argtypes = [C.c_int, C.c_char_p]
     L.zbo_field_offset.restype = C.c_long
     L.zbo_struct_bytes.argtypes = [C.c_int]
+    L.zbo_box_box.argtypes = [fp, fp, fp, fp, fp, fp, C.c_float, fp, fp, fp]
+    L.zbo_box_box.restype = C.c_int
     L.zbo_struct_bytes.restype = C.c_size_t
     if precision == "flops":
         L.zbo_flops_get.argtypes = [C.POINTER(C.c_uint64)]
@@ -182,6 +184,16 @@ class OracleEnv:
         assert rc == 0
         return dict(obs_actor=oa, obs_critic=oc, obs_extra=ox, reward_terms=terms, reward=rew, done=done,
                     success=success)
+
+
+def box_box(c1, R1, s1, c2, R2, s2, margin: float = 0.0, precision: str = "f64"):
+    """The oracle's box-box collider (zb_oracle.c box_box, the sole pair): (positions [k, 3],
+    distances [k], normal from box 1 to box 2). R: 3x3 rotations (columns = the box axes)."""
+    f = lambda a, n: np.ascontiguousarray(np.asarray(a, np.float32).reshape(n))  # noqa: E731
+    pos, dist, nrm = np.zeros(12, np.float32), np.zeros(4, np.float32), np.zeros(3, np.float32)
+    k = lib(precision).zbo_box_box(_p(f(c1, 3)), _p(f(R1, 9)), _p(f(s1, 3)), _p(f(c2, 3)), _p(f(R2, 9)), _p(f(s2, 3)),
+                                   float(margin), _p(pos), _p(dist), _p(nrm))
+    return pos.reshape(4, 3)[:k], dist[:k], nrm
 
 
 def forward_debug(cmodel, cfg, qpos, qvel, ctrl=None, precision: str = "f32") -> dict:

@@ -72,7 +72,8 @@ typedef float real;
 
 #define NB ZB_MAX_BODY
 #define NDOF ZB_MAX_DOF
-#define MAXEFC (2 * ZB_MAX_DOF + 4 * ZB_MAX_CON)
+#define NCON (ZB_MAX_CON + ZB_CON_PER_PAIR) /* floor contacts + the sole pair's */
+#define MAXEFC (2 * ZB_MAX_DOF + 4 * NCON)
 #define MINVAL ((real)1e-15)
 #define MINIMP ((real)0.0001)
 #define MAXIMP ((real)0.9999)
@@ -258,8 +259,8 @@ typedef struct {
   real site_xpos[ZB_MAX_SITE][3], site_xmat[ZB_MAX_SITE][9], site_xquat[ZB_MAX_SITE][4];
   /* contacts */
   int ncon;
-  real con_pos[ZB_MAX_CON][3], con_dist[ZB_MAX_CON], con_mu[ZB_MAX_CON], con_t1[ZB_MAX_CON][3];
-  int con_geom[ZB_MAX_CON], con_efc[ZB_MAX_CON];
+  real con_pos[NCON][3], con_dist[NCON], con_mu[NCON], con_n[NCON][3], con_t1[NCON][3], con_t2[NCON][3];
+  int con_geom[NCON], con_geom1[NCON], con_efc[NCON]; /* geom1 -1: the floor (world) */
   /* constraints */
   int nefc;
   int efc_type[MAXEFC], efc_id[MAXEFC];
@@ -577,8 +578,296 @@ static void add_contact(const ZbModel* m, ZbData* d, int g, const real p[3], rea
   d->con_pos[n][2] = p[2] - (real)0.5 * dist;
   d->con_dist[n] = dist;
   d->con_geom[n] = g;
+  d->con_geom1[n] = -1;
   d->con_mu[n] = m->floor_friction[0] * d->floor_mu;
+  /* frame (n, t1, t2 = n x t1) with n = +z */
+  d->con_n[n][0] = 0; d->con_n[n][1] = 0; d->con_n[n][2] = 1;
   for (int k = 0; k < 3; k++) d->con_t1[n][k] = t1[k];
+  d->con_t2[n][0] = -t1[1]; d->con_t2[n][1] = t1[0]; d->con_t2[n][2] = 0;
+}
+
+/* ------------------------- box-box (the sole pair) --------------------------
+ * [U: MuJoCo's mjc_BoxBox and MJX's box_box are not on disk; this restates the published
+ * separating-axis + face-clipping method they build on (Gottschalk's OBB test, ODE's dBoxBox), with
+ * MJX's four-point manifold selection. The HIP engine (zb_engine.hip pair_contacts) computes the same
+ * candidates in the same order.]
+ *  1. Separating axes: box 1's three face normals, box 2's, then the nine edge cross products
+ *     A_i x B_j (skipped when |A_i x B_j| < 1e-6, parallel edges), normalised.
+ *     sep(L) = |d.L| - (sum_k a_k |A_k.L| + sum_k b_k |B_k.L|), d = c2 - c1. Any sep > margin: no
+ *     contact. The largest sep (least penetration) wins, faces in order first; an edge axis replaces
+ *     the best only if sep > best + 0.05 |best| (ODE's preference for face contacts, 1.05 sep > best
+ *     for a penetration, kept for a gap inside the margin). The normal n = +-L
+ *     points from box 1 to box 2 (n.d >= 0).
+ *  2. Face axis k of the reference box R (I: the incident box): nr points from R toward I (n for
+ *     box 1, -n for box 2); the reference face centre o = cR + r_k nr, its axes u, v (R's axes k+1,
+ *     k+2, half sizes hu, hv). The incident face: I's axis j with the largest |I_j.nr|, on the side
+ *     facing R; its vertices in cyclic order (+,+) (-,+) (-,-) (+,-) along I's axes j+1, j+2. In
+ *     the frame (u, v, nr) at o, the candidates in this order:
+ *       (a) the incident vertices with |x| <= hu and |y| <= hv;
+ *       (b) for each incident edge k -> k+1, its crossings of the sides x = -hu, x = +hu, y = -hv,
+ *           y = +hv (strictly between the edge's ends) within the other coordinate's extent;
+ *       (c) the rectangle corners (-,-) (+,-) (+,+) (-,+) inside the incident quadrilateral, lifted
+ *           onto its plane.
+ *     A candidate at height z is a contact when z <= margin: dist = z, position o + x u + y v +
+ *     (z / 2) nr (halfway between the faces). A candidate within 1e-6 in x and y of an earlier one
+ *     within the margin is dropped. Of more than 4, MJX's manifold points: a the deepest (smallest z, first on ties), b the
+ *     farthest from a, c the farthest from the line ab, d the farthest from the line bc or, failing
+ *     that, ac (the first maximum of |cross(b - c, b - p)| over p followed by |cross(a - c, a - p)|),
+ *     keeping distinct points in the order a, b, c, d.
+ *  3. Edge axis A_i x B_j: one contact at the midpoint of the closest points of box 1's edge along
+ *     A_i that is most extreme toward box 2 and box 2's edge along B_j most extreme toward box 1 (the
+ *     line parameters clamped to the half lengths), dist = sep.
+ * Returns the contact count (<= 4): positions, distances, the common normal. */
+#define BB_MAXC 24
+static int box_box(const real c1[3], const real R1[9], const float* s1, const real c2[3], const real R2[9],
+                   const float* s2, real margin, real pos[4][3], real dist[4], real nrm[3]) {
+  real A[3][3], B[3][3], a[3] = {s1[0], s1[1], s1[2]}, b[3] = {s2[0], s2[1], s2[2]};
+  for (int k = 0; k < 3; k++)
+    for (int r = 0; r < 3; r++) {
+      A[k][r] = R1[3 * r + k]; /* column k of the rotation: the box's axis k in the world */
+      B[k][r] = R2[3 * r + k];
+    }
+  const real dv[3] = {c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]};
+  real best = -1e30, L[3] = {0, 0, 0};
+  int code = -1; /* 0-2: face of box 1, 3-5: face of box 2, 6 + 3 i + j: edge A_i x B_j */
+  for (int ax = 0; ax < 15; ax++) {
+    real l[3];
+    if (ax < 3) {
+      for (int r = 0; r < 3; r++) l[r] = A[ax][r];
+    } else if (ax < 6) {
+      for (int r = 0; r < 3; r++) l[r] = B[ax - 3][r];
+    } else {
+      const int i = (ax - 6) / 3, j = (ax - 6) % 3;
+      cross3(l, A[i], B[j]);
+      const real ln = SQRT(dot3(l, l));
+      if (ln < (real)1e-6) continue;
+      for (int r = 0; r < 3; r++) l[r] /= ln;
+    }
+    real ra = 0, rb = 0;
+    for (int k = 0; k < 3; k++) {
+      ra += a[k] * FABS(dot3(A[k], l));
+      rb += b[k] * FABS(dot3(B[k], l));
+    }
+    const real dl = dot3(dv, l);
+    const real sep = FABS(dl) - (ra + rb);
+    if (sep > margin) return 0;
+    const int better = ax < 6 ? sep > best : sep > best + (real)0.05 * FABS(best);
+    if (better) {
+      best = sep;
+      code = ax;
+      const real sg = dl < 0 ? (real)-1 : (real)1;
+      for (int r = 0; r < 3; r++) L[r] = sg * l[r];
+    }
+  }
+  for (int r = 0; r < 3; r++) nrm[r] = L[r];
+  if (code >= 6) {
+    const int i = (code - 6) / 3, j = (code - 6) % 3;
+    real p1[3] = {c1[0], c1[1], c1[2]}, p2[3] = {c2[0], c2[1], c2[2]};
+    for (int k = 0; k < 3; k++) {
+      if (k != i) {
+        const real sg = dot3(A[k], L) > 0 ? (real)1 : (real)-1;
+        for (int r = 0; r < 3; r++) p1[r] += sg * a[k] * A[k][r];
+      }
+      if (k != j) {
+        const real sg = dot3(B[k], L) > 0 ? (real)-1 : (real)1;
+        for (int r = 0; r < 3; r++) p2[r] += sg * b[k] * B[k][r];
+      }
+    }
+    const real w[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    const real ab = dot3(A[i], B[j]), d1 = dot3(A[i], w), d2 = dot3(B[j], w);
+    const real den = 1 - ab * ab;
+    real t = den > (real)1e-12 ? (real)((ab * d2 - d1) / den) : (real)0;
+    if (t < -a[i]) t = -a[i];
+    if (t > a[i]) t = a[i];
+    real u = d2 + t * ab;
+    if (u < -b[j]) u = -b[j];
+    if (u > b[j]) u = b[j];
+    for (int r = 0; r < 3; r++) pos[0][r] = (real)0.5 * (p1[r] + t * A[i][r] + p2[r] + u * B[j][r]);
+    dist[0] = best;
+    return 1;
+  }
+  /* face contact */
+  const int ref2 = code >= 3, k = ref2 ? code - 3 : code;
+  const real(*Rx)[3] = ref2 ? B : A;
+  const real(*Ix)[3] = ref2 ? A : B;
+  const real* rs = ref2 ? b : a;
+  const real* is = ref2 ? a : b;
+  const real* cR = ref2 ? c2 : c1;
+  const real* cI = ref2 ? c1 : c2;
+  real nr[3];
+  for (int r = 0; r < 3; r++) nr[r] = ref2 ? -L[r] : L[r];
+  const int ku = (k + 1) % 3, kv = (k + 2) % 3;
+  real o[3];
+  for (int r = 0; r < 3; r++) o[r] = cR[r] + rs[k] * nr[r];
+  const real hu = rs[ku], hv = rs[kv];
+  int jj = 0;
+  real bestd = -1;
+  for (int q = 0; q < 3; q++) {
+    const real v = FABS(dot3(Ix[q], nr));
+    if (v > bestd) { bestd = v; jj = q; }
+  }
+  const real sgi = dot3(Ix[jj], nr) > 0 ? (real)-1 : (real)1; /* the face of I facing R */
+  const int ja = (jj + 1) % 3, jb = (jj + 2) % 3;
+  static const real va[4] = {1, -1, -1, 1}, vb[4] = {1, 1, -1, -1};
+  real px[4], py[4], pz[4];
+  for (int q = 0; q < 4; q++) {
+    real V[3];
+    for (int r = 0; r < 3; r++)
+      V[r] = cI[r] + sgi * is[jj] * Ix[jj][r] + va[q] * is[ja] * Ix[ja][r] + vb[q] * is[jb] * Ix[jb][r] - o[r];
+    px[q] = dot3(V, Rx[ku]);
+    py[q] = dot3(V, Rx[kv]);
+    pz[q] = dot3(V, nr);
+  }
+  real cx[BB_MAXC], cy[BB_MAXC], cz[BB_MAXC];
+  int nc = 0;
+  /* (a) incident vertices inside the rectangle */
+  for (int q = 0; q < 4; q++)
+    if (FABS(px[q]) <= hu && FABS(py[q]) <= hv) { cx[nc] = px[q]; cy[nc] = py[q]; cz[nc] = pz[q]; nc++; }
+  /* (b) incident edges crossing the rectangle's sides */
+  for (int q = 0; q < 4; q++) {
+    const int q1 = (q + 1) & 3;
+    for (int sd = 0; sd < 4; sd++) {
+      const int isx = sd < 2;
+      const real X = (sd & 1) ? (isx ? hu : hv) : (isx ? -hu : -hv);
+      const real e0 = isx ? px[q] : py[q], e1 = isx ? px[q1] : py[q1];
+      if (!((e0 - X) * (e1 - X) < 0)) continue;
+      const real t = (X - e0) / (e1 - e0);
+      const real oth = isx ? py[q] + t * (py[q1] - py[q]) : px[q] + t * (px[q1] - px[q]);
+      if (FABS(oth) > (isx ? hv : hu)) continue;
+      cx[nc] = isx ? X : oth;
+      cy[nc] = isx ? oth : X;
+      cz[nc] = pz[q] + t * (pz[q1] - pz[q]);
+      nc++;
+    }
+  }
+  /* (c) rectangle corners inside the incident quadrilateral, on its plane */
+  {
+    real ni[3];
+    for (int r = 0; r < 3; r++) ni[r] = sgi * Ix[jj][r];
+    const real nx = dot3(ni, Rx[ku]), ny = dot3(ni, Rx[kv]), nz = dot3(ni, nr);
+    static const real ca[4] = {-1, 1, 1, -1}, cb[4] = {-1, -1, 1, 1};
+    for (int q = 0; q < 4; q++) {
+      const real X = ca[q] * hu, Y = cb[q] * hv;
+      int pos_ = 0, neg_ = 0;
+      for (int e = 0; e < 4; e++) {
+        const int e1 = (e + 1) & 3;
+        const real cr = (px[e1] - px[e]) * (Y - py[e]) - (py[e1] - py[e]) * (X - px[e]);
+        pos_ += cr >= 0;
+        neg_ += cr <= 0;
+      }
+      if (pos_ < 4 && neg_ < 4) continue;
+      cx[nc] = X;
+      cy[nc] = Y;
+      cz[nc] = pz[0] - (nx * (X - px[0]) + ny * (Y - py[0])) / nz;
+      nc++;
+    }
+  }
+  /* contacts within the margin; a candidate within 1e-6 (x and y) of an earlier one within the margin
+     is a duplicate and dropped */
+  int keep[BB_MAXC], nk = 0;
+  for (int q = 0; q < nc; q++) {
+    if (!(cz[q] <= margin)) continue;
+    int dup = 0;
+    for (int e = 0; e < q; e++)
+      if (cz[e] <= margin && FABS(cx[q] - cx[e]) <= (real)1e-6 && FABS(cy[q] - cy[e]) <= (real)1e-6) dup = 1;
+    if (!dup) keep[nk++] = q;
+  }
+  int sel[4], ns = 0;
+  if (nk <= 4) {
+    for (int q = 0; q < nk; q++) sel[ns++] = keep[q];
+  } else {
+    int ia = keep[0];
+    for (int q = 1; q < nk; q++)
+      if (cz[keep[q]] < cz[ia]) ia = keep[q];
+    int ib = ia;
+    real bm = -1;
+    for (int q = 0; q < nk; q++) {
+      const int p = keep[q];
+      const real dd = (cx[p] - cx[ia]) * (cx[p] - cx[ia]) + (cy[p] - cy[ia]) * (cy[p] - cy[ia]);
+      if (dd > bm) { bm = dd; ib = p; }
+    }
+    int ic = ia;
+    bm = -1;
+    for (int q = 0; q < nk; q++) {
+      const int p = keep[q];
+      const real dd = FABS((cx[ib] - cx[ia]) * (cy[p] - cy[ia]) - (cy[ib] - cy[ia]) * (cx[p] - cx[ia]));
+      if (dd > bm) { bm = dd; ic = p; }
+    }
+    int id = ia;
+    bm = -1;
+    for (int pass = 0; pass < 2; pass++) {
+      const int s0 = pass == 0 ? ib : ia;
+      for (int q = 0; q < nk; q++) {
+        const int p = keep[q];
+        const real dd = FABS((cx[s0] - cx[ic]) * (cy[s0] - cy[p]) - (cy[s0] - cy[ic]) * (cx[s0] - cx[p]));
+        if (dd > bm) { bm = dd; id = p; }
+      }
+    }
+    const int cand[4] = {ia, ib, ic, id};
+    for (int q = 0; q < 4; q++) {
+      int dup = 0;
+      for (int e = 0; e < ns; e++) dup |= sel[e] == cand[q];
+      if (!dup) sel[ns++] = cand[q];
+    }
+  }
+  for (int q = 0; q < ns; q++) {
+    const int p = sel[q];
+    for (int r = 0; r < 3; r++)
+      pos[q][r] = o[r] + cx[p] * Rx[ku][r] + cy[p] * Rx[kv][r] + (real)0.5 * cz[p] * nr[r];
+    dist[q] = cz[p];
+  }
+  return ns;
+}
+
+/* mju_makeFrame for a contact normal: t1 = (0,1,0) (or (0,0,1) when |n_y| >= 0.5) made orthogonal to
+   n and normalised, t2 = n x t1 */
+static void make_frame(const real n[3], real t1[3], real t2[3]) {
+  real y[3] = {0, 1, 0};
+  if (!(FABS(n[1]) < (real)0.5)) { y[1] = 0; y[2] = 1; }
+  const real d = dot3(n, y);
+  for (int k = 0; k < 3; k++) t1[k] = y[k] - d * n[k];
+  const real ln = SQRT(dot3(t1, t1));
+  for (int k = 0; k < 3; k++) t1[k] /= ln;
+  cross3(t2, n, t1);
+}
+
+/* the sole pair's contacts (ZbModel.npair): box-box of geoms pair_geom[0] (geom1) and [1] (geom2) */
+static void pair_collision(const ZbModel* m, ZbData* d) {
+  if (m->npair < 1) return;
+  const int g1 = m->pair_geom[0], g2 = m->pair_geom[1];
+  real pos[4][3], dist[4], n[3];
+  const int nc = box_box(d->geom_xpos[g1], d->geom_xmat[g1], m->geom_size[g1], d->geom_xpos[g2], d->geom_xmat[g2],
+                         m->geom_size[g2], m->pair_margin, pos, dist, n);
+  real t1[3], t2[3];
+  if (nc > 0) make_frame(n, t1, t2);
+  for (int q = 0; q < nc && d->ncon < NCON; q++) {
+    const int c = d->ncon++;
+    for (int k = 0; k < 3; k++) {
+      d->con_pos[c][k] = pos[q][k];
+      d->con_n[c][k] = n[k];
+      d->con_t1[c][k] = t1[k];
+      d->con_t2[c][k] = t2[k];
+    }
+    d->con_dist[c] = dist[q];
+    d->con_geom[c] = g2;
+    d->con_geom1[c] = g1;
+    d->con_mu[c] = m->pair_friction[0];
+  }
+}
+
+/* box_box for the known-answer tests (tests/test_colliders.py); frames as 3x3 row-major rotations */
+int zbo_box_box(const float* c1, const float* R1, const float* s1, const float* c2, const float* R2, const float* s2,
+                float margin, float* pos, float* dist, float* nrm) {
+  real a[3], b[3], Ra[9], Rb[9], p[4][3], dd[4], n[3];
+  for (int k = 0; k < 3; k++) { a[k] = c1[k]; b[k] = c2[k]; }
+  for (int k = 0; k < 9; k++) { Ra[k] = R1[k]; Rb[k] = R2[k]; }
+  const int nc = box_box(a, Ra, s1, b, Rb, s2, margin, p, dd, n);
+  for (int q = 0; q < nc; q++) {
+    for (int k = 0; k < 3; k++) pos[3 * q + k] = (float)p[q][k];
+    dist[q] = (float)dd[q];
+  }
+  for (int k = 0; k < 3; k++) nrm[k] = (float)n[k];
+  return nc;
 }
 
 static void collision(const ZbModel* m, ZbData* d) {
@@ -678,6 +967,7 @@ static void collision(const ZbModel* m, ZbData* d) {
       }
     }
   }
+  pair_collision(m, d);
 }
 
 /* ----------------------- constraint construction -------------------------- */
@@ -763,19 +1053,32 @@ static void make_constraint(const ZbModel* m, ZbData* d, real dt) {
       }
     }
   }
-  /* contacts: pyramidal cone, condim 3 -> 4 rows (+t1, -t1, +t2, -t2) */
-  static const real n[3] = {0, 0, 1};
+  /* contacts: pyramidal cone, condim 3 -> 4 rows (+t1, -t1, +t2, -t2). A contact between two robot
+     geoms (the sole pair) has J = J(body2) - J(body1) at the contact point (mj_jacDifPair; the root
+     dofs' columns cancel exactly) and diagApprox from both bodies' translational invweight0 */
   for (int c = 0; c < d->ncon; c++) {
     int body = m->geom_body[d->con_geom[c]];
+    const int b1 = d->con_geom1[c] >= 0 ? m->geom_body[d->con_geom1[c]] : -1;
     /* frame (n, t1, t2 = n x t1), collision() */
+    const real* n = d->con_n[c];
     const real* t1 = d->con_t1[c];
-    const real t2[3] = {-t1[1], t1[0], 0};
+    const real* t2 = d->con_t2[c];
     real Jn[NDOF], Jt1[NDOF], Jt2[NDOF];
     point_jac_row(m, d, body, d->con_pos[c], n, Jn);
     point_jac_row(m, d, body, d->con_pos[c], t1, Jt1);
     point_jac_row(m, d, body, d->con_pos[c], t2, Jt2);
+    if (b1 >= 0) {
+      real K[NDOF];
+      point_jac_row(m, d, b1, d->con_pos[c], n, K);
+      for (int j = 0; j < NDOF; j++) Jn[j] -= K[j];
+      point_jac_row(m, d, b1, d->con_pos[c], t1, K);
+      for (int j = 0; j < NDOF; j++) Jt1[j] -= K[j];
+      point_jac_row(m, d, b1, d->con_pos[c], t2, K);
+      for (int j = 0; j < NDOF; j++) Jt2[j] -= K[j];
+    }
     real mu = d->con_mu[c];
-    real dA = m->body_invweight0[body][0] * (1 + mu * mu);
+    real tran = m->body_invweight0[body][0] + (b1 >= 0 ? m->body_invweight0[b1][0] : 0);
+    real dA = tran * (1 + mu * mu);
     d->con_efc[c] = r;
     for (int e = 0; e < 4; e++) {
       const real* Jt = e < 2 ? Jt1 : Jt2;
@@ -785,7 +1088,8 @@ static void make_constraint(const ZbModel* m, ZbData* d, real dt) {
       d->efc_id[r] = c;
       d->efc_pos[r] = d->con_dist[c];
       d->efc_floss[r] = 0;
-      add_row_params(d, r, m->floor_solref, m->floor_solimp, dA, dt);
+      if (b1 >= 0) add_row_params(d, r, m->pair_solref, m->pair_solimp, dA, dt);
+      else add_row_params(d, r, m->floor_solref, m->floor_solimp, dA, dt);
       r++;
     }
   }
@@ -1064,10 +1368,12 @@ static void sensors(const ZbModel* m, ZbData* d) {
     real f0 = d->efc_force[r], f1 = d->efc_force[r + 1], f2 = d->efc_force[r + 2], f3 = d->efc_force[r + 3];
     real fn = f0 + f1 + f2 + f3, mu = d->con_mu[k];
     real ft1 = mu * (f0 - f1), ft2 = mu * (f2 - f3);
-    /* world force = fn*n + ft1*t1 + ft2*t2, n = (0,0,1), t2 = n x t1 = (-t1y, t1x, 0) */
-    const real* t1 = d->con_t1[k];
-    real F[3] = {ft1 * t1[0] - ft2 * t1[1], ft1 * t1[1] + ft2 * t1[0], fn};
-    int g = d->con_geom[k];
+    /* world force on geom2's body = fn*n + ft1*t1 + ft2*t2 (geom1's body, when it is not the
+       floor, takes the opposite: mj_rnePostConstraint) */
+    const real *nn = d->con_n[k], *t1 = d->con_t1[k], *t2 = d->con_t2[k];
+    real F[3];
+    for (int a = 0; a < 3; a++) F[a] = fn * nn[a] + ft1 * t1[a] + ft2 * t2[a];
+    int g = d->con_geom[k], g1 = d->con_geom1[k];
     int body = m->geom_body[g];
     real off[3] = {d->con_pos[k][0] - c[0], d->con_pos[k][1] - c[1], d->con_pos[k][2] - c[2]}, tq[3];
     cross3(tq, off, F);
@@ -1075,8 +1381,16 @@ static void sensors(const ZbModel* m, ZbData* d) {
       d->cfrc_ext[body][a] += tq[a];
       d->cfrc_ext[body][3 + a] += F[a];
     }
-    if (g == m->geom_left_foot) d->touch[0] += fn;
-    if (g == m->geom_right_foot) d->touch[1] += fn;
+    if (g1 >= 0) {
+      const int b1 = m->geom_body[g1];
+      for (int a = 0; a < 3; a++) {
+        d->cfrc_ext[b1][a] -= tq[a];
+        d->cfrc_ext[b1][3 + a] -= F[a];
+      }
+    }
+    /* touch: the normal force of the contacts of the sensor's geom (either side of the pair) */
+    if (g == m->geom_left_foot || g1 == m->geom_left_foot) d->touch[0] += fn;
+    if (g == m->geom_right_foot || g1 == m->geom_right_foot) d->touch[1] += fn;
   }
   /* mj_rnePostConstraint: cacc with qacc, cfrc_int */
   real cacc[NB][6], cfrc[NB][6];
@@ -1788,6 +2102,8 @@ static const FieldOff model_fields[] = {
     OFF(ZbModel, fe_amax), OFF(ZbModel, fe_max_torque), OFF(ZbModel, fe_max_velocity), OFF(ZbModel, geom_body),
     OFF(ZbModel, geom_type), OFF(ZbModel, geom_pos), OFF(ZbModel, geom_quat), OFF(ZbModel, geom_size), OFF(ZbModel, floor_friction),
     OFF(ZbModel, floor_solref), OFF(ZbModel, floor_solimp), OFF(ZbModel, floor_margin), OFF(ZbModel, pad_floor),
+    OFF(ZbModel, npair), OFF(ZbModel, pair_geom), OFF(ZbModel, pair_margin), OFF(ZbModel, pair_friction),
+    OFF(ZbModel, pair_solref), OFF(ZbModel, pair_solimp),
     OFF(ZbModel, site_body), OFF(ZbModel, site_pos), OFF(ZbModel, site_quat), OFF(ZbModel, site_imu),
     OFF(ZbModel, site_left_foot), OFF(ZbModel, site_right_foot), OFF(ZbModel, body_base), OFF(ZbModel, body_left_foot),
     OFF(ZbModel, body_right_foot), OFF(ZbModel, geom_left_foot), OFF(ZbModel, geom_right_foot),

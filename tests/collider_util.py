@@ -234,3 +234,34 @@ def touching_states(cm, n, seed, depth=0.003) -> np.ndarray:
         q[2] = -lowest_point(cm, q) - rng.uniform(0.0, depth)
         out[e] = q
     return out
+
+
+# ---- the sole pair (the two box soles against each other; ZbModel.npair, round 5) ----
+
+def sole_pair_desc() -> dict:
+    """The default robot whose two soles collide with each other (MuJoCo's default contype /
+    conaffinity 1 on both): desc["self_pairs"] holds the one pair, compile_model makes it npair 1."""
+    from zbot_amd.model import load_description
+
+    d = load_description()
+    d["self_pairs"] = [["left_foot_sole", "right_foot_sole"]]
+    return d
+
+
+# hip roll offsets (right +, left -) at which the soles cross each other (oracle: 2-4 contacts)
+CROSS_ROLL = (0.19, 0.41)
+
+
+def crossing_states(cm, n: int, seed: int, air: bool = True) -> np.ndarray:
+    """qpos [n, 27] with the legs rolled inward until the soles interpenetrate (CROSS_ROLL), small
+    joint perturbations; air=True lifts the base to 1 m (no floor contact), else the reset height."""
+    rng = np.random.default_rng(seed)
+    q0 = cm.reset_qpos().astype(np.float64)
+    out = np.repeat(q0[None], n, 0)
+    rr = rng.uniform(*CROSS_ROLL, size=n)
+    out[:, 7 + 1] += rr  # right_hip_roll
+    out[:, 7 + 7] -= rr  # left_hip_roll
+    out[:, 7:] += rng.normal(0, 0.01, size=(n, 20))
+    if air:
+        out[:, 2] = 1.0
+    return out

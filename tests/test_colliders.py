@@ -182,3 +182,90 @@ def test_ellipsoid_known_answers():
     u, v = np.meshgrid(np.linspace(0, 2 * np.pi, 721), np.linspace(0, np.pi, 361))
     surf = Ry @ np.stack([a * np.cos(u) * np.sin(v), b * np.sin(u) * np.sin(v), c * np.cos(v)]).reshape(3, -1)
     assert surf[2].min() + h == pytest.approx(d, abs=1e-6)
+
+
+# ---- box-box: the sole pair (oracle box_box; zb_engine.hip pair_contacts restates it) ----
+
+def _rot(axis, deg):
+    a = np.radians(deg)
+    c, s = np.cos(a), np.sin(a)
+    if axis == "x":
+        return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+    if axis == "y":
+        return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+def test_box_box_face_face_known_answer(oracle_mod):
+    """Two axis-aligned soles stacked 0.5 mm into each other and offset in x / y: the overlap rectangle's
+    four corners, each at depth -0.5 mm, halfway between the faces; the normal +z from box 1 to 2."""
+    s = [0.05, 0.03, 0.01]
+    pos, dist, n = oracle_mod.box_box([0, 0, 0], np.eye(3), s, [0.01, 0.005, 0.0195], np.eye(3), s)
+    np.testing.assert_allclose(n, [0, 0, 1], atol=1e-7)
+    np.testing.assert_allclose(dist, [-5e-4] * 4, atol=1e-7)
+    got = sorted(map(tuple, np.round(pos, 7)))
+    want = sorted([(-0.04, -0.025, 0.00975), (0.05, -0.025, 0.00975), (0.05, 0.03, 0.00975), (-0.04, 0.03, 0.00975)])
+    np.testing.assert_allclose(got, want, atol=1e-7)
+    # swapped: the normal still points from box 1 to box 2, now -z
+    _, dist2, n2 = oracle_mod.box_box([0.01, 0.005, 0.0195], np.eye(3), s, [0, 0, 0], np.eye(3), s)
+    np.testing.assert_allclose(n2, [0, 0, -1], atol=1e-7)
+    np.testing.assert_allclose(dist2, [-5e-4] * 4, atol=1e-7)
+
+
+def test_box_box_edge_edge_known_answer(oracle_mod):
+    """Two cubes standing on crossed edges (box 1 turned 45 deg about x, box 2 about y), 1 mm into each
+    other: one contact halfway between the edges at depth -1 mm, normal +z."""
+    h = 0.02
+    top = h * np.sqrt(2)
+    pos, dist, n = oracle_mod.box_box([0, 0, 0], _rot("x", 45), [h] * 3, [0, 0, 2 * top - 1e-3], _rot("y", 45), [h] * 3)
+    assert len(dist) == 1
+    np.testing.assert_allclose(n, [0, 0, 1], atol=1e-6)
+    np.testing.assert_allclose(dist, [-1e-3], atol=1e-6)
+    np.testing.assert_allclose(pos[0], [0, 0, top - 5e-4], atol=1e-6)
+
+
+def test_box_box_separated_and_margin(oracle_mod):
+    s = [0.05, 0.03, 0.01]
+    assert len(oracle_mod.box_box([0, 0, 0], np.eye(3), s, [0, 0, 0.021], np.eye(3), s)[1]) == 0
+    assert len(oracle_mod.box_box([0, 0, 0], np.eye(3), s, [0.2, 0, 0], np.eye(3), s)[1]) == 0
+    # within a 2 mm margin the 1 mm gap is a contact at dist +1 mm
+    _, dist, _ = oracle_mod.box_box([0, 0, 0], np.eye(3), s, [0, 0, 0.021], np.eye(3), s, margin=2e-3)
+    np.testing.assert_allclose(dist, [1e-3] * 4, atol=1e-7)
+
+
+def test_box_box_octagon_keeps_four_spread_points(oracle_mod):
+    """A square turned 45 deg on another: the overlap is an octagon (8 candidates); the manifold keeps
+    4 distinct points, all on both faces' overlap, at the common depth, spanning the octagon."""
+    h = 0.03
+    pos, dist, n = oracle_mod.box_box([0, 0, 0], np.eye(3), [h, h, 0.01], [0, 0, 0.0198], _rot("z", 45), [h, h, 0.01])
+    assert len(dist) == 4
+    np.testing.assert_allclose(dist, [-2e-4] * 4, atol=1e-7)
+    np.testing.assert_allclose(n, [0, 0, 1], atol=1e-7)
+    assert (np.abs(pos[:, :2]) <= h + 1e-7).all()
+    r45 = pos[:, :2] @ _rot("z", 45)[:2, :2]  # in box 2's frame
+    assert (np.abs(r45) <= h + 1e-7).all()
+    assert len({tuple(np.round(p, 6)) for p in pos}) == 4
+    span = np.linalg.norm(pos[:, :2] - pos[:, :2].mean(0), axis=1)
+    assert span.min() > 0.02  # spread around the octagon, not clustered
+
+
+def test_box_box_oracle_precisions_agree(oracle_mod):
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        w, x, y, z = q
+        R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                      [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                      [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+        c2 = rng.normal(0, 0.02, 3)
+        s1, s2 = rng.uniform(0.005, 0.04, 3), rng.uniform(0.005, 0.04, 3)
+        p64, d64, n64 = oracle_mod.box_box([0, 0, 0], np.eye(3), s1, c2, R, s2, precision="f64")
+        p32, d32, n32 = oracle_mod.box_box([0, 0, 0], np.eye(3), s1, c2, R, s2, precision="f32")
+        if len(d64) != len(d32):
+            continue  # a candidate at the clip boundary: the two precisions may keep different sets
+        # every contact is inside (or within the depth of) both boxes, and the normal is unit
+        assert abs(np.linalg.norm(n64) - 1) < 1e-5 if len(d64) else True
+        if len(d64):
+            assert (d64 <= 1e-6).all()
+            np.testing.assert_allclose(n32, n64, atol=1e-4)

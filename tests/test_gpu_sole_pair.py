@@ -1,0 +1,236 @@
+"""The sole pair on the GPU (round 5): the two box soles colliding with each other (ZbModel.npair, the
+XG 3 kernels: box-box contacts as two half rows per pyramid edge, the Newton direction by H_t-
+preconditioned conjugate gradients while a pair row is active) against the oracle (box_box, the dense
+Newton Hessian) on the same model and states: legs crossed until the soles interpenetrate, in the air
+and standing (tests/collider_util.py crossing_states)."""
+
+import numpy as np
+import pytest
+
+import collider_util as U
+from zbot_amd import compile_model, default_config
+from zbot_amd import cstructs as cs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def pair_model():
+    return compile_model(U.sole_pair_desc())
+
+
+def crossing_env(O, cm, cfg, n, seed):
+    """An oracle env at crossing_states: half in the air, half at the reset height (the soles on the
+    floor as well), at rest, no warm start."""
+    env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
+    env.reset()
+    q = np.concatenate([U.crossing_states(cm, n // 2, seed, air=True), U.crossing_states(cm, n - n // 2, seed + 1,
+                                                                                          air=False)])
+    env.state[:, :27] = q.astype(np.float32)
+    env.state[:, 32:58] = 0.0
+    env.state[:, cs.S_QACCW:cs.S_QACCW + 32] = 0.0
+    return env
+
+
+@pytest.mark.parametrize("solver", ["newton", "cg"])
+def test_debug_forward_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
+    """One forward pass: contact and constraint counts exact (floor + pair), the constrained
+    acceleration and both touch sensors against the fp64 oracle (the dense-Hessian Newton)."""
+    torch = torch_gpu
+    from zbot_amd.engine import DBG, HipEngine
+
+    cm = pair_model
+    cfg = default_config(solver=solver)
+    n = 64
+    env = crossing_env(oracle_mod, cm, cfg, n, seed=5)
+    st = env.state.copy()
+    ctrl = (np.random.default_rng(2).normal(size=(n, 20)) * 0.5).astype(np.float32)
+    eng = HipEngine(cm, cfg, n)
+    g = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()
+    worst, npair = 0.0, 0
+    for e in range(n):
+        ref = oracle_mod.forward_debug(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
+        assert int(g[e, DBG["misc"] + 1]) == ref["ncon"], e
+        assert int(g[e, DBG["misc"]]) == ref["nefc"], e
+        p = oracle_mod.constraint_problem(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
+        npair += int(((p["type"] == 2) & (np.abs(p["J"][:, :6]).max(1) == 0)).sum() > 0)
+        qa = g[e, DBG["qacc"]:DBG["qacc"] + 26]
+        err = np.abs(qa - ref["qacc"]).max() / max(1.0, np.abs(ref["qacc"]).max())
+        worst = max(worst, err)
+        # Newton: converged on both sides (the PCG direction vs the dense Cholesky); CG: 8 unconverged
+        # iterations along rounding-sensitive paths
+        assert err <= (1e-3 if solver == "newton" else 5e-2), (e, err)
+        np.testing.assert_allclose(g[e, DBG["misc"] + 2:DBG["misc"] + 4], ref["touch"], rtol=2e-3, atol=2e-3)
+    print(f"\n[sole pair {solver} debug forward] {npair} of {n} envs with pair contacts, max relative qacc "
+          f"error {worst:.2e}")
+    assert npair >= n // 2
+
+
+# One env-step from a crossing state at rest, fp32 engine vs fp32 oracle (the MaxErr contract of the
+# floor colliders, tests/test_gpu_colliders.py): the pair's first impulse through the two half rows.
+PAIR_TOL = {
+    "qpos": (5e-6, 0.0),
+    "qvel": (5e-4, 0.0),
+    "planner": (2e-4, 0.0),
+    "obs_actor": (5e-4, 0.0),
+    "obs_critic": (2e-3, 0.0),
+    "obs_extra": (5e-2, 0.0),
+    "reward": (2e-5, 0.0),
+    "reward_terms": (1e-5, 0.0),
+}
+
+
+@pytest.mark.parametrize("solver", ["newton", "cg"])
+def test_one_step_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
+    torch = torch_gpu
+    from test_gpu_colliders import COLLIDER_TOL_CG
+    from test_gpu_parity import MaxErr, one_step_outputs, oracle_steps
+
+    from zbot_amd.engine import HipEngine
+
+    cm = pair_model
+    cfg = default_config(solver=solver)
+    n = 64
+    env = crossing_env(oracle_mod, cm, cfg, n, seed=11)
+    eng = HipEngine(cm, cfg, n, seed=11)
+    err = MaxErr(f"sole pair {solver} one-step")
+    tols = COLLIDER_TOL_CG if solver == "cg" else PAIR_TOL
+    for t in range(2):
+        eng.set_state(torch.from_numpy(env.state.copy()))
+        eng.set_rand(torch.from_numpy(env.rand.copy()))
+        a = oracle_mod.synthetic_actions(cm.cmodel, 11, n, 0, t)
+        ref, ref64 = oracle_steps(oracle_mod, cm, cfg, env, a, 11)
+        out = eng.step(torch.from_numpy(a).cuda())
+        torch.cuda.synchronize()
+        gs = eng.get_state().cpu().numpy()
+        np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
+        for key, got, want in one_step_outputs(gs, out, env.state, ref):
+            err.add(key, got, want, *tols[key], ref64=ref64[key])
+    err.report()
+
+
+def test_rollout_launch_equals_steps(torch_gpu, pair_model, oracle_mod):
+    torch = torch_gpu
+    from zbot_amd.engine import HipEngine
+
+    cm = pair_model
+    cfg = default_config(push=True)
+    n, T = 32, 6
+    A = torch.from_numpy(np.stack([oracle_mod.synthetic_actions(cm.cmodel, 4, n, 0, t, std=0.3)
+                                   for t in range(T)])).cuda()
+    env = crossing_env(oracle_mod, cm, cfg, n, seed=4)
+    a = HipEngine(cm, cfg, n, seed=4)
+    b = HipEngine(cm, cfg, n, seed=4)
+    for h in (a, b):
+        h.set_state(torch.from_numpy(env.state.copy()))
+        h.set_rand(torch.from_numpy(env.rand.copy()))
+    for t in range(T):
+        a.step(A[t])
+    b.rollout(A, reward_sum=torch.zeros(n, device="cuda"))
+    torch.cuda.synchronize()
+    assert np.array_equal(a.get_state().cpu().numpy(), b.get_state().cpu().numpy())
+
+
+def crossing_actions(O, cm, seed, n, steps, std=0.1):
+    """JOINT_BIASES + noise with the hip rolls driven inward past the crossing offset: the legs scissor
+    and the soles meet while the robot stands, stumbles and falls."""
+    acts = np.stack([O.synthetic_actions(cm.cmodel, seed, n, 0, t, std=std) for t in range(steps)])
+    acts[:, :, 1] += 0.35  # right_hip_roll
+    acts[:, :, 7] -= 0.35  # left_hip_roll
+    return acts.astype(np.float32)
+
+
+@pytest.mark.parametrize("solver", ["newton", "cg"])
+def test_rollout_from_reset_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
+    """48 control steps of 64 envs from reset with the legs driven into each other: the first 8
+    rewards under the one-step contract (fp64 slack at a discontinuity), done flags exact over the
+    first 16 steps, then the ensemble contract (golden_ensemble_check). Prints how many oracle steps
+    had pair contacts (every 4th env)."""
+    torch = torch_gpu
+    from test_gpu_parity import GOLDEN_EXACT_STEPS, GOLDEN_TOL, GOLDEN_TOL_CG, MaxErr, golden_ensemble_check
+
+    from zbot_amd.engine import HipEngine
+
+    cm = pair_model
+    cfg = default_config(solver=solver)
+    n, steps, seed = 64, 48, 13
+    acts = crossing_actions(oracle_mod, cm, seed, n, steps)
+    e32 = oracle_mod.OracleEnv(cm.cmodel, cfg, n, seed=seed)
+    e64 = oracle_mod.OracleEnv(cm.cmodel, cfg, n, seed=seed, precision="f64")
+    e32.reset()
+    ref_r, ref_d, r64s, touching = [], [], [], 0
+    for t in range(steps):
+        if t < 8:
+            e64.state[:] = e32.state
+            e64.rand[:] = e32.rand
+            r64s.append(e64.step(acts[t])["reward"].copy())
+        o = e32.step(acts[t])
+        ref_r.append(o["reward"].copy())
+        ref_d.append(o["done"].copy())
+        for e in range(0, n, 4):
+            p = oracle_mod.constraint_problem(cm.cmodel, cfg, e32.state[e, :27], e32.state[e, 32:58], precision="f64")
+            touching += int(((p["type"] == 2) & (np.abs(p["J"][:, :6]).max(1) == 0)).any())
+    g = {"reward": np.stack(ref_r), "done": np.stack(ref_d), "final_state": e32.state.copy()}
+    eng = HipEngine(cm, cfg, n, seed=seed)
+    eng.reset()
+    rew, done = [], []
+    for t in range(steps):
+        o = eng.step(torch.from_numpy(acts[t]).cuda())
+        rew.append(o["reward"].cpu().numpy().copy())
+        done.append(o["done"].cpu().numpy().copy())
+    rew, done = np.stack(rew), np.stack(done)
+    np.testing.assert_array_equal(done[:GOLDEN_EXACT_STEPS], g["done"][:GOLDEN_EXACT_STEPS])
+    err = MaxErr(f"sole pair {solver} rollout from reset")
+    tol = GOLDEN_TOL_CG if solver == "cg" else GOLDEN_TOL
+    for t in range(8):
+        err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"], ref64=r64s[t])
+    print(f"\n[sole pair {solver} rollout] oracle env-steps with pair contacts (every 4th env): {touching} of "
+          f"{steps * n // 4}")
+    assert touching > 0
+    golden_ensemble_check(f"sole pair {solver}", rew, done, eng.get_state().cpu().numpy(), g)
+    err.report()
+
+
+def test_full_size_properties(torch_gpu, pair_model):
+    """C2 size (8192 envs, pushes + randomization, crossing actions, 8 steps from reset, two env
+    groups): finite, unit quaternions, bit-reproducible, shard- and group-invariant."""
+    torch = torch_gpu
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    cm = pair_model
+    cfg = default_config(push=True, randomize=True)
+    n = 8192
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    bias[1] += 0.35
+    bias[7] -= 0.35
+    acts = [bias + 0.2 * torch.randn(n, 20, device="cuda", generator=g) for _ in range(8)]
+
+    def run(h, lo=0, hi=n):
+        h.reset()
+        for a in acts:
+            out = h.step(a[lo:hi].contiguous())
+        return h.get_state(), out
+
+    st, out = run(HipEngine(cm, cfg, n, seed=9))
+    assert torch.isfinite(st[:, :58]).all() and torch.isfinite(out["obs_critic"]).all()
+    assert torch.allclose(st[:, 3:7].norm(dim=1), torch.ones(n, device="cuda"), atol=2e-6)
+    assert (st[:, cs.S_NAN].view(torch.int32) == 0).all()
+    again, _ = run(HipEngine(cm, cfg, n, seed=9))
+    assert torch.equal(again, st)
+    halves = [run(HipEngine(cm, cfg, n // 2, env_offset=off, seed=9), off, off + n // 2)[0] for off in (0, n // 2)]
+    assert torch.equal(torch.cat(halves), st)
+    grouped = EnvGroups(cm, cfg, n, groups=2, seed=9)
+    gst, _ = run(grouped)
+    grouped.join()
+    assert torch.equal(gst, st)

@@ -569,8 +569,10 @@ def test_self_contact_pairs_follow_mujocos_filter():
 
 
 def test_self_contacts_are_rejected_by_zb_create():
-    """A model whose own geoms collide with each other is refused (ZB_EMODEL, nskip_pair) rather
-    than simulated without those contacts; drop_self_contacts=True compiles it knowingly."""
+    """A model whose own geoms collide with each other is simulated when the only pair is the two
+    box soles (ZbModel.npair, the box-box kernels; round 5) and otherwise refused (ZB_EMODEL,
+    nskip_pair) rather than simulated without those contacts; drop_self_contacts=True compiles it
+    knowingly."""
     import ctypes as C
     import xml.etree.ElementTree as ET
 
@@ -587,11 +589,23 @@ def test_self_contacts_are_rejected_by_zb_create():
     L = E.load_library()
     h = C.c_void_p()
     cm = compile_model(desc)
-    assert cm.cmodel.nskip_pair == 1
+    assert cm.cmodel.nskip_pair == 0 and cm.cmodel.npair == 1
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc != -4, L.zb_last_error()
+    if rc == 0:
+        L.zb_destroy(h)
+    # a second pair (a sole against a shin box that also touches the floor) is refused
+    for b in root.iter("body"):
+        if b.get("name") == "right_knee_pitch_link":
+            b.append(ET.fromstring('<geom name="right_shin" type="box" size="0.015 0.02 0.05" pos="0 0 -0.05"/>'))
+    desc = load_mjcf(ET.tostring(root, encoding="unicode"))
+    assert len(desc["self_pairs"]) >= 2
+    cm = compile_model(desc)
+    assert cm.cmodel.nskip_pair == len(desc["self_pairs"]) and cm.cmodel.npair == 0
     rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
     assert rc == -4 and b"pairs of its own geoms" in L.zb_last_error()
     cm = compile_model(desc, drop_self_contacts=True)
-    assert cm.cmodel.nskip_pair == 0
+    assert cm.cmodel.nskip_pair == 0 and cm.cmodel.npair == 0
     rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
     assert rc != -4, L.zb_last_error()
     if rc == 0:
