@@ -686,7 +686,7 @@ def main(argv: list | None = None) -> None:
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the ksim_env (ZbotWalkingEnv.step), train_defaults (512 x 200), c1_gpu, "
                          "general_colliders (limbs model), cylinder_colliders (cyl model), the other solver's "
-                         "(cg_solver / newton_solver) and the eulerdamp legs")
+                         "(cg_solver / newton_solver), sole_pair and eulerdamp legs")
     ap.add_argument("--inloop-critic", type=int, default=0,
                     help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
                          "(1 one-wave, 2 two-wave, 3 four-wave; DESIGN.md §4f); 0 = the 8-wave critic afterwards")
@@ -801,6 +801,15 @@ def main(argv: list | None = None) -> None:
             cm, default_config(solver=other), f"the {other.upper() if other == 'cg' else 'Newton'} solver (ZbEnvConfig.solver)",
             "r03_flops_count_cg.json" if other == "cg" else "r03_flops_count.json", n, args.steps, args.warmup, dev,
             rank, world, args.seed, G)
+        from zbot_amd.model import load_description  # noqa: PLC0415
+
+        pdesc = load_description()
+        pdesc["self_pairs"] = [["left_foot_sole", "right_foot_sole"]]
+        extra_legs["sole_pair"] = bench_variant(
+            compile_model(pdesc), default_config(solver=args.solver),
+            "the sole-pair model (the soles also collide with each other, box-box; the XG 3 kernels, DESIGN.md §4l)",
+            "r03_flops_count.json" if args.solver == "newton" else "r03_flops_count_cg.json", n, args.steps,
+            args.warmup, dev, rank, world, args.seed, G)
         extra_legs["eulerdamp"] = bench_variant(
             cm, default_config(solver=args.solver, eulerdamp=True),
             f"mj_Euler's implicit joint damping (ZB_F_EULERDAMP), {args.solver} solver",
