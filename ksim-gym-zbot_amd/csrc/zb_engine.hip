@@ -2344,7 +2344,7 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
   if (c.l < NV) {
     const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
     qc = (f0 ? so : 0.f) + (f1 ? sx : 0.f);
-    if constexpr (XG) {
+    if constexpr (XG && XA) {
       const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
       qc += (f2 ? sx0 : 0.f) + (f3 ? sx1 : 0.f);
     }
@@ -2549,7 +2549,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   g20 += (r.hf && r.actf) ? r.Df * jv0 * jv0 : 0.f;
   if (r.anyl) g20 += (r.hl && r.actl) ? r.Dl * jv0 * jv0 : 0.f;
   const bool xprim = !XPAIR<XG> || c.l < 16; /* the lane that counts the second bank's row (pair: half 0) */
-  if constexpr (XG) g20 += (r.x.ex && r.x.act && xprim) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
+  /* XA: the second bank has rows in the wave; without, its terms are exact zeros and its row state is
+     not carried through the loop (fewer live registers in the common copy) */
+  if constexpr (XG && XA) g20 += (r.x.ex && r.x.act && xprim) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
   float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
   tsum_n<4>(cc);
   const float c1 = cc[0], c2 = cc[1];
@@ -2565,7 +2567,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
     DlJ = r.hl ? r.Dl * sv : 0.f;
     DlJ2 = DlJ * sv;
   }
-  const float DXJ = (XG && r.x.ex && xprim) ? r.x.D * r.x.Jv : 0.f, DXJ2 = DXJ * r.x.Jv;
+  const float DXJ = (XG && XA && r.x.ex && xprim) ? r.x.D * r.x.Jv : 0.f, DXJ2 = (XG && XA) ? DXJ * r.x.Jv : 0.f;
   float d1 = cc[2], d2 = c2 + cc[3];
   if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
   const float gtol = cfg->ls_tolerance * (-d1);
@@ -2753,17 +2755,17 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     x += alpha * search;
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
-    if constexpr (XG) r.x.jar += alpha * r.x.Jv;
+    if constexpr (XG && XA) r.x.jar += alpha * r.x.Jv;
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     float oldcost = cost;
-    const int pa = r.act, pf = r.actf, plo = r.actl, pa2 = XG ? r.x.act : 0;
+    const int pa = r.act, pf = r.actf, plo = r.actl, pa2 = (XG && XA) ? r.x.act : 0;
     /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
        value, so the bits of separate tsum calls): cost, |grad|^2 and the active-set change */
     float red[3];
     red[0] = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
-    red[2] = (r.act != pa || r.actf != pf || (XFLOOR<XG> && r.x.act != pa2)) ? 1.f : 0.f;
+    red[2] = (r.act != pa || r.actf != pf || (XFLOOR<XG> && XA && r.x.act != pa2)) ? 1.f : 0.f;
     if (r.anyl && r.actl != plo) red[2] = 1.f;
     tsum_n<3>(red);
     cost = red[0];
@@ -2855,7 +2857,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     x += alpha * search;
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
-    if constexpr (XG) r.x.jar += alpha * r.x.Jv;
+    if constexpr (XG && XA) r.x.jar += alpha * r.x.Jv;
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;

@@ -31,6 +31,8 @@ CASES = {
     # round 4: CG at C1's ensemble size, with pushes (the GPU test compares its first 8 rewards and
     # the 64-step ensemble statistics)
     "c2_cg_64x64_seed4": dict(n=64, steps=64, seed=4, push=True, randomize=False, std=0.1, solver="cg"),
+    # round 5: CG at BASELINE C1's own shape (64 envs x 128 steps, seed 0, the C1 actions)
+    "c1_cg_64x128_seed0": dict(n=64, steps=128, seed=0, push=False, randomize=False, std=0.05, solver="cg"),
     # round 5: mj_Euler's implicit joint damping (ZB_F_EULERDAMP), with each solver
     "c2_eulerdamp_seed5": dict(n=16, steps=16, seed=5, push=False, randomize=False, std=0.05, eulerdamp=True),
     "c5_cg_eulerdamp_seed6": dict(n=16, steps=16, seed=6, push=True, randomize=True, std=0.1, solver="cg",

@@ -447,7 +447,7 @@ def golden_ensemble_check(name, rew, done, final_state, g, k=5.0):
 
 
 @pytest.mark.parametrize("name", ["c1_64x128_seed0", "c5_push_seed1", "c2_cg_seed2", "c2_cg_64x64_seed4",
-                                  "c2_eulerdamp_seed5", "c5_cg_eulerdamp_seed6"])
+                                  "c2_eulerdamp_seed5", "c5_cg_eulerdamp_seed6", "c1_cg_64x128_seed0"])
 def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
     """The engine from reset against a committed oracle rollout. The first 8 rewards follow the
     one-step contract (MaxErr): the fp32 oracle is replayed along the fixture (it reproduces it),
