@@ -84,6 +84,13 @@ int zb_policy_destroy(ZbPolicy* p);
 #define ZB_POL_LAYOUT_WAVE4 3 /* ... over four waves (4 slots, 19 KB) */
 int zb_policy_set_layout(ZbPolicy* p, int layout);
 
+/* Persistent launches (round 5; default on): with the block layout a call over T steps is ONE launch
+ * that runs the recurrence over the T steps with each layer's carry in registers (HBM sees the carry
+ * once on entry and once after step T-1) instead of T launches. Bit-identical either way; 0 = one
+ * launch per step. The slot-sized layouts always launch per step. No reference counterpart: ksim
+ * scans the critic over the trajectory (get_ppo_variables, train.py:1683-1729). */
+int zb_policy_set_persistent(ZbPolicy* p, int on);
+
 /*
  * Actor over T consecutive steps of n envs (T = 1 in the rollout loop).
  *   mode ZB_POL_SAMPLE / ZB_POL_MODE: actions written; ZB_POL_EVAL: read.

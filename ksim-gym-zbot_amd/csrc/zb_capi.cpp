@@ -433,6 +433,7 @@ struct ZbPolicy {
   float* wpack;
   float* bias;
   int layout; /* ZB_POL_LAYOUT_* */
+  int persistent; /* block layout: one launch per call over all T steps */
 };
 
 static int pol_in(int kind) { return kind == ZB_POL_ACTOR ? ZB_POL_ACTOR_IN : ZB_POL_CRITIC_IN; }
@@ -499,6 +500,7 @@ int zb_policy_create(int kind, const float* params, size_t n_params, int device,
     const char* lay = getenv("ZB_POLICY_LAYOUT");
     h->layout = (lay && lay[0] == 'w') ? ZB_POL_LAYOUT_WAVE : ZB_POL_LAYOUT_BLOCK;
   }
+  h->persistent = 1;
   h->device = device;
   h->wpack = nullptr;
   h->bias = nullptr;
@@ -543,7 +545,10 @@ static int policy_run(ZbPolicy* h, int kind, const float* obs, int T, int n, flo
   HIPCHK(hipGetDevice(&cur));
   if (cur != h->device) HIPCHK(hipSetDevice(h->device));
   const size_t I = (size_t)pol_in(kind);
-  for (int t = 0; t < T; t++) {
+  /* the 8-wave block layout runs all T steps in one persistent launch (carry kept in registers,
+     zb_policy.hip); the slot-sized layouts launch once per step */
+  const int per_launch = (h->layout == ZB_POL_LAYOUT_BLOCK && h->persistent) ? T : 1;
+  for (int t = 0; t < T; t += per_launch) {
     zb::PolicyArgs a;
     memset(&a, 0, sizeof a);
     a.obs = obs + (size_t)t * n * I;
@@ -560,9 +565,16 @@ static int policy_run(ZbPolicy* h, int kind, const float* obs, int T, int n, flo
     a.wpack = h->wpack;
     a.bias = h->bias;
     a.layout = h->layout;
+    a.T = per_launch;
     hipError_t e = zb::launch_policy(kind, a, (hipStream_t)stream);
     if (e != hipSuccess) return fail(ZB_ELAUNCH, "policy launch: %s", hipGetErrorString(e));
   }
+  return ZB_OK;
+}
+
+int zb_policy_set_persistent(ZbPolicy* p, int on) {
+  if (!p) return fail(ZB_EARG, "null policy handle");
+  p->persistent = on ? 1 : 0;
   return ZB_OK;
 }
 

@@ -107,6 +107,8 @@ struct PolicyArgs {
   const float* wpack;     /* fragment-packed weights */
   const float* bias;      /* biases and head constants */
   int layout;             /* ZB_POL_LAYOUT_BLOCK / ZB_POL_LAYOUT_WAVE */
+  int T;                  /* block layout: steps run by one persistent launch (obs / reset / outputs
+                             advance by one [n] step each; carry in registers between steps) */
 };
 hipError_t launch_policy(int kind, const PolicyArgs& a, hipStream_t s);
 

@@ -87,7 +87,7 @@ __device__ __forceinline__ void tile_gemm(const float* xs, const float4* wp, int
 }
 
 template <int KIN, int NOUT, bool ACTOR>
-__global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
+__global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
 #pragma clang fp contract(off)
   constexpr int KPAD = (KIN + 15) / 16 * 16;
   constexpr int GIN = KPAD / 16;
@@ -103,7 +103,30 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c16 = lane & 15, k4 = lane >> 4;
   const int e0 = blockIdx.x * M;
-  const float4* wp4 = reinterpret_cast<const float4*>(a.wpack);
+  const float4* wp4 = reinterpret_cast<const float4*>(a0.wpack);
+
+  /* Persistent mode (a0.T > 1): one launch runs T steps of the recurrence. The
+     carry of every layer stays in this thread's registers between steps, as the 8 (unit, env) pairs
+     its GRU update writes (unit 16 w + c16, env crow(et, v, lane)); HBM sees the carry once on entry
+     and once after the last step. Every product is the same k-ordered chain as one launch per step,
+     so the results are the same bits. */
+  const int TT = a0.T > 1 ? a0.T : 1;
+  float hreg[D][NET][4];
+#pragma unroll
+  for (int l = 0; l < D; ++l)
+#pragma unroll
+    for (int et = 0; et < NET; ++et)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) hreg[l][et][v] = 0.f;
+  for (int t = 0; t < TT; ++t) {
+  PolicyArgs a = a0;
+  a.obs = a0.obs + (size_t)t * a0.n * KIN;
+  a.reset = a0.reset ? a0.reset + (size_t)t * a0.n : nullptr;
+  a.step = a0.step + (uint32_t)t;
+  if (a0.actions) a.actions = a0.actions + (size_t)t * a0.n * NJ;
+  if (a0.log_prob) a.log_prob = a0.log_prob + (size_t)t * a0.n * NJ;
+  if (a0.value) a.value = a0.value + (size_t)t * a0.n;
+  const bool last = t == TT - 1;
 
   constexpr int CPT = M * (H / 4) / NTHR;
   static_assert(CPT * NTHR == M * (H / 4), "carry float4s per thread");
@@ -119,7 +142,7 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
         cr[j] = *reinterpret_cast<const float4*>(a.carry + ((size_t)ge * D + l) * H + 4 * q);
     }
   };
-  load_carry(0); /* layer 0's carry loads overlap the observation tile and input projection */
+  if (t == 0) load_carry(0); /* layer 0's carry loads overlap the observation tile and input projection */
 
   /* 1. observation tile [k][env], zero-padded to KPAD. The block's 32 observation rows are one
         contiguous chunk of M * KIN floats: stream it with 16-B loads, all issued before the
@@ -185,18 +208,34 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
   constexpr size_t MAT = (size_t)(3 * H / 16) * GH * 64; /* one packed [3H][H] matrix, float4 */
   int cur = 0;
   for (int l = 0; l < D; ++l) {
-    /* carry of layer l (prefetched during layer l - 1) -> sh */
+    if (t == 0) {
+      /* carry of layer l (prefetched during layer l - 1) -> sh */
 #pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      const int i = tid + j * NTHR;
-      const int e = i / (H / 4), q = i - e * (H / 4);
-      sh[(4 * q) * LDA + e] = cr[j].x;
-      sh[(4 * q + 1) * LDA + e] = cr[j].y;
-      sh[(4 * q + 2) * LDA + e] = cr[j].z;
-      sh[(4 * q + 3) * LDA + e] = cr[j].w;
+      for (int j = 0; j < CPT; ++j) {
+        const int i = tid + j * NTHR;
+        const int e = i / (H / 4), q = i - e * (H / 4);
+        sh[(4 * q) * LDA + e] = cr[j].x;
+        sh[(4 * q + 1) * LDA + e] = cr[j].y;
+        sh[(4 * q + 2) * LDA + e] = cr[j].z;
+        sh[(4 * q + 3) * LDA + e] = cr[j].w;
+      }
+    } else {
+      /* persistent: the previous step's carry from registers (zero where the episode restarts) */
+      const int unit = 16 * w + c16;
+#pragma unroll
+      for (int et = 0; et < NET; ++et)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int e = crow(et, v, lane), ge = e0 + e;
+          float hv = hreg[0][et][v];
+#pragma unroll
+          for (int k = 1; k < D; ++k) hv = l == k ? hreg[k][et][v] : hv;
+          const bool rs = ge >= a.n || (a.reset && a.reset[ge]);
+          sh[unit * LDA + e] = rs ? 0.f : hv;
+        }
     }
     __syncthreads();
-    if (l + 1 < D) load_carry(l + 1);
+    if (t == 0 && l + 1 < D) load_carry(l + 1);
 
     const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
     const float4* whh = wih + MAT;
@@ -262,7 +301,11 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
         const float ho = sh[unit * LDA + e];
         const float hv = nn + z * (ho - nn);
         xo[unit * LDA + e] = hv;
-        if (e0 + e < a.n) a.carry[((size_t)(e0 + e) * D + l) * H + unit] = hv;
+        if (last && e0 + e < a.n) a.carry[((size_t)(e0 + e) * D + l) * H + unit] = hv;
+        if (TT > 1) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) hreg[k][et][v] = l == k ? hv : hreg[k][et][v];
+        }
       }
     }
     __syncthreads();
@@ -322,6 +365,8 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a) {
       a.value[e0 + tid] = acc + tail[0];
     }
   }
+  __syncthreads(); /* the heads' LDS reads are done before the next step's tiles overwrite them */
+  }  /* t */
 }
 
 /* ---------------------------------------------------------------------------------------------

@@ -89,7 +89,9 @@ def load_library(path: str | None = None) -> C.CDLL:
                                   vp]
     L.zb_policy_critic.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, vp]
     L.zb_policy_set_layout.argtypes = [vp, C.c_int]
-    for f in ("zb_policy_create", "zb_policy_destroy", "zb_policy_actor", "zb_policy_critic", "zb_policy_set_layout"):
+    L.zb_policy_set_persistent.argtypes = [vp, C.c_int]
+    for f in ("zb_policy_create", "zb_policy_destroy", "zb_policy_actor", "zb_policy_critic", "zb_policy_set_layout",
+              "zb_policy_set_persistent"):
         getattr(L, f).restype = C.c_int
     if L.zb_abi_version() != ABI_VERSION:
         raise ZbError(f"{lp}: ABI version {L.zb_abi_version()}, this binding speaks {ABI_VERSION}: rebuild it")

@@ -105,6 +105,11 @@ class GruPolicy:
         of a zb_step wave's slot); bit-identical results (include/zbot_policy.h)."""
         _check(self.L.zb_policy_set_layout(self.h, int(layout)))
 
+    def set_persistent(self, on: bool) -> None:
+        """Block layout: a call over T steps as one persistent launch with the carry in registers
+        (default), or one launch per step; bit-identical (include/zbot_policy.h)."""
+        _check(self.L.zb_policy_set_persistent(self.h, 1 if on else 0))
+
     def __del__(self):
         h = getattr(self, "h", None)
         if h is not None and h.value:

@@ -77,3 +77,34 @@ def test_bad_layout_raises(torch_gpu):
     pol = P.GruPolicy(P.ACTOR)
     with pytest.raises(ZbError):
         pol.set_layout(7)
+
+
+@pytest.mark.parametrize("kind", ["critic", "actor"])
+def test_persistent_launch_bit_identical(torch_gpu, kind):
+    """The block layout's persistent launch (one launch over T steps, the carry in registers between
+    steps; zb_policy_set_persistent) against one launch per step: values / actions / log
+    probabilities and the final carry bit-identical over a 33-step call with episode restarts and a
+    partial last tile."""
+    torch = torch_gpu
+    from zbot_amd import policy as P
+
+    n, T = 300, 33
+    spec = P.CRITIC if kind == "critic" else P.ACTOR
+    g = torch.Generator(device="cuda").manual_seed(17)
+    obs = torch.randn(T, n, P.CRITIC_IN if kind == "critic" else P.ACTOR_IN, device="cuda", generator=g)
+    reset = (torch.rand(T, n, device="cuda", generator=g) < 0.05).to(torch.uint8)
+    carry0 = 0.5 * torch.randn(n, P.DEPTH, P.HIDDEN, device="cuda", generator=g)
+    outs = []
+    for persistent in (True, False):
+        pol = P.GruPolicy(spec, P.init_params(spec, seed=6), layout=P.LAYOUT_BLOCK)
+        pol.set_persistent(persistent)
+        carry = carry0.clone()
+        if kind == "critic":
+            res = [pol.critic(obs, carry, reset=reset)]
+        else:
+            acts, lp = pol.actor(obs, carry, reset=reset, seed=3, step=5, log_prob=True)
+            res = [acts, lp]
+        torch.cuda.synchronize()
+        outs.append([_bits(r) for r in res] + [_bits(carry)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
