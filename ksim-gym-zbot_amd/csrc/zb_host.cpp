@@ -4,6 +4,7 @@
  * Plain C++ (no HIP): the product library links it, and csrc/sanitize.mk builds it with the host
  * sanitizers for tests/test_sanitizers.py.
  */
+#include <cstdlib>
 #include "zb_host.h"
 
 #include <stdarg.h>
@@ -178,7 +179,11 @@ int check_model(const ZbModel* m) {
 
 int needs_xg(const ZbModel* m) {
   if (m->npair > 0) return 3; /* the two soles and their pair (the second bank holds the pair's rows) */
-  if (m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX) return 0;
+  /* ZB_FORCE_XG=1 (profiling only): the two-sole model on the general-collider instantiation, whose
+     second bank then stays empty, to time that kernel's overhead on the headline's work */
+  const char* fx = getenv("ZB_FORCE_XG");
+  if (m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX)
+    return (fx && fx[0] == '1') ? 1 : 0;
   for (int g = 0; g < m->ngeom; g++)
     if (m->geom_type[g] == ZB_GEOM_CYLINDER || m->geom_type[g] == ZB_GEOM_ELLIPSOID) return 2;
   return 1;

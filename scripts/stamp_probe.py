@@ -41,17 +41,19 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         open(os.path.join(d, "zb_engine.hip"), "w").write(src)
         open(os.path.join(d, "zb_internal.h"), "w").write(hdr)
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{d}", f"-I{ROOT}/include",
-               "-fno-signed-zeros", "-freciprocal-math", "-fno-math-errno", "-fapprox-func", "-fno-slp-vectorize", "-DZB_STAMPS", "-shared",
-               "-o", out, os.path.join(d, "zb_engine.hip"), os.path.join(CSRC, "zb_capi.cpp")]
-        # zb_capi.cpp must see the patched header: compile it from the temp dir copy
-        capi = open(os.path.join(CSRC, "zb_capi.cpp")).read()
-        open(os.path.join(d, "zb_capi.cpp"), "w").write(capi)
-        cmd[-1] = os.path.join(d, "zb_capi.cpp")
-        # the PPO kernels share the library's C ABI file; the stamp build links the product object
-        subprocess.run(["make", "-C", CSRC, "-s", "build/zb_ppo.o", "build/zb_policy.o"], check=True)
-        cmd += [os.path.join(CSRC, "build", "zb_ppo.o"), os.path.join(CSRC, "build", "zb_policy.o")]
-        subprocess.run(cmd, check=True)
+        # zb_capi.cpp must see the patched header: compiled from a copy beside it
+        open(os.path.join(d, "zb_capi.cpp"), "w").write(open(os.path.join(CSRC, "zb_capi.cpp")).read())
+        flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{d}", f"-I{CSRC}", f"-I{ROOT}/include",
+                 "-fno-signed-zeros", "-freciprocal-math", "-fno-math-errno", "-fapprox-func", "-fno-slp-vectorize",
+                 "-DZB_STAMPS"]
+        objs = []
+        for f in ("zb_engine.hip", "zb_capi.cpp"):
+            objs.append(os.path.join(d, f + ".o"))
+            subprocess.run(["hipcc", *flags, "-c", "-o", objs[-1], os.path.join(d, f)], check=True)
+        # the PPO / policy kernels and the host half are the product objects
+        subprocess.run(["make", "-C", CSRC, "-s", "build/zb_ppo.o", "build/zb_policy.o", "build/zb_host.o"], check=True)
+        objs += [os.path.join(CSRC, "build", o) for o in ("zb_ppo.o", "zb_policy.o", "zb_host.o")]
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs], check=True)
     print(n, ",".join(names))
 
 

@@ -54,3 +54,48 @@ for ss in range(20):
     print(f"substep {ss:2d}: env {watch}: qvel err {dv[watch]:.2e} (fp64 gap {d64[watch]:.2e}), qacc err {dq[watch]:.2e}, "
           f"iters engine {it_g[watch]} oracle {o32.iters[watch]} f64 {o64.iters[watch]}; worst env {int(dv.argmax())} "
           f"{dv.max():.2e} (gap {d64[dv.argmax()]:.2e})")
+
+# the substep with the largest error on the watched env, replayed with the damping switch on and off
+worst = None
+o32 = O.OracleEnv(cm.cmodel, c1, n, seed=7)
+o32.state[:] = env.state
+o32.rand[:] = env.rand
+errs = []
+for ss in range(20):
+    st = o32.state.copy()
+    eng.set_state(torch.from_numpy(st))
+    eng.step(torch.from_numpy(a).cuda())
+    g = eng.get_state().cpu().numpy()
+    o32.step(a)
+    errs.append((np.abs(g[watch, 32:58] - o32.state[watch, 32:58]).max(), ss, st))
+_, ss, st = max(errs, key=lambda e: e[0])
+np.set_printoptions(precision=5, suppress=True, linewidth=200)
+print(f"replaying substep {ss}: touch {st[watch, cs.S_TOUCH:cs.S_TOUCH + 2]} prev contact "
+      f"{st[watch, cs.S_PREV_CONT:cs.S_PREV_CONT + 2]} qpos z {st[watch, 2]:.5f}")
+for e2 in (ed, not ed):
+    c2 = default_config(eulerdamp=e2, ctrl_dt=0.001)
+    oo = O.OracleEnv(cm.cmodel, c2, n, seed=7)
+    oo.state[:] = st
+    oo.rand[:] = o32.rand
+    ee = HipEngine(cm, c2, n, seed=7)
+    ee.set_rand(torch.from_numpy(oo.rand.copy()))
+    ee.set_state(torch.from_numpy(st))
+    ee.step(torch.from_numpy(a).cuda())
+    oo.step(a)
+    g = ee.get_state().cpu().numpy()
+    qa_g = g[watch, cs.S_QACCW:cs.S_QACCW + 26]
+    qa_o = oo.state[watch, cs.S_QACCW:cs.S_QACCW + 26]
+    print(f"eulerdamp {int(e2)}: iters engine {ee.solver_iters().cpu().numpy()[watch]} oracle {oo.iters[watch]}")
+    print("  engine qacc", qa_g)
+    print("  oracle qacc", qa_o)
+    print("  diff       ", qa_g - qa_o)
+ctrl = st[:, cs.S_PLAN_TAU:cs.S_PLAN_TAU + 20].copy()
+dbg = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()[watch]
+qa_e = dbg[1088:1088 + 26]
+print(f"engine forward at the replayed state (ctrl = planner tau): nefc {int(dbg[1728])} ncon {int(dbg[1729])}")
+print("  engine qacc", qa_e)
+for prec in ("f32", "f64"):
+    fd = O.forward_debug(cm.cmodel, c1, st[watch, :27], st[watch, 32:58], ctrl[watch], precision=prec)
+    print(f"{prec} oracle forward: ncon {fd['ncon']} nefc {fd['nefc']}; engine - oracle qacc max "
+          f"{np.abs(qa_e - fd['qacc']).max():.3e}")
+    print("  oracle qacc", fd["qacc"])

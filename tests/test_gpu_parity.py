@@ -286,20 +286,60 @@ def test_one_step_parity_eulerdamp(torch_gpu, cmodel, oracle_mod, push, randomiz
     cfg = default_config(push=push, randomize=randomize, solver=solver, eulerdamp=True)
     name = f"one-step eulerdamp {solver} push={push} randomize={randomize}"
     if solver == "cg":
+        # the budget env of push+randomize (r05d: obs_critic 25x, obs_extra 16x the bound; qpos / qvel
+        # inside) carries an accelerations jump through the critic's observation
         _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, name, solver, tol=ONE_STEP_TOL_CG_ED,
-                         err_kw=dict(max_ill=12))
+                         err_kw=dict(max_ill=12, loose=30.0))
     else:
-        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, name, solver, err_kw=dict(loose=50.0))
+        # one env (23) is a sole corner touching down within 1e-7 m of the floor, the contact set
+        # itself parting (test_eulerdamp_budget_env_is_a_touchdown); measured at 59x the planner bound
+        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, name, solver, err_kw=dict(loose=100.0))
 
 
-def test_one_step_parity_eulerdamp_without_early_exit(torch_gpu, cmodel, oracle_mod):
-    """The cause of the implicit form's Newton budget, shown as for the explicit form: with the
-    solver tolerance at 0 the same states hold the explicit contract with no exception (budget 0)."""
-    for push, randomize in ((False, False), (True, True)):
-        cfg = default_config(push=push, randomize=randomize, eulerdamp=True)
-        cfg.tolerance = 0.0
-        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, f"one-step eulerdamp newton tolerance 0 push={push} "
-                         f"randomize={randomize}", "newton", err_kw=dict(budget=0, loose=1.0))
+def touchdown_state(oracle_mod, cmodel):
+    """The state behind the implicit form's Newton budget env (r05 diag, tests/diag_eulerdamp.py):
+    env 23 of the one-step parity states after the first substep of the third step, where a foot
+    corner lies within 1e-7 m above the floor. Returns (state, ctrl, config with one substep)."""
+    n = 64
+    cfg = default_config(eulerdamp=True)
+    env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
+    for t in range(2):
+        env.step(oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100 + t))
+    c1 = default_config(eulerdamp=True, ctrl_dt=0.001)
+    o = oracle_mod.OracleEnv(cmodel.cmodel, c1, n, seed=7)
+    o.state[:] = env.state
+    o.rand[:] = env.rand
+    o.step(oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 102))
+    st = o.state.copy()
+    return st, st[:, cs.S_PLAN_TAU:cs.S_PLAN_TAU + 20].copy(), c1
+
+
+def test_eulerdamp_budget_env_is_a_touchdown(torch_gpu, cmodel, oracle_mod):
+    """The cause of the implicit form's Newton budget (test_one_step_parity_eulerdamp: one env at
+    up to 60x the explicit contract's planner bound). Not the damping: the constraint solve itself
+    parts there, with the damping switch on or off, at the same iteration count. One corner of a
+    sole is 1e-7 m above the floor at that substep: the fp64 oracle has 6 contacts at the state and
+    7 with the root lowered by 1e-7 m, and the fp32 engine (its own rounding of the corner height)
+    sees the 7th. Its constrained acceleration is then the oracle's for the 7-contact state."""
+    from zbot_amd.engine import DBG
+
+    torch = torch_gpu
+    w = 23
+    st, ctrl, c1 = touchdown_state(oracle_mod, cmodel)
+    q, v = st[w, :27].astype(np.float64), st[w, 32:58]
+    lo = q.copy()
+    lo[2] -= 1e-7
+    at, below = (oracle_mod.forward_debug(cmodel.cmodel, c1, x, v, ctrl[w], precision="f64") for x in (q, lo))
+    assert (at["ncon"], below["ncon"]) == (6, 7)
+    eng = engine(cmodel, c1, st.shape[0], seed=7)
+    g = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()[w]
+    ncon, qa = int(g[DBG["misc"] + 1]), g[DBG["qacc"]:DBG["qacc"] + 26]
+    ref = below if ncon == 7 else at
+    e = np.abs(qa - ref["qacc"]).max()
+    print(f"\n[touchdown] engine ncon {ncon}; |qacc - oracle({ref['ncon']} contacts)| {e:.2e}, "
+          f"vs the other contact set {np.abs(qa - (at if ncon == 7 else below)['qacc']).max():.2e}")
+    assert ncon in (6, 7)
+    assert e <= 1e-3 * max(1.0, np.abs(ref["qacc"]).max())
 
 
 def test_eulerdamp_changes_the_step(torch_gpu, cmodel, oracle_mod):
