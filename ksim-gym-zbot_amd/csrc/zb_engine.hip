@@ -100,6 +100,9 @@ struct __align__(16) EnvL {
   float Di[32];      /* 1 / pivot of the root-chain block */
   float ci[32][10];  /* body cinert (lane b), kept for RNE / sensors / observations */
   float par[5][32];  /* effective dof / body parameters (lane), see P_* */
+  float tgt[32];     /* general-collider kernels: the action target of the actuated dof lanes (held in a
+                        VGPR, the register allocator of those kernels spilled it and reloaded it from
+                        scratch at the head of every substep) */
   EnvS s;
   Sensors sen;
 #ifdef ZB_STAMPS
@@ -2884,12 +2887,15 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
 
 /* ----------------------------- Feetech actuator ---------------------------- */
 /* trapezoidal_step (train.py:1137-1196) + duty/torque (train.py:1260-1269) */
+template <int XG>
+constexpr bool TGT_LDS = XG != 0; /* the action target in EnvL.tgt, not in LaneS.tgt */
+template <int XG>
 __device__ __forceinline__ void feetech(const Ctx& c, LaneS& ls) {
   MP m = c.m;
   if (c.act < 0) { ls.ctrl = 0.f; return; }
   const int a = c.act;
   const float dt = c.cfg->dt;
-  float pos = ls.pp, vel = ls.pv, tgt = ls.tgt;
+  float pos = ls.pp, vel = ls.pv, tgt = TGT_LDS<XG> ? c.L->tgt[c.l] : ls.tgt;
   float err = tgt - pos;
   bool in_db = fabsf(err) <= DEADBAND;
   float db_vel = vel * 0.8f;
@@ -3706,7 +3712,11 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   bool partial = false;                               /* a chunk before the last one */
   for (int t = 0; t < nsteps; t++) {
     const bool last_t = t == nsteps - 1;
-    if (c.act >= 0) ls.tgt = a.action[((size_t)t * a.n_envs + vopq(ee)) * ZB_NJ + vopq(c.act)];
+    if (c.act >= 0) {
+      const float at = a.action[((size_t)t * a.n_envs + vopq(ee)) * ZB_NJ + vopq(c.act)];
+      if constexpr (TGT_LDS<XG>) c.L->tgt[c.l] = at;
+      else ls.tgt = at;
+    }
     if (ch == 0 && (cfg->flags & ZB_F_PUSH)) push_event(c, s, ls, a.curriculum);
     float total = 0.f;
     int ss = ch * cfg->n_substeps / K;
@@ -3721,7 +3731,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       c.m = opaque((MP)m);
       c.cfg = opaque((CP)cfg);
       STAMP(S_STEPEND);
-      if (!resetting && !ghost) feetech(c, ls);
+      if (!resetting && !ghost) feetech<XG>(c, ls);
       STAMP(S_FEETECH);
       int it_pass = 0;
       forward<SOLVER, XG>(c, s, ls, B, r, resetting || ss == cfg->n_substeps - 1, sen, it_pass);
