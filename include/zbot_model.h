@@ -15,7 +15,8 @@
  *     (root only) or hinge; other bodies are welded (no joint);
  *   - nbody <= ZB_MAX_BODY, nv <= ZB_MAX_DOF, dof-chain depth <= ZB_MAX_DEPTH;
  *   - collision = floor plane (world geom) vs up to ZB_MAX_GEOM per-body boxes,
- *     capsules, cylinders, spheres or ellipsoids (the two foot soles first by
+ *     capsules, cylinders, spheres, ellipsoids or convex meshes (<= ZB_MAX_MESHV hull
+ *     vertices each; the two foot soles first by
  *     convention); of the robot's own pairs only the two box soles against each
  *     other (npair <= 1, box-box, with no other floor collider); any other
  *     self pair is counted in nskip_pair and refused;
@@ -32,16 +33,18 @@ extern "C" {
 #endif
 
 #define ZB_MODEL_MAGIC   0x5A424F54u /* 'ZBOT' */
-#define ZB_MODEL_VERSION 7
+#define ZB_MODEL_VERSION 8
 
 #define ZB_MAX_BODY  32
 #define ZB_MAX_DOF   32
 #define ZB_MAX_QPOS  40
 #define ZB_MAX_DEPTH 12
 #define ZB_MAX_GEOM  4   /* floor colliders */
+#define ZB_MAX_MESHV 64  /* convex hull vertices of one mesh collider */
+#define ZB_MAX_MESHVERT (ZB_MAX_GEOM * ZB_MAX_MESHV)
 #define ZB_MAX_SITE  8
 #define ZB_MAX_ACT   32
-#define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-cylinder 4, plane-capsule 2, plane-sphere / -ellipsoid 1 */
+#define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-cylinder 4, plane-mesh 4, plane-capsule 2, plane-sphere / -ellipsoid 1 */
 #define ZB_CON_PER_PAIR 4 /* box-box (the sole pair): at most 4 contacts */
 #define ZB_MAX_CON  (ZB_MAX_GEOM * ZB_CON_PER_GEOM)
 
@@ -56,6 +59,7 @@ extern "C" {
 #define ZB_GEOM_ELLIPSOID 4
 #define ZB_GEOM_CYLINDER 5
 #define ZB_GEOM_BOX     6
+#define ZB_GEOM_MESH    7 /* a convex mesh: the hull's vertices (geom_vertadr / geom_vertnum / mesh_vert) */
 
 typedef struct ZbModel {
   /* header */
@@ -134,7 +138,8 @@ typedef struct ZbModel {
   float    geom_pos[ZB_MAX_GEOM][4];
   float    geom_quat[ZB_MAX_GEOM][4];
   float    geom_size[ZB_MAX_GEOM][4];    /* mjModel.geom_size: box half sizes; capsule / cylinder
-                                           radius, half-length (local z); sphere radius */
+                                           radius, half-length (local z); sphere radius; mesh: the
+                                           largest vertex distance from the geom origin (a bound) */
   /* floor: geom_priority=2 (train.py:1330) -> floor friction/solref/solimp win */
   float    floor_friction[4];            /* sliding, torsional, rolling */
   float    floor_solref[4];
@@ -200,6 +205,13 @@ typedef struct ZbModel {
   /* task constants: JOINT_BIASES (train.py:61-82), ctrl order */
   float    joint_bias[ZB_MAX_ACT];
   float    joint_weight[ZB_MAX_ACT];
+
+  /* convex mesh colliders (ZB_GEOM_MESH, model v8): geom g's hull vertices are
+     mesh_vert[geom_vertadr[g] .. + geom_vertnum[g]] in the geom frame, in the order MJX's plane_convex
+     scans them (its manifold selection breaks ties by index) */
+  int32_t  geom_vertadr[ZB_MAX_GEOM];
+  int32_t  geom_vertnum[ZB_MAX_GEOM];
+  float    mesh_vert[ZB_MAX_MESHVERT][4];
   float    pad_end[4];
 } ZbModel;
 

@@ -295,6 +295,26 @@ __device__ __forceinline__ void reduce_to_lds(const float v[K], float* out) {
   const int idx = ((threadIdx.x & 16) ? H : 0) + slot;
   if (li < S && slot < H && idx < K) out[idx] = sum;
 }
+/* the largest v over the lane's 16-lane row (every lane of the row ends with it) */
+__device__ __forceinline__ float rowmax16(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  v = fmaxf(v, dppf<0x141>(v));
+  v = fmaxf(v, dppf<0x140>(v));
+  return v;
+}
+/* (w, i) with the row's largest w, the smallest i among equal w (jnp.argmax's first maximum) */
+__device__ __forceinline__ void rowargmax16(float& w, int& i) {
+  auto take = [&](float w2, int i2) {
+    const bool t = w2 > w || (w2 == w && i2 < i);
+    w = t ? w2 : w;
+    i = t ? i2 : i;
+  };
+  take(dppf<0xB1>(w), dppi<0xB1>(i));
+  take(dppf<0x4E>(w), dppi<0x4E>(i));
+  take(dppf<0x141>(w), dppi<0x141>(i));
+  take(dppf<0x140>(w), dppi<0x140>(i));
+}
 __device__ __forceinline__ float tmaxf(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
@@ -1603,7 +1623,8 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
   /* XG 2: the instantiation for models with cylinders or ellipsoids (zb_host.cpp needs_xg), so that
      the others carry no code for them */
   const bool box = !XFLOOR<XG> || ty == ZB_GEOM_BOX, cap = XFLOOR<XG> && ty == ZB_GEOM_CAPSULE,
-             cyl = XG == 2 && ty == ZB_GEOM_CYLINDER, ell = XG == 2 && ty == ZB_GEOM_ELLIPSOID;
+             cyl = XG == 2 && ty == ZB_GEOM_CYLINDER, ell = XG == 2 && ty == ZB_GEOM_ELLIPSOID,
+             msh = XG == 2 && ty == ZB_GEOM_MESH;
   /* the lane's point relative to the geom centre, geom frame -> body frame -> world */
   float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
   float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
@@ -1611,7 +1632,7 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
   float p[3], dist;
   bool slot_ok;
   float t1x = 0.f, t1y = 1.f;
-  if (cyl || ell) {
+  if (cyl || ell || msh) {
     /* the geom's world rotation R from one quaternion product (body then geom), and its centre */
     const float qw0 = xqs[0] * gq[0] - xqs[1] * gq[1] - xqs[2] * gq[2] - xqs[3] * gq[3];
     const float qw1 = xqs[0] * gq[1] + xqs[1] * gq[0] + xqs[2] * gq[3] - xqs[3] * gq[2];
@@ -1623,7 +1644,107 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
     float cw[3];
     quat_rotate(cw, xqs, gp);
     const float c0 = xp[0] + cw[0], c1 = xp[1] + cw[1], c2 = xp[2] + cw[2];
-    if (cyl) {
+    if (msh) {
+      /* MJX plane_convex (oracle plane_mesh, which states the rule): the 16 lanes of the geom's half
+         scan the hull's vertices (lane li: vertices li + 16 j), every argmax a row reduction; the
+         lane's slot then takes manifold point a, b, c or d */
+      const int adr = m->geom_vertadr[g], nvt = m->geom_vertnum[g];
+      const int li = l & 15;
+      const float n[3] = {R20, R21, R22}; /* the plane normal in the geom frame, R' e_z */
+      const float pp[3] = {-(R00 * c0 + R10 * c1 + R20 * c2), -(R01 * c0 + R11 * c1 + R21 * c2),
+                           -(R02 * c0 + R12 * c1 + R22 * c2)}; /* the plane's origin, R' (0 - c) */
+      constexpr int NJ = ZB_MAX_MESHV / 16;
+      float v[NJ][3], sup[NJ], dm[NJ];
+      bool ok[NJ];
+      float smax = -3.0e38f;
+#pragma unroll
+      for (int j = 0; j < NJ; j++) {
+        const int i = li + 16 * j;
+        ok[j] = i < nvt;
+        const int ii = adr + (ok[j] ? i : 0);
+#pragma unroll
+        for (int k = 0; k < 3; k++) v[j][k] = m->mesh_vert[ii][k];
+        sup[j] = (pp[0] - v[j][0]) * n[0] + (pp[1] - v[j][1]) * n[1] + (pp[2] - v[j][2]) * n[2];
+        smax = ok[j] ? fmaxf(smax, sup[j]) : smax;
+      }
+      smax = rowmax16(smax);
+      const float thr = fmaxf(smax - 1e-3f, 0.f);
+#pragma unroll
+      for (int j = 0; j < NJ; j++) dm[j] = sup[j] > thr ? 0.f : -1e6f;
+      /* argmax over the lane's vertices (in index order), then over the row; absent vertices never win */
+      auto argmax = [&](auto value) {
+        float bw = -3.0e38f;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+          const float w = value(j) + dm[j];
+          if (ok[j] && w > bw) { bw = w; bi = li + 16 * j; }
+        }
+        rowargmax16(bw, bi);
+        return bi;
+      };
+      const int ia = argmax([&](int) { return 0.f; });
+      float A[3], Bv[3], Cv[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) A[k] = m->mesh_vert[adr + ia][k];
+      const int ib = argmax([&](int j) {
+        const float e0 = A[0] - v[j][0], e1 = A[1] - v[j][1], e2 = A[2] - v[j][2];
+        return e0 * e0 + e1 * e1 + e2 * e2;
+      });
+#pragma unroll
+      for (int k = 0; k < 3; k++) Bv[k] = m->mesh_vert[adr + ib][k];
+      float ab[3];
+      {
+        const float amb[3] = {A[0] - Bv[0], A[1] - Bv[1], A[2] - Bv[2]};
+        cross3(ab, n, amb);
+      }
+      const int ic = argmax([&](int j) {
+        const float ap[3] = {A[0] - v[j][0], A[1] - v[j][1], A[2] - v[j][2]};
+        return fabsf(dot3(ap, ab));
+      });
+#pragma unroll
+      for (int k = 0; k < 3; k++) Cv[k] = m->mesh_vert[adr + ic][k];
+      float ac[3], bc[3];
+      {
+        const float amc[3] = {A[0] - Cv[0], A[1] - Cv[1], A[2] - Cv[2]};
+        const float bmc[3] = {Bv[0] - Cv[0], Bv[1] - Cv[1], Bv[2] - Cv[2]};
+        cross3(ac, n, amc);
+        cross3(bc, n, bmc);
+      }
+      /* d: the first maximum over the concatenation [|(b - v) . bc| ..., |(a - v) . ac| ...] (key i, then
+         nvt + i) */
+      int id;
+      {
+        float bw = -3.0e38f;
+        int bk = 0x7fffffff;
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int j = 0; j < NJ; j++) {
+            const float* o = h == 0 ? Bv : A;
+            const float* ax = h == 0 ? bc : ac;
+            const float op[3] = {o[0] - v[j][0], o[1] - v[j][1], o[2] - v[j][2]};
+            const float w = fabsf(dot3(op, ax)) + dm[j];
+            const int key = (h == 0 ? 0 : nvt) + li + 16 * j;
+            if (ok[j] && (w > bw || (w == bw && key < bk))) { bw = w; bk = key; }
+          }
+        rowargmax16(bw, bk);
+        id = bk < nvt ? bk : bk - nvt;
+      }
+      /* the lane's manifold point (slot 0..3: a, b, c, d); a repeat of an earlier one has dist 1 */
+      const int iq = slot == 0 ? ia : (slot == 1 ? ib : (slot == 2 ? ic : id));
+      const bool uniq = slot == 0 || (slot == 1 && ib != ia) || (slot == 2 && ic != ia && ic != ib) ||
+                        (slot == 3 && id != ia && id != ib && id != ic);
+      float V[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) V[k] = m->mesh_vert[adr + iq][k];
+      const float sq = (pp[0] - V[0]) * n[0] + (pp[1] - V[1]) * n[1] + (pp[2] - V[2]) * n[2];
+      p[0] = c0 + (R00 * V[0] + R01 * V[1] + R02 * V[2]);
+      p[1] = c1 + (R10 * V[0] + R11 * V[1] + R12 * V[2]);
+      p[2] = c2 + (R20 * V[0] + R21 * V[1] + R22 * V[2]);
+      dist = uniq ? -sq : 1.f;
+      slot_ok = true;
+    } else if (cyl) {
       /* mjc_PlaneCylinder (oracle collision()): the axis a (R's z column) turned toward the plane,
          v the radius vector in the disk planes toward it; slot 0 the near disk's deepest point
          c + v + a, 1 the far disk's c + v - a, 2 / 3 the near disk's points 120 degrees away,

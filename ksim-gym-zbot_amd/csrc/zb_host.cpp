@@ -4,6 +4,7 @@
  * Plain C++ (no HIP): the product library links it, and csrc/sanitize.mk builds it with the host
  * sanitizers for tests/test_sanitizers.py.
  */
+#include <cmath>
 #include <cstdlib>
 #include "zb_host.h"
 
@@ -108,10 +109,23 @@ int check_model(const ZbModel* m) {
     return fail(ZB_EMODEL, "ngeom=%d: 1 to %d floor colliders", m->ngeom, ZB_MAX_GEOM);
   for (int g = 0; g < m->ngeom; g++) {
     const int ty = m->geom_type[g];
-    const int nsz = (ty == ZB_GEOM_BOX || ty == ZB_GEOM_ELLIPSOID) ? 3 : (ty == ZB_GEOM_CAPSULE || ty == ZB_GEOM_CYLINDER) ? 2 : ty == ZB_GEOM_SPHERE ? 1 : 0;
-    if (nsz == 0) return fail(ZB_EMODEL, "geom %d: type %d (box 6, cylinder 5, ellipsoid 4, capsule 3, sphere 2)", g, ty);
+    const int nsz = (ty == ZB_GEOM_BOX || ty == ZB_GEOM_ELLIPSOID) ? 3
+                    : (ty == ZB_GEOM_CAPSULE || ty == ZB_GEOM_CYLINDER) ? 2
+                    : (ty == ZB_GEOM_SPHERE || ty == ZB_GEOM_MESH) ? 1 : 0;
+    if (nsz == 0)
+      return fail(ZB_EMODEL, "geom %d: type %d (mesh 7, box 6, cylinder 5, ellipsoid 4, capsule 3, sphere 2)", g, ty);
     for (int k = 0; k < nsz; k++)
       if (!(m->geom_size[g][k] > 0.f)) return fail(ZB_EMODEL, "geom %d: size[%d] must be positive", g, k);
+    if (ty == ZB_GEOM_MESH) {
+      /* the hull's vertices: a range of the pool, within the kernel's per-mesh limit */
+      const int adr = m->geom_vertadr[g], num = m->geom_vertnum[g];
+      if (num < 1 || num > ZB_MAX_MESHV || adr < 0 || adr + num > ZB_MAX_MESHVERT)
+        return fail(ZB_EMODEL, "geom %d: mesh vertices [%d, %d + %d) (1 to %d hull vertices in a pool of %d)", g, adr,
+                    adr, num, ZB_MAX_MESHV, ZB_MAX_MESHVERT);
+      for (int i = adr; i < adr + num; i++)
+        for (int k = 0; k < 3; k++)
+          if (!std::isfinite(m->mesh_vert[i][k])) return fail(ZB_EMODEL, "geom %d: mesh vertex %d not finite", g, i - adr);
+    }
   }
   if (m->max_depth > ZB_MAX_DEPTH) return fail(ZB_EMODEL, "dof depth %d > %d", m->max_depth, ZB_MAX_DEPTH);
   if (m->npair < 0 || m->npair > 1) return fail(ZB_EMODEL, "npair=%d: the sole pair at most", m->npair);
@@ -185,7 +199,8 @@ int needs_xg(const ZbModel* m) {
   if (m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX)
     return (fx && fx[0] == '1') ? 1 : 0;
   for (int g = 0; g < m->ngeom; g++)
-    if (m->geom_type[g] == ZB_GEOM_CYLINDER || m->geom_type[g] == ZB_GEOM_ELLIPSOID) return 2;
+    if (m->geom_type[g] == ZB_GEOM_CYLINDER || m->geom_type[g] == ZB_GEOM_ELLIPSOID || m->geom_type[g] == ZB_GEOM_MESH)
+      return 2;
   return 1;
 }
 

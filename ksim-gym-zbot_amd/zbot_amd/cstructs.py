@@ -11,18 +11,20 @@ MAX_DOF = 32
 MAX_QPOS = 40
 MAX_DEPTH = 12
 MAX_GEOM = 4
+MAX_MESHV = 64
+MAX_MESHVERT = MAX_GEOM * MAX_MESHV
 MAX_SITE = 8
 MAX_ACT = 32
 CON_PER_GEOM = 4
 CON_PER_PAIR = 4  # box-box: the sole pair
 
 MODEL_MAGIC = 0x5A424F54
-MODEL_VERSION = 7
+MODEL_VERSION = 8
 
 JNT_NONE = -1
 JNT_FREE = 0
 JNT_HINGE = 3
-GEOM_SPHERE, GEOM_CAPSULE, GEOM_ELLIPSOID, GEOM_CYLINDER, GEOM_BOX = 2, 3, 4, 5, 6
+GEOM_SPHERE, GEOM_CAPSULE, GEOM_ELLIPSOID, GEOM_CYLINDER, GEOM_BOX, GEOM_MESH = 2, 3, 4, 5, 6, 7
 
 # zbot_layout.h
 NJ = 20
@@ -223,6 +225,9 @@ class ZbModel(C.Structure):
         ("level_mem", _i(MAX_DEPTH, 8)),
         ("joint_bias", _f(MAX_ACT)),
         ("joint_weight", _f(MAX_ACT)),
+        ("geom_vertadr", _i(MAX_GEOM)),
+        ("geom_vertnum", _i(MAX_GEOM)),
+        ("mesh_vert", _f(MAX_MESHVERT, 4)),
         ("pad_end", _f(4)),
     ]
 

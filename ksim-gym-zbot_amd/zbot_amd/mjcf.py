@@ -23,7 +23,12 @@ MJCF semantics (XML reference, MuJoCo 3.3.4 [U]):
     inertiafromgeom="true"), the mass and inertia of the body's box / sphere /
     capsule / cylinder / ellipsoid geoms (density or mass, fromto,
     inertiagrouprange), composed about their common centre of mass;
-  * box / capsule / cylinder / ellipsoid (size or fromto) / sphere <geom>s whose
+  * <asset><mesh> (inline `vertex`, or an STL / OBJ `file` under <compiler meshdir>,
+    `scale`) for mesh <geom>s: a mesh collider is its convex hull (MuJoCo and MJX collide a mesh
+    by its hull), its vertices in the geom frame in the file's order [U: MuJoCo re-centres a
+    mesh on its centroid and principal axes; the hull is the same solid either way]; at most
+    ZB_MAX_MESHV = 64 hull vertices (MJCF's maxhullvert can cap a hull);
+  * box / capsule / cylinder / ellipsoid (size or fromto) / sphere / mesh <geom>s whose
     contype / conaffinity pass MuJoCo's test against the floor's
     ((ct1 & ca2) || (ct2 & ca1)) as floor colliders, up to 4 in document order
     (the engine's plane-box / -capsule / -cylinder / -sphere / -ellipsoid contacts;
@@ -54,7 +59,8 @@ import numpy as np
 from .model import load_description
 
 # floor colliders the engine has contacts for (type -> sizes) and how many (ZB_MAX_GEOM)
-COLLIDER_TYPES = {"box": 3, "capsule": 2, "cylinder": 2, "sphere": 1, "ellipsoid": 3}
+COLLIDER_TYPES = {"box": 3, "capsule": 2, "cylinder": 2, "sphere": 1, "ellipsoid": 3, "mesh": 0}
+MAX_HULL_VERTS = 64  # ZB_MAX_MESHV
 MAX_COLLIDERS = 4
 
 
@@ -136,10 +142,92 @@ def _fromto_frame(ft: list[float]) -> tuple[np.ndarray, np.ndarray, float]:
     return pos, R, L / 2
 
 
+def read_mesh_file(path: str) -> np.ndarray:
+    """The vertices [n, 3] of an STL (binary or ASCII) or OBJ file, each distinct vertex once in the
+    order it first appears (MuJoCo merges an STL's repeated face corners)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    ext = os.path.splitext(path)[1].lower()
+    if ext == ".obj":
+        pts = [[float(x) for x in ln.split()[1:4]] for ln in data.decode("utf-8", "replace").splitlines()
+               if ln.startswith("v ")]
+    elif ext == ".stl":
+        ntri = int.from_bytes(data[80:84], "little") if len(data) >= 84 else -1
+        if len(data) == 84 + 50 * ntri:  # binary: header, count, then normal + 3 corners + attribute per face
+            rec = np.frombuffer(data[84:], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]),
+                                count=ntri)
+            pts = rec["v"].reshape(-1, 3).astype(np.float64).tolist()
+        else:
+            pts = [[float(x) for x in ln.split()[1:4]] for ln in data.decode("utf-8", "replace").splitlines()
+                   if ln.strip().startswith("vertex")]
+    else:
+        raise ValueError(f"mesh file {path}: STL or OBJ expected")
+    if not pts:
+        raise ValueError(f"mesh file {path}: no vertices")
+    out, seen = [], set()
+    for p in pts:
+        key = tuple(p)
+        if key not in seen:
+            seen.add(key)
+            out.append(p)
+    return np.asarray(out, dtype=np.float64)
+
+
+def hull_vertices(vert: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """The convex hull of a point set: (its vertices in the input order, its triangles as indices into
+    them). MuJoCo and MJX collide a mesh geom by this hull [U: MJX's vertex order]."""
+    from scipy.spatial import ConvexHull  # noqa: PLC0415
+
+    vert = np.asarray(vert, dtype=np.float64).reshape(-1, 3)
+    if len(vert) < 4:
+        raise ValueError("a mesh needs at least 4 vertices")
+    h = ConvexHull(vert)
+    keep = np.sort(h.vertices)
+    remap = {int(i): k for k, i in enumerate(keep)}
+    tri = np.array([[remap[int(i)] for i in s] for s in h.simplices], dtype=np.int64)
+    # orient every face outward (its normal away from the hull's centroid)
+    v = vert[keep]
+    cen = v.mean(axis=0)
+    for t in tri:
+        a, b, c = v[t[0]], v[t[1]], v[t[2]]
+        if np.dot(np.cross(b - a, c - a), a - cen) < 0:
+            t[1], t[2] = t[2], t[1]
+    return v, tri
+
+
+def _mesh_mass_props(v: np.ndarray, tri: np.ndarray):
+    """(volume, centroid, inertia tensor per unit density about the centroid) of the closed solid
+    with outward triangles tri over vertices v (signed tetrahedra from the origin)."""
+    vol, c1, S = 0.0, np.zeros(3), np.zeros((3, 3))
+    for t in tri:
+        a, b, c = v[t[0]], v[t[1]], v[t[2]]
+        dv = float(np.dot(a, np.cross(b, c))) / 6.0
+        vol += dv
+        c1 += dv * (a + b + c) / 4.0
+        # second moments of the tetrahedron (0, a, b, c): dv / 20 (sum_i x_i x_i' + (sum_i x_i)(sum_i x_i)')
+        s = a + b + c
+        S += dv / 20.0 * (np.outer(a, a) + np.outer(b, b) + np.outer(c, c) + np.outer(s, s))
+    if not vol > 0:
+        raise ValueError("mesh volume must be positive")
+    com = c1 / vol
+    S = S - vol * np.outer(com, com)
+    return vol, com, np.trace(S) * np.eye(3) - S
+
+
 def _geom_mass_inertia(ga: dict, quat: list[float]):
     """(mass, centre, rotation, principal moments) of one solid geom, as MuJoCo's compiler
     takes it for inertiafromgeom: uniform density (default 1000) or the geom's explicit mass."""
     gt = ga.get("type", "sphere")
+    if gt == "mesh":
+        # the hull as a solid [U: MuJoCo's mesh inertia modes; "convex" is the hull's volume]
+        hv, tri = hull_vertices(ga["_mesh_vert"])
+        vol, com, I1 = _mesh_mass_props(hv, tri)
+        m = float(ga["mass"]) if "mass" in ga else float(ga.get("density", "1000")) * vol
+        I = I1 * (m / vol)
+        diag, iq = _principal(I)
+        Rg = np.array(_quat_mat(quat))
+        pos = np.array(_floats(ga.get("pos", "0 0 0"), 3)) + Rg @ com
+        return m, pos, Rg @ np.array(_quat_mat(iq)), diag
     size = _floats(ga.get("size", "0 0 0"))
     pos = np.array(_floats(ga.get("pos", "0 0 0"), 3))
     R = np.array(_quat_mat(quat))
@@ -293,6 +381,24 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
     fromgeom = comp.get("inertiafromgeom", "auto") if comp is not None else "auto"
     grp = [int(x) for x in comp.get("inertiagrouprange", "0 5").split()] if comp is not None else [0, 5]
     defaults = _Defaults(root.find("default"))
+    meshdir = ""
+    if comp is not None:
+        meshdir = comp.get("meshdir", comp.get("assetdir", ""))
+    base_dir = os.path.dirname(os.path.abspath(src)) if not src.lstrip().startswith("<") else os.getcwd()
+    meshes: dict[str, np.ndarray] = {}
+    for asset in root.findall("asset"):
+        for me in asset.findall("mesh"):
+            ma = defaults.attrs(me, me.get("class", "main"))
+            if "vertex" in ma:
+                mv = np.array(_floats(ma["vertex"]), dtype=np.float64).reshape(-1, 3)
+            elif "file" in ma:
+                fp = ma["file"] if os.path.isabs(ma["file"]) else os.path.join(base_dir, meshdir, ma["file"])
+                mv = read_mesh_file(fp)
+            else:
+                raise ValueError(f"mesh {ma.get('name')}: vertex or file needed")
+            mv = mv * np.array(_floats(ma.get("scale", "1 1 1"), 3))
+            mname = ma.get("name") or os.path.splitext(os.path.basename(ma["file"]))[0]
+            meshes[mname] = mv
     flag = root.find("option/flag")
     filterparent = flag is None or flag.get("filterparent", "enable") != "disable"
     parent_of: dict[str, str] = {}
@@ -407,6 +513,10 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                 if c.tag == "geom":
                     ga = defaults.attrs(c, cls)
                     if grp[0] <= int(ga.get("group", "0")) <= grp[1]:
+                        if ga.get("type") == "mesh":
+                            if ga.get("mesh") not in meshes:
+                                raise ValueError(f"body {name}: geom of unknown mesh {ga.get('mesh')!r}")
+                            ga = dict(ga, _mesh_vert=meshes[ga["mesh"]])
                         parts.append(_geom_mass_inertia(ga, orientation(c, ga)))
             if not parts:
                 raise ValueError(f"body {name}: no <inertial> element and no geoms to infer it from")
@@ -434,6 +544,16 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                     continue
                 nsz = COLLIDER_TYPES[gt]
                 gd = {"name": gname, "body": name, "type": gt}
+                if gt == "mesh":
+                    if ga.get("mesh") not in meshes:
+                        raise ValueError(f"geom {gname}: unknown mesh {ga.get('mesh')!r}")
+                    hv, _ = hull_vertices(meshes[ga["mesh"]])
+                    if len(hv) > MAX_HULL_VERTS:
+                        # the engine's plane-mesh contact scans at most 64 hull vertices
+                        desc.setdefault("skipped_geoms", []).append(
+                            {"name": gname, "body": name, "type": gt, "hull_vertices": len(hv)})
+                        continue
+                    gd["vert"] = [[float(x) for x in p] for p in hv]
                 # contact parameters other than MuJoCo's defaults (the sole pair's mix, model.py)
                 for key, nk in (("friction", 3), ("solref", 2), ("solimp", 5)):
                     if key in ga:
@@ -444,7 +564,10 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                 if "margin" in ga:
                     gd["margin"] = float(ga["margin"])
                 gq = orientation(c, ga)
-                if "fromto" in ga:
+                if gt == "mesh":
+                    if "pos" in ga:
+                        gd["pos"] = _floats(ga["pos"], 3)
+                elif "fromto" in ga:
                     if gt == "sphere":
                         raise ValueError(f"geom {gd['name']}: fromto on a {gt} collider")
                     fpos, fR, hl = _fromto_frame(_floats(ga["fromto"], 6))
@@ -597,6 +720,12 @@ def to_mjcf(desc: dict) -> str:
         attrs = " ".join(f'{k}="{float(sc[k])!r}"' for k in ("armature", "damping", "frictionloss") if k in sc)
         lines.append(f'    <default class="{cname}"><joint {attrs}/></default>')
     lines.append("  </default>")
+    mesh_geoms = [g for g in desc.get("geoms", []) if g.get("type") == "mesh"]
+    if mesh_geoms:
+        lines.append("  <asset>")
+        for g in mesh_geoms:  # the hull's vertices inline, one mesh asset per collider
+            lines.append(f'    <mesh name="{g["name"]}_mesh" vertex="{_fmt(np.asarray(g["vert"]).ravel())}"/>')
+        lines.append("  </asset>")
     lines.append("  <worldbody>")
     fl = desc.get("floor", {})
     fattr = " ".join(f'{k}="{_fmt(fl[k])}"' for k in ("friction", "solref", "solimp") if k in fl)
@@ -645,7 +774,8 @@ def to_mjcf(desc: dict) -> str:
             gq = f' quat="{_fmt(g["quat"])}"' if "quat" in g else ""
             # contype 1 / conaffinity 0: the floor (1 / 1) collides with every collider and no two
             # colliders collide with each other, which is what the engine simulates
-            lines.append(f'{ind}  <geom name="{g["name"]}" type="{g.get("type", "box")}" size="{_fmt(g["size"])}"{gp}{gq} '
+            shape = (f'mesh="{g["name"]}_mesh"' if g.get("type") == "mesh" else f'size="{_fmt(g["size"])}"')
+            lines.append(f'{ind}  <geom name="{g["name"]}" type="{g.get("type", "box")}" {shape}{gp}{gq} '
                          f'contype="1" conaffinity="0"/>')
         for s in sites.get(b["name"], []):
             sq = f' quat="{_fmt(s["quat"])}"' if "quat" in s else ""

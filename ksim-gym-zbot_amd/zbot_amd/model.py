@@ -477,13 +477,30 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
         m.joint_weight[a] = JOINT_BIASES[a][2]
 
     gtypes = {"box": (cs.GEOM_BOX, 3), "capsule": (cs.GEOM_CAPSULE, 2), "cylinder": (cs.GEOM_CYLINDER, 2),
-              "sphere": (cs.GEOM_SPHERE, 1), "ellipsoid": (cs.GEOM_ELLIPSOID, 3)}
+              "sphere": (cs.GEOM_SPHERE, 1), "ellipsoid": (cs.GEOM_ELLIPSOID, 3), "mesh": (cs.GEOM_MESH, 0)}
+    vadr = 0
     for gi, gd in enumerate(geoms):
         gt = gd.get("type", "box")
         if gt not in gtypes:
-            raise ValueError(f"geom {gd['name']}: type {gt!r} (box, capsule, cylinder, sphere and ellipsoid collide with the floor)")
+            raise ValueError(f"geom {gd['name']}: type {gt!r} (box, capsule, cylinder, sphere, ellipsoid and convex "
+                             "mesh collide with the floor)")
         code, nsize = gtypes[gt]
-        if len(gd["size"]) < nsize or any(not (v > 0) for v in gd["size"][:nsize]):
+        if gt == "mesh":
+            # a convex mesh: its hull vertices in the geom frame, in the order MJX's plane_convex scans
+            # them; geom_size[0] = the largest vertex distance from the geom origin (the second bank's
+            # reach bound, zb_engine.hip contact_rows)
+            vert = np.asarray(gd["vert"], dtype=np.float64).reshape(-1, 3)
+            if not (1 <= len(vert) <= cs.MAX_MESHV) or not np.isfinite(vert).all():
+                raise ValueError(f"geom {gd['name']}: a mesh collider needs 1 to {cs.MAX_MESHV} finite hull vertices "
+                                 f"(has {len(vert)}; MJCF <mesh maxhullvert> can cap the hull)")
+            m.geom_vertadr[gi] = vadr
+            m.geom_vertnum[gi] = len(vert)
+            for i, v in enumerate(vert):
+                for k in range(3):
+                    m.mesh_vert[vadr + i][k] = float(v[k])
+            vadr += len(vert)
+            m.geom_size[gi][0] = max(float(np.sqrt((np.float32(vert) ** 2).sum(axis=1)).max()), 1e-6) * (1 + 1e-6)
+        elif len(gd["size"]) < nsize or any(not (v > 0) for v in gd["size"][:nsize]):
             raise ValueError(f"geom {gd['name']}: a {gt} needs {nsize} positive sizes")
         m.geom_body[gi] = names[gd["body"]]
         m.geom_type[gi] = code

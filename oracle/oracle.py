@@ -58,6 +58,8 @@ def lib(precision: str = "f32") -> C.CDLL:
     L.zbo_struct_bytes.argtypes = [C.c_int]
     L.zbo_box_box.argtypes = [fp, fp, fp, fp, fp, fp, C.c_float, fp, fp, fp]
     L.zbo_box_box.restype = C.c_int
+    L.zbo_plane_mesh.argtypes = [fp, C.c_int, fp, fp, C.c_float, C.POINTER(C.c_int32), fp, fp]
+    L.zbo_plane_mesh.restype = C.c_int
     L.zbo_struct_bytes.restype = C.c_size_t
     if precision == "flops":
         L.zbo_flops_get.argtypes = [C.POINTER(C.c_uint64)]
@@ -194,6 +196,21 @@ def box_box(c1, R1, s1, c2, R2, s2, margin: float = 0.0, precision: str = "f64")
     k = lib(precision).zbo_box_box(_p(f(c1, 3)), _p(f(R1, 9)), _p(f(s1, 3)), _p(f(c2, 3)), _p(f(R2, 9)), _p(f(s2, 3)),
                                    float(margin), _p(pos), _p(dist), _p(nrm))
     return pos.reshape(4, 3)[:k], dist[:k], nrm
+
+
+def plane_mesh(verts, R, c, margin: float = 0.0, precision: str = "f64"):
+    """The oracle's plane - convex mesh collider (zb_oracle.c plane_mesh, MJX's plane_convex): the four
+    candidates' vertex indices [4], distances [4] (1 for a repeat) and world positions [4, 3] (the
+    vertices, before the half-distance shift), and how many pass the margin. verts: [nv, 3] hull
+    vertices in the geom frame; R: the geom's 3x3 world rotation; c: its centre."""
+    v = np.zeros((len(verts), 4), np.float32)
+    v[:, :3] = np.asarray(verts, np.float32)
+    f = lambda a, n: np.ascontiguousarray(np.asarray(a, np.float32).reshape(n))  # noqa: E731
+    idx, dist, pos = np.zeros(4, np.int32), np.zeros(4, np.float32), np.zeros(12, np.float32)
+    k = lib(precision).zbo_plane_mesh(_p(v), len(verts), _p(f(R, 9)), _p(f(c, 3)), float(margin),
+                                      idx.ctypes.data_as(C.POINTER(C.c_int32)), _p(dist), _p(pos))
+    assert k >= 0
+    return idx, dist, pos.reshape(4, 3), k
 
 
 def forward_debug(cmodel, cfg, qpos, qvel, ctrl=None, precision: str = "f32") -> dict:

@@ -870,6 +870,108 @@ int zbo_box_box(const float* c1, const float* R1, const float* s1, const float* 
   return nc;
 }
 
+/* ------------------------- plane - convex mesh -------------------------------
+ * MJX's plane_convex with its _manifold_points (mjx/_src/collision_convex.py) [U: mujoco-mjx 3.3.4
+ * is not on disk; restated from its published method]. In the geom frame (R, c the geom's world
+ * rotation and centre; v_i its hull vertices, i < nv, in the model's order):
+ *   n = R' e_z, the plane normal; p = R' (0 - c), the plane's origin;
+ *   support_i = (p - v_i) . n, the depth of vertex i below the plane;
+ *   mask_i = support_i > max(0, max_j support_j - 1e-3): penetrating, within a 1 mm skin of the deepest;
+ *   every argmax below is over w_i = value_i + (mask_i ? 0 : -1e6), the first index on ties:
+ *   a = argmax w (the first masked vertex); b = argmax |a - v_i|^2 (the farthest from a);
+ *   c = argmax |(a - v_i) . (n x (a - b))| (the farthest from the line ab);
+ *   d = the first maximum of |(b - v_i) . (n x (b - c))| over i, then of |(a - v_i) . (n x (a - c))|.
+ * Contacts q = a, b, c, d (in this order): dist = -support (1 for a repeat of an earlier index),
+ * position the vertex in the world moved by -dist/2 along the plane normal, frame mju_makeFrame(+z).
+ * As for the other colliders, a contact exists where dist <= the margin. Writes the four candidates'
+ * vertex indices, distances and world positions (before the half-distance shift); returns how many
+ * pass the margin. */
+static int plane_mesh(const float (*vert)[4], int nv, const real R[9], const real c[3], real margin, int idx[4],
+                      real dist[4], real pos[4][3]) {
+  const real n[3] = {R[6], R[7], R[8]};
+  const real mc[3] = {-c[0], -c[1], -c[2]};
+  real p[3];
+  mulmtv3(p, R, mc);
+  real sup[ZB_MAX_MESHV], smax = (real)-1e30;
+  for (int i = 0; i < nv; i++) {
+    const real dv[3] = {p[0] - vert[i][0], p[1] - vert[i][1], p[2] - vert[i][2]};
+    sup[i] = dot3(dv, n);
+    if (sup[i] > smax) smax = sup[i];
+  }
+  const real thr = smax - (real)1e-3 > 0 ? smax - (real)1e-3 : (real)0;
+  real dm[ZB_MAX_MESHV];
+  for (int i = 0; i < nv; i++) dm[i] = sup[i] > thr ? (real)0 : (real)-1e6;
+  int ia = 0;
+  for (int i = 1; i < nv; i++)
+    if (dm[i] > dm[ia]) ia = i;
+  const real A[3] = {vert[ia][0], vert[ia][1], vert[ia][2]};
+  int ib = 0;
+  real best = 0;
+  for (int i = 0; i < nv; i++) {
+    const real e0 = A[0] - vert[i][0], e1 = A[1] - vert[i][1], e2 = A[2] - vert[i][2];
+    const real w = (e0 * e0 + e1 * e1 + e2 * e2) + dm[i];
+    if (i == 0 || w > best) { best = w; ib = i; }
+  }
+  const real B[3] = {vert[ib][0], vert[ib][1], vert[ib][2]};
+  real ab[3];
+  {
+    const real amb[3] = {A[0] - B[0], A[1] - B[1], A[2] - B[2]};
+    cross3(ab, n, amb);
+  }
+  int ic = 0;
+  for (int i = 0; i < nv; i++) {
+    const real ap[3] = {A[0] - vert[i][0], A[1] - vert[i][1], A[2] - vert[i][2]};
+    const real w = FABS(dot3(ap, ab)) + dm[i];
+    if (i == 0 || w > best) { best = w; ic = i; }
+  }
+  const real C[3] = {vert[ic][0], vert[ic][1], vert[ic][2]};
+  real ac[3], bc[3];
+  {
+    const real amc[3] = {A[0] - C[0], A[1] - C[1], A[2] - C[2]};
+    const real bmc[3] = {B[0] - C[0], B[1] - C[1], B[2] - C[2]};
+    cross3(ac, n, amc);
+    cross3(bc, n, bmc);
+  }
+  int id = 0;
+  for (int j = 0; j < 2 * nv; j++) {
+    const int i = j < nv ? j : j - nv;
+    const real* o = j < nv ? B : A;
+    const real* ax = j < nv ? bc : ac;
+    const real op[3] = {o[0] - vert[i][0], o[1] - vert[i][1], o[2] - vert[i][2]};
+    const real w = FABS(dot3(op, ax)) + dm[i];
+    if (j == 0 || w > best) { best = w; id = i; }
+  }
+  idx[0] = ia; idx[1] = ib; idx[2] = ic; idx[3] = id;
+  int cnt = 0;
+  for (int q = 0; q < 4; q++) {
+    int uniq = 1;
+    for (int r = 0; r < q; r++)
+      if (idx[r] == idx[q]) uniq = 0;
+    dist[q] = uniq ? -sup[idx[q]] : (real)1;
+    const real v[3] = {vert[idx[q]][0], vert[idx[q]][1], vert[idx[q]][2]};
+    real w[3];
+    mulmv3(w, R, v);
+    for (int k = 0; k < 3; k++) pos[q][k] = c[k] + w[k];
+    if (dist[q] <= margin) cnt++;
+  }
+  return cnt;
+}
+
+/* plane_mesh for the known-answer tests (tests/test_colliders.py): R row-major, verts [nv][4] */
+int zbo_plane_mesh(const float* verts, int nv, const float* R, const float* c, float margin, int* idx, float* dist,
+                   float* pos) {
+  real Rr[9], cr[3], dd[4], pp[4][3];
+  for (int k = 0; k < 9; k++) Rr[k] = R[k];
+  for (int k = 0; k < 3; k++) cr[k] = c[k];
+  if (nv < 1 || nv > ZB_MAX_MESHV) return -1;
+  const int cnt = plane_mesh((const float(*)[4])verts, nv, Rr, cr, margin, idx, dd, pp);
+  for (int q = 0; q < 4; q++) {
+    dist[q] = (float)dd[q];
+    for (int k = 0; k < 3; k++) pos[3 * q + k] = (float)pp[q][k];
+  }
+  return cnt;
+}
+
 static void collision(const ZbModel* m, ZbData* d) {
   static const real ty[3] = {0, 1, 0};
   d->ncon = 0;
@@ -965,6 +1067,12 @@ static void collision(const ZbModel* m, ZbData* d) {
           }
         }
       }
+    } else if (m->geom_type[g] == ZB_GEOM_MESH) {
+      int idx[4];
+      real dist[4], pos[4][3];
+      plane_mesh((const float(*)[4])m->mesh_vert[m->geom_vertadr[g]], m->geom_vertnum[g], R, c, margin, idx, dist, pos);
+      for (int q = 0; q < 4; q++)
+        if (dist[q] <= margin) add_contact(m, d, g, pos[q], dist[q], ty);
     }
   }
   pair_collision(m, d);
@@ -2111,7 +2219,8 @@ static const FieldOff model_fields[] = {
     OFF(ZbModel, body_child), OFF(ZbModel, depth_maxchild), OFF(ZbModel, dof_desc), OFF(ZbModel, dof_ancpk),
     OFF(ZbModel, dof_rowmask), OFF(ZbModel, dof_act), OFF(ZbModel, dof_rowoff), OFF(ZbModel, geom_lastdof),
     OFF(ZbModel, nlevel), OFF(ZbModel, pad_lvl), OFF(ZbModel, level_nmem), OFF(ZbModel, level_mem),
-    OFF(ZbModel, joint_bias), OFF(ZbModel, joint_weight), OFF(ZbModel, pad_end),
+    OFF(ZbModel, joint_bias), OFF(ZbModel, joint_weight), OFF(ZbModel, geom_vertadr), OFF(ZbModel, geom_vertnum),
+    OFF(ZbModel, mesh_vert), OFF(ZbModel, pad_end),
 };
 static const FieldOff config_fields[] = {
     OFF(ZbEnvConfig, struct_bytes), OFF(ZbEnvConfig, flags), OFF(ZbEnvConfig, n_substeps),

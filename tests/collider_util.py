@@ -73,6 +73,103 @@ def cyl_desc() -> dict:
     return _variant(edit)
 
 
+def _jitter(v, seed, amp=0.0004) -> np.ndarray:
+    """Every vertex moved by up to amp per axis (a fixed draw): MJX's manifold selection breaks exact
+    ties (a flat face's parallel edges, a symmetric solid's equal distances) by the rounding of the
+    implementation, which a test against the oracle cannot pin; a generic hull has none."""
+    return np.asarray(v, np.float64) + np.random.default_rng(seed).uniform(-amp, amp, size=np.shape(v))
+
+
+def chamfered_sole(hx=0.045, hy=0.025, hz=0.005) -> np.ndarray:
+    """A sole box (the box sole's size) whose bottom corners are cut, 16 hull vertices (top corners,
+    the side edges' lower ends 3 mm up, the bottom face an octagon with cuts of 3 / 4.5 mm along x
+    and 3.5 / 5 mm along y by side), jittered by up to 0.4 mm."""
+    cx, cy = {-1: 0.003, 1: 0.0045}, {-1: 0.0035, 1: 0.005}
+    v = []
+    for sx in (-1, 1):
+        for sy in (-1, 1):
+            v.append([sx * hx, sy * hy, hz])
+            v.append([sx * hx, sy * hy, -hz + 0.003])
+            v.append([sx * (hx - cx[sx]), sy * hy, -hz])
+            v.append([sx * hx, sy * (hy - cy[sy]), -hz])
+    return _jitter(v, 3)
+
+
+def icosahedron(r=0.022) -> np.ndarray:
+    """The 12 vertices of an icosahedron of circumradius r, flattened 20 % along z."""
+    p = (1 + 5 ** 0.5) / 2
+    v = []
+    for a in (-1, 1):
+        for b in (-p, p):
+            v += [[0, a, b], [a, b, 0], [b, 0, a]]
+    v = np.array(v, np.float64)
+    v = v / np.linalg.norm(v[0]) * r
+    v[:, 2] *= 0.8
+    return _jitter(v, 4)
+
+
+def mesh_desc() -> dict:
+    """Convex mesh colliders (round 5): a chamfered right sole (16 hull vertices, the touch sensor's
+    zone) beside the left box sole, a flattened icosahedron on the right shin and a cube mesh on the
+    left hand (4 colliders; both contact-row banks hold a mesh)."""
+
+    def fmt(v):
+        return " ".join(repr(float(x)) for x in np.asarray(v).ravel())
+
+    def edit(root):
+        asset = ET.SubElement(root, "asset")
+        ET.SubElement(asset, "mesh", name="sole_mesh", vertex=fmt(chamfered_sole()))
+        ET.SubElement(asset, "mesh", name="ico_mesh", vertex=fmt(icosahedron()))
+        cube = _jitter(np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+                       * [0.012, 0.015, 0.02], 5)
+        ET.SubElement(asset, "mesh", name="cube_mesh", vertex=fmt(cube))
+        root.remove(asset)
+        root.insert(1, asset)
+        for g in root.iter("geom"):
+            if g.get("name") == "right_foot_sole":
+                g.set("type", "mesh")
+                g.set("mesh", "sole_mesh")
+                del g.attrib["size"]
+        for b in root.iter("body"):
+            if b.get("name") == "right_knee_pitch_link":
+                b.append(ET.fromstring('<geom name="right_shin" type="mesh" mesh="ico_mesh" pos="0 0 -0.05" '
+                                       'euler="0.2 0 0.1" contype="1" conaffinity="0"/>'))
+            if b.get("name") == "left_gripper_roll_link":
+                b.append(ET.fromstring('<geom name="left_hand" type="mesh" mesh="cube_mesh" pos="0 0 -0.03" '
+                                       'euler="0.3 -0.2 0.5" contype="1" conaffinity="0"/>'))
+
+    return _variant(edit)
+
+
+def plane_convex(c, R, vert) -> list[tuple[np.ndarray, float]]:
+    """MJX's plane_convex with _manifold_points against the floor z = 0 (numpy, float64; the
+    oracle's plane_mesh states the rule): the four manifold points (a, b, c, d) as (vertex in the
+    world, distance), repeats at distance 1."""
+    vert = np.asarray(vert, np.float64)
+    n = R.T @ np.array([0.0, 0.0, 1.0])
+    p = R.T @ (np.zeros(3) - c)
+    support = (p - vert) @ n
+    mask = support > max(0.0, support.max() - 1e-3)
+    dm = np.where(mask, 0.0, -1e6)
+    ia = int(np.argmax(dm))
+    a = vert[ia]
+    ib = int(np.argmax(((a - vert) ** 2).sum(axis=1) + dm))
+    b = vert[ib]
+    ab = np.cross(n, a - b)
+    ap = a - vert
+    ic = int(np.argmax(np.abs(ap @ ab) + dm))
+    cc = vert[ic]
+    ac, bc = np.cross(n, a - cc), np.cross(n, b - cc)
+    dist_bp = np.abs((b - vert) @ bc) + dm
+    dist_ap = np.abs(ap @ ac) + dm
+    idx = [ia, ib, ic, int(np.argmax(np.concatenate([dist_bp, dist_ap])) % len(vert))]
+    out = []
+    for q, i in enumerate(idx):
+        d = -support[i] if i not in idx[:q] else 1.0
+        out.append((c + R @ vert[i], float(d)))
+    return out
+
+
 def _qmat(q) -> np.ndarray:
     w, x, y, z = np.asarray(q, np.float64) / np.linalg.norm(q)
     return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
@@ -91,7 +188,7 @@ def geom_frames(cm, qpos) -> list[tuple[str, np.ndarray, np.ndarray, list[float]
         b = names.index(g["body"])
         c = xpos[b] + xmat[b] @ np.asarray(g.get("pos", [0.0, 0.0, 0.0]))
         R = xmat[b] @ _qmat(g.get("quat", [1.0, 0.0, 0.0, 0.0]))
-        out.append((g.get("type", "box"), c, R, list(g["size"])))
+        out.append((g.get("type", "box"), c, R, list(g["vert"]) if g.get("type") == "mesh" else list(g["size"])))
     return out
 
 
@@ -175,6 +272,8 @@ def contacts(cm, qpos, margin=0.0) -> list[list[tuple[np.ndarray, float]]]:
             p, d = ellipsoid_point(c, R, sz)
             if d <= margin:
                 cons.append((p, d))
+        elif ty == "mesh":
+            cons = [(p, d) for p, d in plane_convex(c, R, sz) if d <= margin]
         else:
             d = c[2] - sz[0]
             if d <= margin:
@@ -198,6 +297,8 @@ def lowest_point(cm, qpos) -> float:
             z = min(z, c[2] - sz[1] * abs(R[2, 2]) - sz[0] * np.sqrt(max(0.0, 1.0 - R[2, 2] ** 2)))
         elif ty == "ellipsoid":
             z = min(z, ellipsoid_point(c, R, sz)[1])
+        elif ty == "mesh":
+            z = min(z, float((c[2] + np.asarray(sz) @ R[2, :]).min()))
         else:
             z = min(z, c[2] - sz[0])
     return float(z)

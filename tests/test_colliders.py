@@ -12,7 +12,7 @@ from zbot_amd import compile_model, default_config
 from zbot_amd import cstructs as cs
 
 
-DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc}
+DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc, "mesh": U.mesh_desc}
 
 
 @pytest.fixture(scope="module", params=list(DESCS))
@@ -33,6 +33,15 @@ def test_variant_models_compile(variant):
         assert list(m.geom_type)[:3] == [cs.GEOM_CAPSULE, cs.GEOM_CAPSULE, cs.GEOM_SPHERE]
         # the touch sensors read the capsule feet
         assert (m.geom_right_foot, m.geom_left_foot) == (0, 1)
+    elif name == "mesh":
+        assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "right_shin", "left_hand"]
+        assert list(m.geom_type)[:4] == [cs.GEOM_MESH, cs.GEOM_BOX, cs.GEOM_MESH, cs.GEOM_MESH]
+        assert [m.geom_vertnum[g] for g in (0, 2, 3)] == [16, 12, 8]
+        assert [m.geom_vertadr[g] for g in (0, 2, 3)] == [0, 16, 28]
+        # the hull's vertices in the mesh's own order (the chamfered sole: every vertex on the hull)
+        np.testing.assert_allclose([list(m.mesh_vert[i])[:3] for i in range(16)], U.chamfered_sole(), rtol=1e-6)
+        # geom_size[0]: a bound on the vertices' distance from the geom origin
+        assert m.geom_size[0][0] >= np.linalg.norm(U.chamfered_sole(), axis=1).max()
     else:
         assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "left_shin", "right_hand"]
         assert list(m.geom_type)[:4] == [cs.GEOM_CYLINDER, cs.GEOM_BOX, cs.GEOM_CYLINDER, cs.GEOM_ELLIPSOID]
@@ -79,6 +88,150 @@ def test_oracle_contact_sets_match_mujoco_rules(variant, oracle_mod, precision):
     assert (touched > 0).all(), touched
 
 
+# ---- convex meshes (MJX plane_convex; oracle plane_mesh, zb_engine.hip contact_point XG 2) ----
+
+def _cube(h=0.01):
+    return np.array([[sx, sy, sz] for sz in (-1, 1) for sy in (-1, 1) for sx in (-1, 1)], np.float64) * h
+
+
+def _rx(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_mesh_flat_cube_is_the_box_bottom(oracle_mod, precision):
+    """A cube mesh lying flat 1 mm into the floor: the manifold of its four bottom corners (all masked,
+    at -1 mm). a the first masked vertex (0), b the farthest from it (3, the diagonal), c the farthest
+    from the line ab (1 and 2 tie: 1); for d, vertices 0 and 2 tie as the farthest from the line bc
+    and the first maximum of the concatenation is vertex 0 itself, a repeat. So an exactly flat square
+    keeps three of its corners (MJX's first-maximum rule on exact ties); the corners kept are the
+    box collider's."""
+    idx, dist, pos, k = oracle_mod.plane_mesh(_cube(), np.eye(3), [0.0, 0.0, 0.009], precision=precision)
+    assert k == 3 and list(idx) == [0, 3, 1, 0]
+    np.testing.assert_allclose(dist, [-0.001] * 3 + [1.0], atol=1e-7)
+    np.testing.assert_allclose(pos[:3, 2], [-0.001] * 3, atol=1e-7)
+    key = lambda p: tuple(round(float(x), 6) for x in p[:2])  # noqa: E731
+    box = {key(U._corner([0.01] * 3, i)) for i, _ in U.box_corners(np.array([0.0, 0.0, 0.009]), np.eye(3), [0.01] * 3)}
+    assert {key(p) for p in pos[:3]} <= box
+    # a quadrilateral prism whose fourth corner (1) lies farther from the line bc than a does: all four
+    # bottom corners
+    quad = np.array([[-0.01, -0.01, -0.01], [0.01, -0.01, -0.01], [-0.006, 0.01, -0.01], [0.01, 0.004, -0.01],
+                     [-0.01, -0.01, 0.01], [0.01, -0.01, 0.01], [-0.006, 0.01, 0.01], [0.006, 0.01, 0.01]])
+    idx, dist, pos, k = oracle_mod.plane_mesh(quad, np.eye(3), [0.0, 0.0, 0.009], precision=precision)
+    assert k == 4 and list(idx) == [0, 3, 2, 1]
+
+
+def test_mesh_edge_and_tip_known_answers(oracle_mod):
+    """A cube rolled 45 degrees about x rests on an edge: two contacts at the edge's ends, the other
+    two slots repeats (distance 1). An octahedron on its tip: one contact. Above the floor: none."""
+    c = np.array([0.0, 0.0, 0.01 * np.sqrt(2) - 0.0005])
+    idx, dist, pos, k = oracle_mod.plane_mesh(_cube(), _rx(np.pi / 4), c)
+    assert k == 2
+    np.testing.assert_allclose(np.sort(dist)[:2], [-0.0005] * 2, atol=1e-9)
+    assert sorted(dist)[2:] == [1.0, 1.0]
+    assert sorted(np.round(pos[dist < 0.5][:, 0], 9)) == [-0.01, 0.01]
+    octa = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float64) * 0.02
+    idx, dist, pos, k = oracle_mod.plane_mesh(octa, np.eye(3), [0.0, 0.0, 0.0195])
+    assert k == 1 and idx[0] == 5 and abs(dist[0] + 0.0005) < 1e-9
+    _, _, _, k = oracle_mod.plane_mesh(octa, np.eye(3), [0.0, 0.0, 0.03])
+    assert k == 0
+
+
+def test_mesh_oracle_matches_numpy_restatement(oracle_mod):
+    """200 random hulls (8-40 points on a squashed sphere) at random poses near the floor: the f64
+    oracle's manifold equals collider_util.plane_convex's (indices, distances, points), and the f32
+    oracle's contact count agrees wherever no vertex sits within 1e-5 of a threshold."""
+    from zbot_amd.mjcf import hull_vertices
+
+    rng = np.random.default_rng(7)
+    agree = 0
+    for t in range(200):
+        p = rng.normal(size=(rng.integers(8, 41), 3))
+        p = p / np.linalg.norm(p, axis=1, keepdims=True) * [0.03, 0.02, 0.01]
+        v, _ = hull_vertices(p)
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        R = U._qmat(q)
+        c = np.array([0.0, 0.0, -float((v @ R[2, :]).min()) - rng.uniform(0, 0.003)])
+        ref = U.plane_convex(c, R, v)
+        idx, dist, pos, k = oracle_mod.plane_mesh(v, R, c)
+        # the contacts (repeats, at distance 1, may differ in which vertex they repeat when two
+        # candidates tie to rounding)
+        got = sorted((round(float(d), 7), *np.round(p, 7)) for p, d in zip(pos, dist) if d <= 0)
+        want = sorted((round(float(d), 7), *np.round(p, 7)) for p, d in ref if d <= 0)
+        assert k == len(want) == len(got), t
+        np.testing.assert_allclose(np.array(got, float).reshape(-1, 4), np.array(want, float).reshape(-1, 4), atol=2e-7)
+        z = c[2] + v @ R[2, :]
+        near = np.abs(z - z.min() - 1e-3).min() < 1e-5 or np.abs(z).min() < 1e-5
+        _, _, _, k32 = oracle_mod.plane_mesh(v, R, c, precision="f32")
+        if not near:
+            assert k32 == k, t
+            agree += 1
+    assert agree > 150
+
+
+def test_mesh_hull_and_files(tmp_path):
+    """hull_vertices keeps the hull's vertices in input order (interior points dropped); STL (binary
+    and ASCII) and OBJ files read back the same distinct vertices in first-appearance order; an MJCF
+    <mesh file> with scale compiles to those vertices."""
+    import struct
+
+    from zbot_amd.mjcf import hull_vertices, load_mjcf, read_mesh_file, to_mjcf
+
+    cube = _cube(0.01)
+    pts = np.vstack([cube[:3], [[0.0, 0.0, 0.0]], cube[3:]])
+    v, tri = hull_vertices(pts)
+    np.testing.assert_array_equal(v, cube)
+    assert tri.shape == (12, 3)
+    faces = [(0, 1, 3), (0, 3, 2), (4, 6, 7), (4, 7, 5), (0, 4, 5), (0, 5, 1), (2, 3, 7), (2, 7, 6),
+             (0, 2, 6), (0, 6, 4), (1, 5, 7), (1, 7, 3)]
+    with open(tmp_path / "c.stl", "wb") as f:
+        f.write(b"\0" * 80 + struct.pack("<I", len(faces)))
+        for fa in faces:
+            f.write(struct.pack("<3f", 0, 0, 0) + b"".join(struct.pack("<3f", *cube[i]) for i in fa) + b"\0\0")
+    with open(tmp_path / "a.stl", "w") as f:
+        f.write("solid c\n" + "".join("facet normal 0 0 0\nouter loop\n" + "".join(
+            f"vertex {float(cube[i][0])!r} {float(cube[i][1])!r} {float(cube[i][2])!r}\n" for i in fa) + "endloop\nendfacet\n"
+            for fa in faces) + "endsolid c\n")
+    with open(tmp_path / "c.obj", "w") as f:
+        f.write("".join(f"v {float(x)!r} {float(y)!r} {float(z)!r}\n" for x, y, z in cube) + "".join(
+            f"f {a + 1} {b + 1} {c + 1}\n" for a, b, c in faces))
+    order = [tuple(cube[i]) for i in dict.fromkeys(i for fa in faces for i in fa)]
+    for name in ("c.stl", "a.stl"):
+        got = read_mesh_file(str(tmp_path / name))
+        np.testing.assert_allclose(got, np.array(order), rtol=1e-6)
+    np.testing.assert_allclose(read_mesh_file(str(tmp_path / "c.obj")), cube)
+    text = to_mjcf(U.mesh_desc()).replace('<compiler angle="radian"/>',
+                                         f'<compiler angle="radian" meshdir="{tmp_path}"/>')
+    text = text.replace('<mesh name="left_hand_mesh" vertex=', '<mesh name="left_hand_mesh" file="c.obj" scale="1.2 1.5 2" x=')
+    d = load_mjcf(text)
+    hand = next(g for g in d["geoms"] if g["name"] == "left_hand")
+    np.testing.assert_allclose(hand["vert"], cube * [1.2, 1.5, 2.0])
+
+
+def test_mesh_model_round_trips_and_refusals():
+    """to_mjcf writes a mesh model back (hull vertices inline) and it compiles to the same bytes; a
+    hull of more than 64 vertices is listed as skipped (zb_create refuses it) and compile_model
+    rejects a mesh without vertices."""
+    from zbot_amd.mjcf import load_mjcf, to_mjcf
+
+    d = U.mesh_desc()
+    assert bytes(compile_model(load_mjcf(to_mjcf(d))).cmodel) == bytes(compile_model(d).cmodel)
+    rng = np.random.default_rng(1)
+    sph = rng.normal(size=(200, 3))
+    sph = sph / np.linalg.norm(sph, axis=1, keepdims=True) * 0.02
+    text = to_mjcf(d).replace('<mesh name="left_hand_mesh" vertex="',
+                              '<mesh name="left_hand_mesh" vertex="' + " ".join(repr(float(x)) for x in sph.ravel()) + " ")
+    d2 = load_mjcf(text)
+    assert any(g["name"] == "left_hand" and g["hull_vertices"] > 64 for g in d2["skipped_geoms"])
+    assert compile_model(d2).cmodel.nskip_geom == 1
+    bad = U.mesh_desc()
+    next(g for g in bad["geoms"] if g["type"] == "mesh")["vert"] = []
+    with pytest.raises(ValueError):
+        compile_model(bad)
+
+
 def test_tilted_box_keeps_mujocos_corners():
     """A known answer for the box rule: a 0.02 x 0.02 x 0.02 cube rolled 30 degrees about x, centre
     at height h. A corner's offset along z is y sin30 + z cos30 (y, z = +-0.01): below the centre are
@@ -118,6 +271,20 @@ def test_cyl_asset_is_the_test_variant():
     with open(path) as f:
         assert f.read() == to_mjcf(U.cyl_desc()) + "\n"
     assert bytes(compile_model(load_mjcf(path)).cmodel) == bytes(compile_model(U.cyl_desc()).cmodel)
+
+
+def test_mesh_asset_is_the_test_variant():
+    """assets/zbot_like_mesh.xml (bench.py's mesh_colliders leg) is collider_util.mesh_desc written
+    out (hull vertices inline)."""
+    import os
+
+    from zbot_amd.mjcf import load_mjcf, to_mjcf
+    from zbot_amd.model import DEFAULT_ASSET
+
+    path = os.path.join(os.path.dirname(DEFAULT_ASSET), "zbot_like_mesh.xml")
+    with open(path) as f:
+        assert f.read() == to_mjcf(U.mesh_desc()) + "\n"
+    assert bytes(compile_model(load_mjcf(path)).cmodel) == bytes(compile_model(U.mesh_desc()).cmodel)
 
 
 def test_cylinder_known_answers():

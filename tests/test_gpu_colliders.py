@@ -23,7 +23,7 @@ def torch_gpu():
     return torch
 
 
-DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc}
+DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc, "mesh": U.mesh_desc}
 
 
 @pytest.fixture(scope="module", params=list(DESCS))
@@ -212,7 +212,11 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
     # NO_FP64_SLACK: each fp32 implementation picks its contact triangle from its own rounding, and
     # on MI355X a few envs part from the fp32 oracle from the fifth step (r04 v21: rewards within
     # 2.4e-6 over steps 0-3, then 1-4 of 64 envs beyond the bound), so its window is 4 steps
-    for t in range(4 if name in NO_FP64_SLACK else 8):
+    # the mesh variant: MJX's manifold rule reselects all four points when a vertex enters or leaves
+    # the penetrating set, so one rounding-level difference at such a crossing moves the whole contact
+    # set; on MI355X (r05) rewards held 7.5e-7 over steps 0-3, then 1-2 of 64 envs left the bound per
+    # step (the fp32 / fp64 oracles themselves part at 1 env of 64 in 8 steps), so its window is 4 steps
+    for t in range(4 if name in NO_FP64_SLACK or name == "mesh" else 8):
         err.add(f"reward[{t}]", rew[t], g["reward"][t], GOLDEN_TOL["reward"],
                 ref64=None if name in NO_FP64_SLACK else r64s[t])
     print(f"\n[colliders {name} rollout] steps with a contact per collider (every 4th env): "

@@ -394,9 +394,9 @@ def test_colliders_are_parsed_and_unsupported_ones_reported():
                   "<geom name='hand' type='sphere' size='0.02' pos='0.1 0 0'/>"
                   "<geom name='cyl' type='cylinder' size='0.01 0.05 0.3'/>"
                   "<geom name='ell' type='ellipsoid' size='0.01 0.02 0.03' fromto='0 0 0 0 0 -0.1'/>"
-                  "<geom name='foot' type='mesh' mesh='m'/>"
-                  "<geom name='vis' type='mesh' mesh='m' contype='0' conaffinity='0'/></body></worldbody></mujoco>")
-    assert b["skipped_geoms"] == [{"name": "foot", "body": "b", "type": "mesh"}]
+                  "<geom name='foot' type='hfield' hfield='m'/>"
+                  "<geom name='vis' type='hfield' hfield='m' contype='0' conaffinity='0'/></body></worldbody></mujoco>")
+    assert b["skipped_geoms"] == [{"name": "foot", "body": "b", "type": "hfield"}]
     shin, hand, cyl, ell = b["geoms"]
     # an ellipsoid with fromto: the two semi-axes across, the segment's half-length along
     np.testing.assert_allclose(ell["size"], [0.01, 0.02, 0.05])
@@ -442,7 +442,7 @@ def test_missing_file_is_reported():
 
 
 def test_skipped_colliders_are_rejected_by_zb_create():
-    """A collider the engine has no floor contact for (a mesh here; or a fifth collider) is not
+    """A collider the engine has no floor contact for (a height field here; or a fifth collider) is not
     dropped silently: zb_create rejects the model (ZB_EMODEL, nskip_geom); compile_model(...,
     drop_colliders=True) drops it knowingly (missing item 3). Supported extra colliders
     (a capsule or, since round 4, a cylinder or an ellipsoid shin) pass validation."""
@@ -457,7 +457,7 @@ def test_skipped_colliders_are_rejected_by_zb_create():
         for b in root.iter("body"):
             if "knee" in b.get("name"):
                 shape = ('size="0.015 0.02 0.04" pos="0 0 -0.04"' if gtype == "ellipsoid"
-                         else 'mesh="shin"' if gtype == "mesh" else 'size="0.015" fromto="0 0 0 0 0 -0.08"')
+                         else 'hfield="shin"' if gtype == "hfield" else 'size="0.015" fromto="0 0 0 0 0 -0.08"')
                 b.append(ET.fromstring(f'<geom name="shin_col" type="{gtype}" {shape} mass="0" contype="1" '
                                        'conaffinity="0"/>'))
                 break
@@ -465,7 +465,7 @@ def test_skipped_colliders_are_rejected_by_zb_create():
 
     L = E.load_library()
     h = C.c_void_p()
-    desc = with_shin("mesh")
+    desc = with_shin("hfield")
     assert [g["name"] for g in desc["skipped_geoms"]] == ["shin_col"]
     cm = compile_model(desc)
     assert cm.cmodel.nskip_geom == 1
