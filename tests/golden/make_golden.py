@@ -37,14 +37,26 @@ CASES = {
     "c2_eulerdamp_seed5": dict(n=16, steps=16, seed=5, push=False, randomize=False, std=0.05, eulerdamp=True),
     "c5_cg_eulerdamp_seed6": dict(n=16, steps=16, seed=6, push=True, randomize=True, std=0.1, solver="cg",
                                   eulerdamp=True),
+    # round 5: the convex-mesh collider model (assets/zbot_like_mesh.xml; CPU regression pin of the
+    # oracle's plane_mesh through a rollout with pushes: the GPU side is tests/test_gpu_colliders.py)
+    "mesh_32x24_seed7": dict(n=32, steps=24, seed=7, push=True, randomize=False, std=0.2, model="zbot_like_mesh.xml"),
 }
+
+
+def case_model(model=None):
+    """The compiled model of a case: the default descriptor, or an MJCF asset of the package."""
+    if model is None:
+        return compile_model()
+    from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
+
+    return compile_model(load_mjcf(os.path.join(ROOT, "ksim-gym-zbot_amd", "assets", str(model))))
 
 
 EXACT_STEPS = 16  # tests/test_gpu_parity.py GOLDEN_EXACT_STEPS: the per-env state is also kept at this step
 
 
-def run_case(name, n, steps, seed, push, randomize, std, solver="newton", eulerdamp=False):
-    cm = compile_model()
+def run_case(name, n, steps, seed, push, randomize, std, solver="newton", eulerdamp=False, model=None):
+    cm = case_model(model)
     cfg = default_config(push=push, randomize=randomize, solver=solver, eulerdamp=eulerdamp)
     env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
     oa0, oc0, _ = env.reset()
