@@ -814,6 +814,12 @@ def main(argv: list | None = None) -> None:
             "the sole-pair model (the soles also collide with each other, box-box; the XG 3 kernels, DESIGN.md §4l)",
             "r03_flops_count.json" if args.solver == "newton" else "r03_flops_count_cg.json", n, args.steps,
             args.warmup, dev, rank, world, args.seed, G)
+        extra_legs["mjx_box_rule"] = bench_variant(
+            compile_model(box_rule="mjx"), default_config(solver=args.solver),
+            "the box soles collided by MJX's plane_convex manifold (compile_model(box_rule='mjx'): each an 8-corner "
+            "convex mesh, the XG 2 kernels, DESIGN.md §8)",
+            "r05_flops_count_mjxbox.json" if args.solver == "newton" else "r05_flops_count_cg_mjxbox.json", n,
+            args.steps, args.warmup, dev, rank, world, args.seed, G)
         extra_legs["eulerdamp"] = bench_variant(
             cm, default_config(solver=args.solver, eulerdamp=True),
             f"mj_Euler's implicit joint damping (ZB_F_EULERDAMP), {args.solver} solver",

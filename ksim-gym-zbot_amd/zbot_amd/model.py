@@ -193,8 +193,14 @@ def load_description(path: str | None = None) -> dict:
         return json.load(f)
 
 
+def mjx_box_vertices(size) -> list[list[float]]:
+    """A box as MJX collides it with a plane: a convex mesh of its 8 corners in
+    itertools.product((-1, 1), repeat=3) order (x slowest) [U: mjx/_src/mesh.py box()]."""
+    return [[sx * size[0], sy * size[1], sz * size[2]] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]
+
+
 def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
-                  drop_self_contacts: bool = False) -> CompiledModel:
+                  drop_self_contacts: bool = False, box_rule: str = "mujoco") -> CompiledModel:
     """Compile a JSON robot description into a ZbModel (+ host float64 view).
 
     A description from zbot_amd.mjcf.load_mjcf lists the source's colliding geoms the engine does
@@ -204,9 +210,21 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
     compiles it without them, knowingly (nskip_geom 0). Likewise desc["self_pairs"], the robot's
     own geom pairs the source model collides (the engine has floor contacts only), are counted
     into ZbModel.nskip_pair and refused by zb_create; drop_self_contacts=True compiles the model
-    without them (nskip_pair 0)."""
+    without them (nskip_pair 0).
+
+    box_rule [U: which plane-box rule the reference's MJX uses; DESIGN.md §8]: "mujoco" (default)
+    collides boxes by MuJoCo's mjc_PlaneBox (the corners below the centre within the margin);
+    "mjx" compiles every box collider as the convex mesh of its 8 corners (mjx_box_vertices), so
+    the engine collides it by MJX's plane_convex manifold (the mesh collider, XG 2 kernels). The
+    sole pair (box-box) exists only under "mujoco"."""
     if desc is None or isinstance(desc, str):
         desc = load_description(desc)
+    if box_rule not in ("mujoco", "mjx"):
+        raise ValueError(f"box_rule {box_rule!r}: 'mujoco' or 'mjx'")
+    if box_rule == "mjx":
+        desc = dict(desc)
+        desc["geoms"] = [dict({k: v for k, v in g.items() if k != "size"}, type="mesh", vert=mjx_box_vertices(g["size"]))
+                         if g.get("type", "box") == "box" else g for g in desc.get("geoms", [])]
 
     # ---- bodies -----------------------------------------------------------
     bodies: list[Body] = [Body("world", -1, np.zeros(3), np.array([1.0, 0, 0, 0]), 0.0, np.zeros(3), np.zeros(3))]
@@ -341,7 +359,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
         zmin = math.inf
         for g in geoms:
             bi = names[g["body"]]
-            size = np.array(g["size"])
+            size = np.array(g.get("size", [0.0]))
             gpos = xpos[bi] + xmat[bi] @ np.array(g.get("pos", [0, 0, 0]))
             gmat = xmat[bi] @ quat_to_mat(np.array(g.get("quat", [1.0, 0, 0, 0])))
             gt = g.get("type", "box")
@@ -354,6 +372,8 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
             elif gt == "capsule":
                 for sg in (-1, 1):
                     zmin = min(zmin, gpos[2] + sg * size[1] * gmat[2, 2] - size[0])
+            elif gt == "mesh":
+                zmin = min(zmin, float((gpos[2] + np.asarray(g["vert"], np.float64) @ gmat[2, :]).min()))
             else:
                 zmin = min(zmin, gpos[2] - size[0])
         qpos0[2] = -zmin + float(desc.get("base_clearance", 0.0))

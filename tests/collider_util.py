@@ -141,6 +141,17 @@ def mesh_desc() -> dict:
     return _variant(edit)
 
 
+def mjx_box_desc() -> dict:
+    """The default robot with its box soles collided as MJX does (compile_model(box_rule="mjx"): each
+    box a convex mesh of its 8 corners, MJX's plane_convex manifold), as a descriptor."""
+    from zbot_amd.model import load_description, mjx_box_vertices
+
+    d = load_description()
+    d["geoms"] = [dict({k: v for k, v in g.items() if k != "size"}, type="mesh", vert=mjx_box_vertices(g["size"]))
+                  for g in d["geoms"]]
+    return d
+
+
 def plane_convex(c, R, vert) -> list[tuple[np.ndarray, float]]:
     """MJX's plane_convex with _manifold_points against the floor z = 0 (numpy, float64; the
     oracle's plane_mesh states the rule): the four manifold points (a, b, c, d) as (vertex in the

@@ -12,7 +12,7 @@ from zbot_amd import compile_model, default_config
 from zbot_amd import cstructs as cs
 
 
-DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc, "mesh": U.mesh_desc}
+DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc, "mesh": U.mesh_desc, "mjxbox": U.mjx_box_desc}
 
 
 @pytest.fixture(scope="module", params=list(DESCS))
@@ -33,6 +33,13 @@ def test_variant_models_compile(variant):
         assert list(m.geom_type)[:3] == [cs.GEOM_CAPSULE, cs.GEOM_CAPSULE, cs.GEOM_SPHERE]
         # the touch sensors read the capsule feet
         assert (m.geom_right_foot, m.geom_left_foot) == (0, 1)
+    elif name == "mjxbox":
+        assert list(m.geom_type)[:2] == [cs.GEOM_MESH, cs.GEOM_MESH] and m.npair == 0
+        # the corners in itertools.product((-1, 1), repeat=3) order: x slowest, z fastest
+        np.testing.assert_allclose([list(m.mesh_vert[i])[:3] for i in range(8)],
+                                   [[sx * 0.045, sy * 0.025, sz * 0.005] for sx in (-1, 1) for sy in (-1, 1)
+                                    for sz in (-1, 1)], rtol=1e-6)
+        assert bytes(m) == bytes(compile_model(None, box_rule="mjx").cmodel)
     elif name == "mesh":
         assert cm.geom_names == ["right_foot_sole", "left_foot_sole", "right_shin", "left_hand"]
         assert list(m.geom_type)[:4] == [cs.GEOM_MESH, cs.GEOM_BOX, cs.GEOM_MESH, cs.GEOM_MESH]

@@ -23,7 +23,7 @@ def torch_gpu():
     return torch
 
 
-DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc, "mesh": U.mesh_desc}
+DESCS = {"limbs": U.limbs_desc, "round": U.round_desc, "cyl": U.cyl_desc, "mesh": U.mesh_desc, "mjxbox": U.mjx_box_desc}
 
 
 @pytest.fixture(scope="module", params=list(DESCS))
@@ -105,6 +105,14 @@ COLLIDER_TOL_CG = {
 # within the same bounds (r04 v17 measured qpos 3.0e-7, qvel 5.3e-6 with Newton; qpos 3.1e-6,
 # qvel 2.3e-4 with CG).
 NO_FP64_SLACK = {"cyl"}
+# The box soles collided by MJX's plane_convex manifold (compile_model(box_rule="mjx")) stand exactly
+# flat at reset, where the rule's first-maximum tie-breaks between corners at equal distances decide
+# which corners carry the robot: the fp32 and fp64 oracles part in 60-64 of 64 envs over the first
+# steps of the rollout below and agree again once the robots have left the flat pose (about 1 env
+# from the eleventh step; profiles/r05_mjxbox_oracle_gap.txt). Any fp32 implementation, MJX's
+# included, picks its corners from its own rounding there, so that rollout is held to the ensemble
+# contract alone; the one-step tests from touching states (no flat face) keep the full contract.
+ENSEMBLE_ONLY = {"mjxbox"}
 
 
 @pytest.mark.parametrize("solver", ["newton", "cg"])
@@ -119,9 +127,11 @@ def test_one_step_matches_oracle(torch_gpu, variant, oracle_mod, solver):
     n = 64
     env = contact_env(oracle_mod, cm, cfg, n, seed=11)
     eng = HipEngine(cm, cfg, n, seed=11)
-    err = MaxErr(f"colliders {name} {solver} one-step")
+    err = MaxErr(f"colliders {name} {solver} one-step", exempt_ill=name in ENSEMBLE_ONLY)
     tols = COLLIDER_TOL_CG if solver == "cg" else COLLIDER_TOL
-    for t in range(2):
+    # the second step starts from the oracle's first, where the lying robots (56 of 64) have been
+    # reset onto flat soles: for ENSEMBLE_ONLY variants that is the flat-face tie of their rollouts
+    for t in range(1 if name in ENSEMBLE_ONLY else 2):
         eng.set_state(torch.from_numpy(env.state.copy()))
         eng.set_rand(torch.from_numpy(env.rand.copy()))
         a = oracle_mod.synthetic_actions(cm.cmodel, 11, n, 0, t)
@@ -206,6 +216,11 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
         rew.append(o["reward"].cpu().numpy().copy())
         done.append(o["done"].cpu().numpy().copy())
     rew, done = np.stack(rew), np.stack(done)
+    if name in ENSEMBLE_ONLY:
+        print(f"\n[colliders {name} rollout] steps with a contact per collider (every 4th env): "
+              + ", ".join(f"{names[k]} {int(extra[k])}" for k in range(len(names))))
+        golden_ensemble_check(f"colliders {name}", rew, done, eng.get_state().cpu().numpy(), g)
+        return
     np.testing.assert_array_equal(done[:GOLDEN_EXACT_STEPS], g["done"][:GOLDEN_EXACT_STEPS])
     err = MaxErr(f"colliders {name} rollout from reset")
     # the cyl variant's cylinder foot stands exactly upright at reset, the flat-disk discontinuity of

@@ -68,8 +68,13 @@ class MaxErr:
     lands further away (that env: 2.8x the qpos bound, 6.3x the planner bound); the budget admits
     one such env per output and step, within 10x the bound."""
 
-    def __init__(self, name, budget=1, loose=10.0, max_ill=3):
+    def __init__(self, name, budget=1, loose=10.0, max_ill=3, exempt_ill=False):
         self.name, self.err, self.bad, self.err_well = name, {}, [], {}
+        # exempt_ill: an env at a discontinuity is not bounded at all (still at most max_ill of them):
+        # for a contact rule whose tie-breaks pick among equally valid branches by rounding (MJX's
+        # manifold on a flat face, tests/test_gpu_colliders.py ENSEMBLE_ONLY), a third fp32
+        # implementation may take a branch neither oracle took
+        self.exempt_ill = exempt_ill
         self.budget, self.loose, self.nout = budget, loose, {}
         # envs per output and step that may take the discontinuity slack (measured 0-3 of 64 in r03)
         self.max_ill = max_ill
@@ -90,6 +95,8 @@ class MaxErr:
             gap = np.abs(ref - np.asarray(ref64, np.float64))
             slack = 2.0 * gap.reshape(gap.shape[0], -1).max(1).reshape((-1,) + (1,) * (gap.ndim - 1))
             ill = np.asarray(slack).reshape(-1) > tol
+            if self.exempt_ill:
+                slack = np.where(ill.reshape(slack.shape), np.inf, slack)
             self.ill = max(getattr(self, "ill", 0), int(ill.sum()))
             if int(ill.sum()) > self.max_ill:
                 self.bad.append(f"{key}: {int(ill.sum())} envs at a discontinuity (fp32 / fp64 oracles disagree by "
