@@ -361,6 +361,10 @@ template <bool B>
 struct BoolC {
   static constexpr bool value = B;
 };
+template <int N>
+struct IntC {
+  static constexpr int value = N;
+};
 
 /* Diagnostic phase stamps (separate build, -DZB_STAMPS): cycles per phase of the
    step, accumulated per env; never compiled into the product library. */
@@ -1653,7 +1657,9 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
       const float n[3] = {R20, R21, R22}; /* the plane normal in the geom frame, R' e_z */
       const float pp[3] = {-(R00 * c0 + R10 * c1 + R20 * c2), -(R01 * c0 + R11 * c1 + R21 * c2),
                            -(R02 * c0 + R12 * c1 + R22 * c2)}; /* the plane's origin, R' (0 - c) */
-      constexpr int NJ = ZB_MAX_MESHV / 16;
+      /* NJ vertices per lane: one for a hull of at most 16 (a box's 8 corners), four otherwise */
+      auto manifold = [&](auto njc) {
+      constexpr int NJ = decltype(njc)::value;
       float v[NJ][3], sup[NJ], dm[NJ];
       bool ok[NJ];
       float smax = -3.0e38f;
@@ -1744,6 +1750,9 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
       p[2] = c2 + (R20 * V[0] + R21 * V[1] + R22 * V[2]);
       dist = uniq ? -sq : 1.f;
       slot_ok = true;
+      };
+      if (nvt <= 16) manifold(IntC<1>{});
+      else manifold(IntC<ZB_MAX_MESHV / 16>{});
     } else if (cyl) {
       /* mjc_PlaneCylinder (oracle collision()): the axis a (R's z column) turned toward the plane,
          v the radius vector in the disk planes toward it; slot 0 the near disk's deepest point

@@ -22,13 +22,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--groups", type=int, default=1, help="env groups on their own streams (EnvGroups)")
     ap.add_argument("--model", default=None, help="an MJCF file (e.g. the limbs asset) instead of the default model")
+    ap.add_argument("--box-rule", default="mujoco", choices=["mujoco", "mjx"], help="compile_model(box_rule=...)")
     a = ap.parse_args()
     if a.model:
         from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
 
-        cm = compile_model(load_mjcf(a.model))
+        cm = compile_model(load_mjcf(a.model), box_rule=a.box_rule)
     else:
-        cm = compile_model()
+        cm = compile_model(box_rule=a.box_rule)
     bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
     acts = [bias + 0.05 * torch.randn(a.n, 20, device="cuda") for _ in range(8)]
     if a.groups > 1:
