@@ -98,10 +98,12 @@ def test_default_chunking(torch_gpu, cmodel, n, push, steps):
     assert same(torch, ref.get_stats(), auto.get_stats())
 
 
-def test_chunked_step_bit_exact_general_colliders(torch_gpu, oracle_mod):
+@pytest.mark.parametrize("variant", ["limbs", "mesh"])
+def test_chunked_step_bit_exact_general_colliders(torch_gpu, oracle_mod, variant):
     """The general-collider kernels (a shin box and a hand capsule beside the soles, DESIGN.md
-    §4j) chunked against unchunked, from states where those colliders touch the floor, so that the
-    second contact bank and its global-scratch rows are in use across the hand-offs."""
+    §4j; or the convex mesh sole, shin and hand, round 5) chunked against unchunked, from states where
+    those colliders touch the floor, so that the second contact bank and its global-scratch rows are
+    in use across the hand-offs."""
     torch = torch_gpu
     import numpy as np
 
@@ -109,7 +111,7 @@ def test_chunked_step_bit_exact_general_colliders(torch_gpu, oracle_mod):
     from zbot_amd import compile_model
     from zbot_amd import cstructs as cs
 
-    cm = compile_model(U.limbs_desc())
+    cm = compile_model(getattr(U, f"{variant}_desc")())
     cfg = default_config(push=True, randomize=True)
     n = 37
     ref, chk = make(cm, cfg, n, 1), make(cm, cfg, n, 5)
