@@ -368,7 +368,8 @@ def bench_general_colliders(cfg, n: int, steps: int, warmup: int, dev, rank: int
     the floor besides the soles), which runs the general-collider kernel instantiation (DESIGN.md
     §4j); same groups and actions as the headline. asset="zbot_like_cyl.xml": the cylinder foot,
     cylinder shin and ellipsoid hand model (the third instantiation); "zbot_like_mesh.xml": the convex
-    mesh right sole, shin and hand (the same instantiation, MJX's plane_convex, §4j)."""
+    mesh right sole, shin and hand (the same instantiation, MJX's plane_convex, §4j); "zbot_like_many.xml":
+    nine colliders, the second bank chosen per substep (§4j)."""
     from zbot_amd import compile_model  # noqa: PLC0415
     from zbot_amd.engine import EnvGroups, HipEngine  # noqa: PLC0415
     from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
@@ -687,7 +688,7 @@ def main(argv: list | None = None) -> None:
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the ksim_env (ZbotWalkingEnv.step), train_defaults (512 x 200), c1_gpu, "
                          "general_colliders (limbs model), cylinder_colliders (cyl model), mesh_colliders (mesh "
-                         "model), the other solver's "
+                         "model), many_colliders (nine colliders), the other solver's "
                          "(cg_solver / newton_solver), sole_pair and eulerdamp legs")
     ap.add_argument("--inloop-critic", type=int, default=0,
                     help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
@@ -799,6 +800,8 @@ def main(argv: list | None = None) -> None:
                                                                    args.seed, G, "zbot_like_cyl.xml")
         extra_legs["mesh_colliders"] = bench_general_colliders(cfg, n, args.steps, args.warmup, dev, rank, world,
                                                                args.seed, G, "zbot_like_mesh.xml")
+        extra_legs["many_colliders"] = bench_general_colliders(cfg, n, args.steps, args.warmup, dev, rank, world,
+                                                               args.seed, G, "zbot_like_many.xml")
         # the [U] physics switches timed both ways: the other solver, and implicit damping
         other = "cg" if args.solver == "newton" else "newton"
         extra_legs[f"{other}_solver"] = bench_variant(

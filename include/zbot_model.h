@@ -14,7 +14,7 @@
  *   - a kinematic tree with at most one joint per body; joint types: free
  *     (root only) or hinge; other bodies are welded (no joint);
  *   - nbody <= ZB_MAX_BODY, nv <= ZB_MAX_DOF, dof-chain depth <= ZB_MAX_DEPTH;
- *   - collision = floor plane (world geom) vs up to ZB_MAX_GEOM per-body boxes,
+ *   - collision = floor plane (world geom) vs up to ZB_MAX_GEOM = 16 per-body boxes,
  *     capsules, cylinders, spheres, ellipsoids or convex meshes (<= ZB_MAX_MESHV hull
  *     vertices each; the two foot soles first by
  *     convention); of the robot's own pairs only the two box soles against each
@@ -33,15 +33,16 @@ extern "C" {
 #endif
 
 #define ZB_MODEL_MAGIC   0x5A424F54u /* 'ZBOT' */
-#define ZB_MODEL_VERSION 8
+#define ZB_MODEL_VERSION 9
 
 #define ZB_MAX_BODY  32
 #define ZB_MAX_DOF   32
 #define ZB_MAX_QPOS  40
 #define ZB_MAX_DEPTH 12
-#define ZB_MAX_GEOM  4   /* floor colliders */
+#define ZB_MAX_GEOM  16  /* floor colliders (model v9; the engine collides the two soles and, per substep,
+                            the first two others within reach of the floor: DESIGN.md §4j) */
 #define ZB_MAX_MESHV 64  /* convex hull vertices of one mesh collider */
-#define ZB_MAX_MESHVERT (ZB_MAX_GEOM * ZB_MAX_MESHV)
+#define ZB_MAX_MESHVERT 512 /* the mesh vertex pool (all mesh colliders together) */
 #define ZB_MAX_SITE  8
 #define ZB_MAX_ACT   32
 #define ZB_CON_PER_GEOM 4 /* plane-box at most 4 corners, plane-cylinder 4, plane-mesh 4, plane-capsule 2, plane-sphere / -ellipsoid 1 */

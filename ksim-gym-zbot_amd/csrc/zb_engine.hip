@@ -74,6 +74,9 @@ struct EnvS {
   uint32_t env, seed_lo, seed_hi;
   /* XG kernels: the env's block of second-bank Jacobian rows in global scratch (xrows) */
   uint32_t xj_lo, xj_hi;
+  /* XG 1 / 2: the geoms in the second contact-row bank this substep (half 0, half 1; -1: none):
+     the first two of geoms 2.. within reach of the floor (select_bank2) */
+  int32_t xsel[2];
 };
 struct Sensors {
   float fq[4], gyro[3], acc[3], touch[2], force[6];
@@ -667,6 +670,7 @@ struct XRow {
   bool any; /* wave-uniform: some row of the bank exists in either env of the wave */
   bool ex;
   int chd; int kdep;
+  uint32_t rowmask; /* XG 1 / 2: the bank's rows whose chain holds dof l (its geoms change per substep) */
   float aref, D, jar, Jv, f;
   int act;
   int nrow;
@@ -1587,6 +1591,14 @@ template <int XG>
 __device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& gb) {
   MP m = c.m;
   const int gl = c.l >> 4;
+  if (XFLOOR<XG> && bank == 1) {
+    /* the second bank's geoms of this substep (select_bank2) */
+    const int sg = c.L->s.xsel[gl];
+    const bool sv = sg >= 0;
+    g = sv ? sg : 0;
+    gb = sv ? m->geom_body[g] : 0;
+    return sv;
+  }
   g = XFLOOR<XG> ? 2 * bank + gl : gl;
   const bool gvalid = XFLOOR<XG> ? g < m->ngeom : gl < NGEOM;
   if (!gvalid) g = 0;
@@ -1870,27 +1882,12 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   r.Jv = 0.f;
   r.D = 0.f;
   r.aref = 0.f;
-  if (XFLOOR<XG> && bank == 1) {
-    /* the second bank (shins, hands: usually off the floor) first by a bound: no point of a geom
-       lies lower than its body's origin minus |geom_pos| minus the geom's bounding radius (box: the
-       half-diagonal; capsule: radius + half-length; cylinder: the rim's distance from the centre,
-       sqrt(r^2 + h^2); ellipsoid: the largest semi-axis; sphere: the radius). While no lane of the
-       wave can reach the margin (+1 mm against rounding), the bank has no row: the same state as
-       the full test below finds, without its shuffles and rotations */
-    const float zb = tsh(B.xp[2], gb);
-    const float gx = m->geom_pos[g][0], gy = m->geom_pos[g][1], gz = m->geom_pos[g][2];
-    const float s0 = m->geom_size[g][0], s1 = m->geom_size[g][1], s2 = m->geom_size[g][2];
-    const int ty = m->geom_type[g];
-    const float rb = ty == ZB_GEOM_BOX ? sqrtf(s0 * s0 + s1 * s1 + s2 * s2)
-                     : ty == ZB_GEOM_CAPSULE ? s0 + s1
-                     : ty == ZB_GEOM_CYLINDER ? sqrtf(s0 * s0 + s1 * s1)
-                     : ty == ZB_GEOM_ELLIPSOID ? fmaxf(s0, fmaxf(s1, s2)) : s0;
-    const bool reach = gvalid && zb - sqrtf(gx * gx + gy * gy + gz * gz) - rb <= m->floor_margin + 1e-3f;
-    if (__ballot(reach) == 0ull) {
-      r.nrow = 0;
-      r.exmask = 0u;
-      return;
-    }
+  if (XFLOOR<XG> && bank == 1 && __ballot(gvalid) == 0ull) {
+    /* no geom of the second bank within reach of the floor in either env of the wave (select_bank2):
+       no row, the same state as the full test finds, without its shuffles and rotations */
+    r.nrow = 0;
+    r.exmask = 0u;
+    return;
   }
   float Jc[CAP];
 #pragma unroll
@@ -2270,6 +2267,52 @@ __device__ __forceinline__ void pair_rows(const Ctx& c, const EnvS& s, const Bod
 }
 
 /* collision + contact rows (lane r; XG: both banks) + dof rows (lane j) */
+/* The second contact-row bank's geoms for this substep (XG 1 / 2; model v9: up to ZB_MAX_GEOM floor
+   colliders). Lane l tests geom 2 + l by a bound: no point of a geom lies lower than its body origin
+   minus |geom_pos| minus the geom's bounding radius (box half-diagonal; capsule radius + half-length;
+   cylinder sqrt(r^2 + h^2); ellipsoid largest semi-axis; sphere radius; mesh the largest vertex
+   distance, geom_size[0]); the first two within reach of the margin (+1 mm against rounding), in
+   geom order, take the bank's halves (EnvS.xsel, -1: none). Any other geom is then off the floor, so
+   the contacts are MuJoCo's, except when more than two such geoms are within reach in one substep:
+   their contacts beyond the first two are not simulated, and the sticky state flag records it
+   (EnvS.nanflag bit 1, ZB_S_NAN). */
+template <int XG>
+__device__ __forceinline__ void select_bank2(const Ctx& c, const BodyK& B) {
+  MP m = c.m;
+  const int ng = m->ngeom;
+  const int g = 2 + c.l;
+  const bool valid = g < ng;
+  const int gg = valid ? g : 0;
+  const float zb = tsh(B.xp[2], m->geom_body[gg]);
+  const float gx = m->geom_pos[gg][0], gy = m->geom_pos[gg][1], gz = m->geom_pos[gg][2];
+  const float s0 = m->geom_size[gg][0], s1 = m->geom_size[gg][1], s2 = m->geom_size[gg][2];
+  const int ty = m->geom_type[gg];
+  const float rb = ty == ZB_GEOM_BOX ? sqrtf(s0 * s0 + s1 * s1 + s2 * s2)
+                   : ty == ZB_GEOM_CAPSULE ? s0 + s1
+                   : ty == ZB_GEOM_CYLINDER ? sqrtf(s0 * s0 + s1 * s1)
+                   : ty == ZB_GEOM_ELLIPSOID ? fmaxf(s0, fmaxf(s1, s2)) : s0;
+  const bool reach = valid && zb - sqrtf(gx * gx + gy * gy + gz * gz) - rb <= m->floor_margin + 1e-3f;
+  uint32_t mk = team_ballot(reach);
+  int sel0, sel1;
+  if (ng <= 2 + NGEOM) {
+    /* at most two other geoms: each keeps its own half (geom 2 lanes 0-15, geom 3 lanes 16-31), the
+       row layout of the static bank */
+    sel0 = (mk & 1u) ? 2 : -1;
+    sel1 = (mk & 2u) ? 3 : -1;
+    mk = 0u;
+  } else {
+    sel0 = mk ? 1 + __ffs(mk) : -1; /* 2 + (ffs - 1) */
+    mk &= mk - 1u;
+    sel1 = mk ? 1 + __ffs(mk) : -1;
+    mk &= mk - 1u;
+  }
+  /* team-uniform values, written by every lane of the team */
+  c.L->s.xsel[0] = sel0;
+  c.L->s.xsel[1] = sel1;
+  if (mk) c.L->s.nanflag |= 2u;
+  tsync();
+}
+
 template <int XG>
 __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, const LaneS& ls, const BodyK& B, const float cm[3],
                                  Rows& r) {
@@ -2278,8 +2321,28 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
   const int l = c.l;
   contact_rows<XG>(c, s, B, cm, 0, r, &c.L->u.J[l][0]);
   if constexpr (XG) {
-    if constexpr (XPAIR<XG>) pair_rows(c, s, B, cm, r.x, xrows(c.L) + l * CAP);
-    else contact_rows<XG>(c, s, B, cm, 1, r.x, xrows(c.L) + l * CAP);
+    if constexpr (XPAIR<XG>) {
+      pair_rows(c, s, B, cm, r.x, xrows(c.L) + l * CAP);
+    } else {
+      select_bank2<XG>(c, B);
+      contact_rows<XG>(c, s, B, cm, 1, r.x, xrows(c.L) + l * CAP);
+      /* the bank's rows on dof l's chain: dof l is an ancestor of (or is) the geom's last dof kd, a
+         root dof or one of kd's own limb chain at or above it */
+      uint32_t rm = c.rowmask2; /* at most two other geoms: zb_create's static mask (geoms 2, 3) */
+      if (m->ngeom > 2 + NGEOM) {
+        rm = 0u;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const int sg = c.L->s.xsel[h];
+          const int kd = sg >= 0 ? m->body_lastdof[m->geom_body[sg]] : -1;
+          const int kdc = kd >= 0 ? kd : 0;
+          const int hkd = tshi(c.chd, kdc);
+          const bool on = l < NV && kd >= 0 && l <= kd && (l < NROOT || c.chd == hkd);
+          rm |= on ? (0xFFFFu << (16 * h)) : 0u;
+        }
+      }
+      r.x.rowmask = rm;
+    }
     /* the second bank's work is skipped, bit for bit, while no row of it exists in the wave (the
        usual case: shins and hands off the floor) */
     r.x.any = __ballot(r.x.ex) != 0ull;
@@ -2478,7 +2541,8 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
     const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
     qc = (f0 ? so : 0.f) + (f1 ? sx : 0.f);
     if constexpr (XG && XA) {
-      const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
+      const uint32_t rm2 = XPAIR<XG> ? c.rowmask2 : r.x.rowmask;
+      const bool f2 = (rm2 & 0xFFFFu) != 0u, f3 = (rm2 >> 16) != 0u;
       qc += (f2 ? sx0 : 0.f) + (f3 ? sx1 : 0.f);
     }
     if (r.hf) qc += r.ff;
@@ -2605,7 +2669,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
       Hd += d0 + d1;
       if (XFLOOR<XG> && XA && r.x.any) {
         const float* GX = &L->Hs[0][0] + ddep * CAP;
-        const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
+        const bool f2 = (r.x.rowmask & 0xFFFFu) != 0u, f3 = (r.x.rowmask >> 16) != 0u;
         const float* G2 = f2 ? GX : &L->L[31][0];
         const float* G3 = f3 ? GX + CAP * CAP : &L->L[31][0];
         ld_row(G2, g0);
@@ -2625,7 +2689,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     if (XFLOOR<XG> && XA && r.x.any) {
       dl2 = r.x.ex ? ((r.x.act ? r.x.D : 0.f) - (pa2 ? r.x.D : 0.f)) : 0.f;
       ch2 = team_ballot(dl2 != 0.f); /* team-uniform: some row of the bank changed */
-      tb2 = ch2 & c.rowmask2;        /* per dof lane: the changed rows on its chain */
+      tb2 = ch2 & r.x.rowmask;       /* per dof lane: the changed rows on its chain */
     }
     tsync();
   }
@@ -3169,8 +3233,9 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     float fnt = ex7[6];
     /* the pair's halves: g = 2 geom2's body (+F), g = 3 geom1's (-F, in xdir); each foot's touch
        sensor takes the pair's normal force (its geom is in the contact) */
-    const int gg = (XPAIR<XG> && b1) ? m->pair_geom[g == NGEOM ? 1 : 0] : g;
-    if (gg < m->ngeom && c.l == m->geom_body[gg]) {
+    const int gg = (XPAIR<XG> && b1) ? m->pair_geom[g == NGEOM ? 1 : 0]
+                   : (XFLOOR<XG> && b1) ? c.L->s.xsel[g - NGEOM] : g;
+    if (gg >= 0 && gg < m->ngeom && c.l == m->geom_body[gg]) {
 #pragma unroll
       for (int k = 0; k < 6; k++) fext[k] += ext[k];
     }

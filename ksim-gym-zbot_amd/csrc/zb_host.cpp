@@ -104,8 +104,10 @@ int check_model(const ZbModel* m) {
                            "them knowingly", m->nskip_pair);
   if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
-  /* colliders: two banks of 32 contact-row lanes, 16 rows (4 contacts x 4 pyramid edges) per geom */
-  if (m->ngeom < 1 || m->ngeom * ZB_CON_PER_GEOM * 4 > 2 * 32)
+  /* colliders: two banks of 32 contact-row lanes, 16 rows (4 contacts x 4 pyramid edges) per geom; the
+     first bank holds geoms 0-1 (the soles), the second the first two others within reach of the floor
+     each substep (zb_engine.hip select_bank2) */
+  if (m->ngeom < 1 || m->ngeom > ZB_MAX_GEOM)
     return fail(ZB_EMODEL, "ngeom=%d: 1 to %d floor colliders", m->ngeom, ZB_MAX_GEOM);
   for (int g = 0; g < m->ngeom; g++) {
     const int ty = m->geom_type[g];

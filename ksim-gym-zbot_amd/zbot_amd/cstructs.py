@@ -10,16 +10,16 @@ MAX_BODY = 32
 MAX_DOF = 32
 MAX_QPOS = 40
 MAX_DEPTH = 12
-MAX_GEOM = 4
+MAX_GEOM = 16
 MAX_MESHV = 64
-MAX_MESHVERT = MAX_GEOM * MAX_MESHV
+MAX_MESHVERT = 512
 MAX_SITE = 8
 MAX_ACT = 32
 CON_PER_GEOM = 4
 CON_PER_PAIR = 4  # box-box: the sole pair
 
 MODEL_MAGIC = 0x5A424F54
-MODEL_VERSION = 8
+MODEL_VERSION = 9
 
 JNT_NONE = -1
 JNT_FREE = 0

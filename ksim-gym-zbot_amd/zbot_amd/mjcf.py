@@ -30,7 +30,7 @@ MJCF semantics (XML reference, MuJoCo 3.3.4 [U]):
     ZB_MAX_MESHV = 64 hull vertices (MJCF's maxhullvert can cap a hull);
   * box / capsule / cylinder / ellipsoid (size or fromto) / sphere / mesh <geom>s whose
     contype / conaffinity pass MuJoCo's test against the floor's
-    ((ct1 & ca2) || (ct2 & ca1)) as floor colliders, up to 4 in document order
+    ((ct1 & ca2) || (ct2 & ca1)) as floor colliders, up to 16 in document order
     (the engine's plane-box / -capsule / -cylinder / -sphere / -ellipsoid contacts;
     other such geoms are listed in desc["skipped_geoms"] and make zb_create refuse
     the model), the <geom type="plane"> of the worldbody as the floor (friction,
@@ -61,7 +61,7 @@ from .model import load_description
 # floor colliders the engine has contacts for (type -> sizes) and how many (ZB_MAX_GEOM)
 COLLIDER_TYPES = {"box": 3, "capsule": 2, "cylinder": 2, "sphere": 1, "ellipsoid": 3, "mesh": 0}
 MAX_HULL_VERTS = 64  # ZB_MAX_MESHV
-MAX_COLLIDERS = 4
+MAX_COLLIDERS = 16  # ZB_MAX_GEOM
 
 
 def _floats(s: str | None, n: int | None = None) -> list[float] | None:

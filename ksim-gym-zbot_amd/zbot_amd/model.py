@@ -204,7 +204,7 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
     """Compile a JSON robot description into a ZbModel (+ host float64 view).
 
     A description from zbot_amd.mjcf.load_mjcf lists the source's colliding geoms the engine does
-    not collide with the floor (it collides up to 4 boxes, capsules, cylinders, spheres and ellipsoids) in
+    not collide with the floor (it collides up to 16 boxes, capsules, cylinders, spheres, ellipsoids and convex meshes) in
     desc["skipped_geoms"]. They are counted into ZbModel.nskip_geom, and zb_create rejects such a
     model (ZB_EMODEL) rather than simulating it without those contacts. drop_colliders=True
     compiles it without them, knowingly (nskip_geom 0). Likewise desc["self_pairs"], the robot's

@@ -141,6 +141,63 @@ def mesh_desc() -> dict:
     return _variant(edit)
 
 
+def many_desc() -> dict:
+    """Nine floor colliders (model v9): the box soles, shin boxes, thigh capsules, a hand capsule, a
+    hand cube mesh and a head sphere. The engine's second bank takes, per substep, the first two of
+    the seven others within reach of the floor."""
+
+    def fmt(v):
+        return " ".join(repr(float(x)) for x in np.asarray(v).ravel())
+
+    def edit(root):
+        asset = ET.Element("asset")
+        cube = _jitter(np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+                       * [0.012, 0.015, 0.02], 6)
+        ET.SubElement(asset, "mesh", name="hand_mesh", vertex=fmt(cube))
+        root.insert(1, asset)
+        extra = {
+            "right_knee_pitch_link": '<geom name="right_shin" type="box" size="0.015 0.02 0.05" pos="0 0 -0.05" '
+                                     'euler="0.2 0 0.1" contype="1" conaffinity="0"/>',
+            "left_knee_pitch_link": '<geom name="left_shin" type="box" size="0.015 0.02 0.05" pos="0 0 -0.05" '
+                                    'euler="-0.1 0.1 0" contype="1" conaffinity="0"/>',
+            "right_hip_yaw_link": '<geom name="right_thigh" type="capsule" size="0.02" fromto="0 0 0 0 0.005 -0.07" '
+                                  'contype="1" conaffinity="0"/>',
+            "left_hip_yaw_link": '<geom name="left_thigh" type="capsule" size="0.02" fromto="0 0 0 0 -0.005 -0.07" '
+                                 'contype="1" conaffinity="0"/>',
+            "left_gripper_roll_link": '<geom name="left_hand" type="capsule" size="0.012" '
+                                      'fromto="0 0 0 0.01 0.0 -0.06" contype="1" conaffinity="0"/>',
+            "right_gripper_roll_link": '<geom name="right_hand" type="mesh" mesh="hand_mesh" pos="0 0 -0.03" '
+                                       'contype="1" conaffinity="0"/>',
+            "head": '<geom name="head_ball" type="sphere" size="0.05" pos="0 0 0.02" contype="1" conaffinity="0"/>',
+        }
+        for b in root.iter("body"):
+            if b.get("name") in extra:
+                b.append(ET.fromstring(extra[b.get("name")]))
+
+    return _variant(edit)
+
+
+def bank2_candidates(cm, qpos, margin=0.0) -> list[int]:
+    """The geoms (index in the compiled model's order, >= 2) that the engine's second-bank selection
+    finds within reach of the floor at qpos (zb_engine.hip select_bank2's bound, float64)."""
+    from zbot_amd.model import _kinematics
+
+    m = cm.cmodel
+    xpos, _ = _kinematics(cm.bodies, np.asarray(qpos, np.float64))
+    out = []
+    for g in range(2, m.ngeom):
+        s = [float(m.geom_size[g][k]) for k in range(3)]
+        ty = int(m.geom_type[g])
+        from zbot_amd import cstructs as cs
+
+        rb = {cs.GEOM_BOX: np.sqrt(s[0] ** 2 + s[1] ** 2 + s[2] ** 2), cs.GEOM_CAPSULE: s[0] + s[1],
+              cs.GEOM_CYLINDER: np.sqrt(s[0] ** 2 + s[1] ** 2), cs.GEOM_ELLIPSOID: max(s)}.get(ty, s[0])
+        gp = np.array([float(m.geom_pos[g][k]) for k in range(3)])
+        if xpos[m.geom_body[g]][2] - np.linalg.norm(gp) - rb <= margin + 1e-3:
+            out.append(g)
+    return out
+
+
 def mjx_box_desc() -> dict:
     """The default robot with its box soles collided as MJX does (compile_model(box_rule="mjx"): each
     box a convex mesh of its 8 corners, MJX's plane_convex manifold), as a descriptor."""

@@ -275,3 +275,94 @@ def test_full_size_properties(torch_gpu, name):
     gst, _ = run(grouped)
     grouped.join()
     assert torch.equal(gst, st)
+
+
+# ---- nine floor colliders (model v9): the second bank's per-substep selection ----
+
+def test_many_colliders_match_oracle_within_two(torch_gpu, oracle_mod):
+    """Nine floor colliders (collider_util.many_desc): the engine collides the soles and, per substep,
+    the first two of the other seven within reach of the floor (zb_engine.hip select_bank2). From
+    touching states: where the selection finds at most two (collider_util.bank2_candidates), one
+    forward pass matches the oracle, which collides all nine (contact and constraint counts exact,
+    qacc within 1e-3 relative), and one step holds the collider one-step contract for every env
+    whose step kept within two (no overflow flag, ZB_S_NAN bit 1); an env that starts with more
+    carries the flag after the step."""
+    torch = torch_gpu
+    from test_gpu_parity import MaxErr, one_step_outputs, oracle_steps
+
+    from zbot_amd.engine import DBG, HipEngine
+
+    cm = compile_model(U.many_desc())
+    cfg = default_config()
+    n = 64
+    env = contact_env(oracle_mod, cm, cfg, n, seed=5)
+    st = env.state.copy()
+    cand = [len(U.bank2_candidates(cm, st[e, :27].astype(np.float64))) for e in range(n)]
+    ctrl = (np.random.default_rng(2).normal(size=(n, 20)) * 0.5).astype(np.float32)
+    eng = HipEngine(cm, cfg, n, seed=5)
+    g = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()
+    checked = 0
+    for e in range(n):
+        if cand[e] > 2:
+            continue
+        ref = oracle_mod.forward_debug(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
+        assert int(g[e, DBG["misc"] + 1]) == ref["ncon"], e
+        assert int(g[e, DBG["misc"]]) == ref["nefc"], e
+        qa = g[e, DBG["qacc"]:DBG["qacc"] + 26]
+        assert np.abs(qa - ref["qacc"]).max() / max(1.0, np.abs(ref["qacc"]).max()) <= 1e-3, e
+        checked += 1
+    print(f"\n[many colliders] forward pass: {checked} of {n} envs within two second-bank candidates "
+          f"(candidates per env {np.bincount(cand).tolist()})")
+    assert checked >= n // 2
+    # one step
+    eng.set_state(torch.from_numpy(env.state.copy()))
+    eng.set_rand(torch.from_numpy(env.rand.copy()))
+    a = oracle_mod.synthetic_actions(cm.cmodel, 5, n, 0, 0)
+    ref, ref64 = oracle_steps(oracle_mod, cm, cfg, env, a, 5)
+    out = eng.step(torch.from_numpy(a).cuda())
+    torch.cuda.synchronize()
+    gs = eng.get_state().cpu().numpy()
+    flag = (gs[:, cs.S_NAN].view(np.int32) & 2) != 0
+    assert flag[np.array(cand) > 2].all(), "an env that starts with more than two candidates is flagged"
+    keep = ~flag
+    err = MaxErr("many colliders one-step (unflagged envs)")
+    for key, got, want in one_step_outputs(gs, out, env.state, ref):
+        err.add(key, got[keep], want[keep], *COLLIDER_TOL[key], ref64=ref64[key][keep])
+    print(f"[many colliders] one step: {int(keep.sum())} of {n} envs without the overflow flag")
+    err.report()
+
+
+def test_many_colliders_full_size(torch_gpu):
+    """The nine-collider model at the C2 size (8192 envs, pushes and randomization, 8 steps from reset):
+    finite, no non-finite flag (bit 0), bit-reproducible, and the same bits from two half-size handles
+    and from two env groups; prints how many envs ever overflowed the second bank."""
+    torch = torch_gpu
+    from zbot_amd.engine import EnvGroups, HipEngine
+
+    cm = compile_model(U.many_desc())
+    cfg = default_config(push=True, randomize=True)
+    n = 8192
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
+    acts = [bias + 0.2 * torch.randn(n, 20, device="cuda", generator=g) for _ in range(8)]
+
+    def run(h, lo=0, hi=n):
+        h.reset()
+        for a in acts:
+            out = h.step(a[lo:hi].contiguous())
+        return h.get_state(), out
+
+    st, out = run(HipEngine(cm, cfg, n, seed=9))
+    assert torch.isfinite(st[:, :58]).all() and torch.isfinite(out["obs_critic"]).all()
+    flags = st[:, cs.S_NAN].view(torch.int32)
+    assert ((flags & 1) == 0).all()
+    print(f"\n[many colliders C2] envs that overflowed the second bank in 8 steps: {int(((flags & 2) != 0).sum())}")
+    again, _ = run(HipEngine(cm, cfg, n, seed=9))
+    assert torch.equal(again, st)
+    halves = [run(HipEngine(cm, cfg, n // 2, env_offset=off, seed=9), off, off + n // 2)[0] for off in (0, n // 2)]
+    assert torch.equal(torch.cat(halves), st)
+    grouped = EnvGroups(cm, cfg, n, groups=2, seed=9)
+    gst, _ = run(grouped)
+    grouped.join()
+    assert torch.equal(gst, st)

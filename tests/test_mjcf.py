@@ -413,12 +413,13 @@ def test_colliders_are_parsed_and_unsupported_ones_reported():
     assert "skipped_geoms" not in load_mjcf(to_mjcf(load_description()))
 
 
-def test_colliders_past_four_are_reported():
-    geoms = "".join(f"<geom name='g{i}' type='box' size='0.01 0.01 0.01'/>" for i in range(6))
+def test_colliders_past_sixteen_are_reported():
+    """Up to 16 floor colliders (model v9, ZB_MAX_GEOM); the overflow is listed as skipped."""
+    geoms = "".join(f"<geom name='g{i}' type='box' size='0.01 0.01 0.01'/>" for i in range(18))
     b = load_mjcf("<mujoco><worldbody><body name='b'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
                   f"{geoms}</body></worldbody></mujoco>")
-    assert [g["name"] for g in b["geoms"]] == ["g0", "g1", "g2", "g3"]
-    assert [g["name"] for g in b["skipped_geoms"]] == ["g4", "g5"]
+    assert [g["name"] for g in b["geoms"]] == [f"g{i}" for i in range(16)]
+    assert [g["name"] for g in b["skipped_geoms"]] == ["g16", "g17"]
 
 
 def test_command_line_round_trip(tmp_path):
@@ -442,7 +443,7 @@ def test_missing_file_is_reported():
 
 
 def test_skipped_colliders_are_rejected_by_zb_create():
-    """A collider the engine has no floor contact for (a height field here; or a fifth collider) is not
+    """A collider the engine has no floor contact for (a height field here; or a seventeenth collider) is not
     dropped silently: zb_create rejects the model (ZB_EMODEL, nskip_geom); compile_model(...,
     drop_colliders=True) drops it knowingly (missing item 3). Supported extra colliders
     (a capsule or, since round 4, a cylinder or an ellipsoid shin) pass validation."""
@@ -495,16 +496,16 @@ def test_collider_sizes_beyond_the_type_are_ignored():
 
 
 def test_touch_sensor_colliders_win_the_cap():
-    """With more than four colliders the touch sensors' geoms (the soles) are kept even when four
-    other colliders come first in the document; the overflow is listed as skipped."""
-    geoms = "".join(f"<geom name='g{i}' type='sphere' size='0.01'/>" for i in range(4))
+    """With more than sixteen colliders the touch sensors' geoms (the soles) are kept even when
+    sixteen other colliders come first in the document; the overflow is listed as skipped."""
+    geoms = "".join(f"<geom name='g{i}' type='sphere' size='0.01'/>" for i in range(16))
     b = load_mjcf("<mujoco><worldbody><body name='a'><freejoint/><inertial mass='1' diaginertia='1 1 1'/>"
                   f"{geoms}<body name='foot'><joint name='j' type='hinge'/><inertial mass='1' diaginertia='1 1 1'/>"
                   "<geom name='sole' type='box' size='0.02 0.03 0.005'/><site name='foot_site'/></body></body>"
                   "</worldbody><actuator><motor joint='j'/></actuator>"
                   "<sensor><touch site='foot_site'/></sensor></mujoco>")
-    assert [g["name"] for g in b["geoms"]] == ["g0", "g1", "g2", "sole"]
-    assert [g["name"] for g in b["skipped_geoms"]] == ["g3"]
+    assert [g["name"] for g in b["geoms"]] == [f"g{i}" for i in range(15)] + ["sole"]
+    assert [g["name"] for g in b["skipped_geoms"]] == ["g15"]
     assert [s.get("touch_geom") for s in b["sites"]] == ["sole"]
 
 
