@@ -173,15 +173,19 @@ def read_mesh_file(path: str) -> np.ndarray:
     return np.asarray(out, dtype=np.float64)
 
 
-def hull_vertices(vert: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+def hull_vertices(vert: np.ndarray, maxhullvert: int = -1) -> tuple[np.ndarray, np.ndarray]:
     """The convex hull of a point set: (its vertices in the input order, its triangles as indices into
-    them). MuJoCo and MJX collide a mesh geom by this hull [U: MJX's vertex order]."""
+    them). MuJoCo and MJX collide a mesh geom by this hull [U: MJX's vertex order]. maxhullvert > 3:
+    MJCF's <mesh maxhullvert>, qhull stopped after that many vertices (MuJoCo passes qhull "TA" with
+    maxhullvert - 4, the vertices added after the initial simplex) [U: the qhull version]."""
     from scipy.spatial import ConvexHull  # noqa: PLC0415
 
     vert = np.asarray(vert, dtype=np.float64).reshape(-1, 3)
     if len(vert) < 4:
         raise ValueError("a mesh needs at least 4 vertices")
-    h = ConvexHull(vert)
+    if maxhullvert != -1 and maxhullvert < 4:
+        raise ValueError(f"maxhullvert {maxhullvert}: -1 or more than 3")
+    h = ConvexHull(vert, qhull_options="Qt" + (f" TA{maxhullvert - 4}" if maxhullvert > 3 else ""))
     keep = np.sort(h.vertices)
     remap = {int(i): k for k, i in enumerate(keep)}
     tri = np.array([[remap[int(i)] for i in s] for s in h.simplices], dtype=np.int64)
@@ -220,7 +224,7 @@ def _geom_mass_inertia(ga: dict, quat: list[float]):
     gt = ga.get("type", "sphere")
     if gt == "mesh":
         # the hull as a solid [U: MuJoCo's mesh inertia modes; "convex" is the hull's volume]
-        hv, tri = hull_vertices(ga["_mesh_vert"])
+        hv, tri = hull_vertices(ga["_mesh_vert"], int(ga.get("_maxhullvert", -1)))
         vol, com, I1 = _mesh_mass_props(hv, tri)
         m = float(ga["mass"]) if "mass" in ga else float(ga.get("density", "1000")) * vol
         I = I1 * (m / vol)
@@ -358,11 +362,15 @@ def self_pairs(geoms: list[dict], parent: dict[str, str], welded: set[str], excl
 
 
 def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | None = None,
-              base_clearance: float | None = None, template: dict | None = None) -> dict:
+              base_clearance: float | None = None, template: dict | None = None,
+              maxhullvert: int | None = None) -> dict:
     """Parse an MJCF file (path or XML text) into the descriptor compile_model() takes.
 
     template: descriptor supplying what MJCF does not hold (servo classes, the joint -> servo
-    map, base clearance, constraint solref/solimp); default assets/zbot_like.json."""
+    map, base clearance, constraint solref/solimp); default assets/zbot_like.json.
+    maxhullvert: cap every mesh's hull at this many vertices where the file sets no smaller cap (as
+    MJCF's <mesh maxhullvert>; e.g. 64, the engine's limit, to collide meshes whose full hull is
+    larger, knowingly with a coarser hull)."""
     tmpl = template or load_description()
     if src.lstrip().startswith("<"):
         text = src
@@ -386,6 +394,7 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
         meshdir = comp.get("meshdir", comp.get("assetdir", ""))
     base_dir = os.path.dirname(os.path.abspath(src)) if not src.lstrip().startswith("<") else os.getcwd()
     meshes: dict[str, np.ndarray] = {}
+    mesh_cap: dict[str, int] = {}  # the hull's vertex cap per mesh (maxhullvert; -1 none)
     for asset in root.findall("asset"):
         for me in asset.findall("mesh"):
             ma = defaults.attrs(me, me.get("class", "main"))
@@ -399,6 +408,10 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
             mv = mv * np.array(_floats(ma.get("scale", "1 1 1"), 3))
             mname = ma.get("name") or os.path.splitext(os.path.basename(ma["file"]))[0]
             meshes[mname] = mv
+            cap = int(ma.get("maxhullvert", "-1"))
+            if maxhullvert is not None and (cap == -1 or cap > maxhullvert):
+                cap = int(maxhullvert)
+            mesh_cap[mname] = cap
     flag = root.find("option/flag")
     filterparent = flag is None or flag.get("filterparent", "enable") != "disable"
     parent_of: dict[str, str] = {}
@@ -516,7 +529,7 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                         if ga.get("type") == "mesh":
                             if ga.get("mesh") not in meshes:
                                 raise ValueError(f"body {name}: geom of unknown mesh {ga.get('mesh')!r}")
-                            ga = dict(ga, _mesh_vert=meshes[ga["mesh"]])
+                            ga = dict(ga, _mesh_vert=meshes[ga["mesh"]], _maxhullvert=mesh_cap[ga["mesh"]])
                         parts.append(_geom_mass_inertia(ga, orientation(c, ga)))
             if not parts:
                 raise ValueError(f"body {name}: no <inertial> element and no geoms to infer it from")
@@ -547,7 +560,7 @@ def load_mjcf(src: str, servo_classes: dict | None = None, joint_servo: dict | N
                 if gt == "mesh":
                     if ga.get("mesh") not in meshes:
                         raise ValueError(f"geom {gname}: unknown mesh {ga.get('mesh')!r}")
-                    hv, _ = hull_vertices(meshes[ga["mesh"]])
+                    hv, _ = hull_vertices(meshes[ga["mesh"]], mesh_cap[ga["mesh"]])
                     if len(hv) > MAX_HULL_VERTS:
                         # the engine's plane-mesh contact scans at most 64 hull vertices
                         desc.setdefault("skipped_geoms", []).append(

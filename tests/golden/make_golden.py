@@ -40,6 +40,8 @@ CASES = {
     # round 5: the convex-mesh collider model (assets/zbot_like_mesh.xml; CPU regression pin of the
     # oracle's plane_mesh through a rollout with pushes: the GPU side is tests/test_gpu_colliders.py)
     "mesh_32x24_seed7": dict(n=32, steps=24, seed=7, push=True, randomize=False, std=0.2, model="zbot_like_mesh.xml"),
+    # round 5: nine floor colliders (model v9; the oracle collides all of them)
+    "many_32x24_seed8": dict(n=32, steps=24, seed=8, push=True, randomize=True, std=0.2, model="zbot_like_many.xml"),
 }
 
 

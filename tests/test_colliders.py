@@ -224,6 +224,28 @@ def test_mesh_hull_and_files(tmp_path):
     np.testing.assert_allclose(hand["vert"], cube * [1.2, 1.5, 2.0])
 
 
+def test_mesh_maxhullvert():
+    """MJCF's <mesh maxhullvert="N"> (and load_mjcf(maxhullvert=N) for meshes without a smaller cap)
+    keeps N hull vertices, each a vertex of the full hull, so a mesh whose hull exceeds the engine's
+    64 collides with a coarser hull instead of being skipped."""
+    from zbot_amd.mjcf import hull_vertices, load_mjcf, to_mjcf
+
+    rng = np.random.default_rng(1)
+    sph = rng.normal(size=(200, 3))
+    sph = sph / np.linalg.norm(sph, axis=1, keepdims=True) * 0.02
+    full, _ = hull_vertices(sph)
+    cap, tri = hull_vertices(sph, 24)
+    assert len(full) > 64 and len(cap) == 24 and tri.shape[1] == 3
+    assert {tuple(v) for v in cap} <= {tuple(v) for v in full}
+    vtx = " ".join(repr(float(x)) for x in sph.ravel())
+    text = to_mjcf(U.mesh_desc()).replace('<mesh name="left_hand_mesh" vertex="', '<mesh name="left_hand_mesh" maxhullvert="40" vertex="' + vtx + " ")
+    hand = next(g for g in load_mjcf(text)["geoms"] if g["name"] == "left_hand")
+    assert len(hand["vert"]) == 40
+    text2 = to_mjcf(U.mesh_desc()).replace('<mesh name="left_hand_mesh" vertex="', '<mesh name="left_hand_mesh" vertex="' + vtx + " ")
+    d = load_mjcf(text2, maxhullvert=64)
+    assert len(next(g for g in d["geoms"] if g["name"] == "left_hand")["vert"]) == 64 and "skipped_geoms" not in d
+
+
 def test_mesh_model_round_trips_and_refusals():
     """to_mjcf writes a mesh model back (hull vertices inline) and it compiles to the same bytes; a
     hull of more than 64 vertices is listed as skipped (zb_create refuses it) and compile_model
