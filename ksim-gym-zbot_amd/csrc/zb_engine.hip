@@ -628,12 +628,18 @@ struct Ctx {
   uint64_t lvlch; /* per body depth: max #children among bodies at that depth (4 bits each) */
   /* lane as dof */
   int ddep, dbody, qadr, act;
-  uint32_t rowmask;  /* contact rows whose Jacobian chain contains dof l */
-  uint32_t rowmask2; /* the same in the second bank (XG) */
+  /* contact rows whose Jacobian chain contains dof l, by 16-row half: bits 0-1 the first bank's
+     (geoms 0, 1), bits 2-3 the second bank's (XG); one register instead of two masks */
+  uint32_t rmb;
   int dk0;          /* index of dof l within its body's joint (free joint: 0..5) */
   int dfree;        /* dof l belongs to a free joint */
 };
 
+
+/* a 2-bit half mask of Ctx::rmb as the 32-row mask */
+__device__ __forceinline__ uint32_t rm_rows(uint32_t b) {
+  return ((b & 1u) ? 0xFFFFu : 0u) | ((b & 2u) ? 0xFFFF0000u : 0u);
+}
 
 /* the team's RNG identity (EnvS.env / seed, written by make_ctx) */
 __device__ __forceinline__ uint64_t cseed(const Ctx& c) {
@@ -2328,7 +2334,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
       contact_rows<XG>(c, s, B, cm, 1, r.x, xrows(c.L) + l * CAP);
       /* the bank's rows on dof l's chain: dof l is an ancestor of (or is) the geom's last dof kd, a
          root dof or one of kd's own limb chain at or above it */
-      uint32_t rm = c.rowmask2; /* at most two other geoms: zb_create's static mask (geoms 2, 3) */
+      uint32_t rm = rm_rows(c.rmb >> 2); /* at most two other geoms: zb_create's static mask (geoms 2, 3) */
       if (m->ngeom > 2 + NGEOM) {
         rm = 0u;
 #pragma unroll
@@ -2538,10 +2544,10 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
   tsync();
   float qc = 0.f;
   if (c.l < NV) {
-    const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
+    const bool f0 = (c.rmb & 1u) != 0u, f1 = (c.rmb & 2u) != 0u;
     qc = (f0 ? so : 0.f) + (f1 ? sx : 0.f);
     if constexpr (XG && XA) {
-      const uint32_t rm2 = XPAIR<XG> ? c.rowmask2 : r.x.rowmask;
+      const uint32_t rm2 = XPAIR<XG> ? rm_rows(c.rmb >> 2) : r.x.rowmask;
       const bool f2 = (rm2 & 0xFFFFu) != 0u, f3 = (rm2 >> 16) != 0u;
       qc += (f2 ? sx0 : 0.f) + (f3 ? sx1 : 0.f);
     }
@@ -2654,7 +2660,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
       /* the G row of each foot whose chain holds the dof, else the zero row 31 of L
          (G occupies rows 0..23): no per-entry selects */
       const float* G = &L->L[0][0] + ddep * CAP;
-      const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
+      const bool f0 = (c.rmb & 1u) != 0u, f1 = (c.rmb & 2u) != 0u;
       static_assert(NGEOM * CAP * CAP <= 31 * CAP, "G staged below the zero row 31");
       const float* G0 = f0 ? G : &L->L[31][0];
       const float* G1 = f1 ? G + CAP * CAP : &L->L[31][0];
@@ -2685,7 +2691,7 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     Hd = L->Hsd[c.l];
     const float dl = r.ex ? ((r.act ? r.D : 0.f) - (pa ? r.D : 0.f)) : 0.f;
     L->rowF[c.l] = dl; /* rowF is free until the next update_constraint */
-    tb = team_ballot(dl != 0.f) & c.rowmask;
+    tb = team_ballot(dl != 0.f) & rm_rows(c.rmb);
     if (XFLOOR<XG> && XA && r.x.any) {
       dl2 = r.x.ex ? ((r.x.act ? r.x.D : 0.f) - (pa2 ? r.x.D : 0.f)) : 0.f;
       ch2 = team_ballot(dl2 != 0.f); /* team-uniform: some row of the bank changed */
@@ -2841,8 +2847,8 @@ __device__ __forceinline__ float hmul_pair(const Ctx& c, const Rows& r, const fl
   const float so = tsh(cs0, ddep), sx = tsh(cs0, 16 + ddep), s2 = tsh(cs1, ddep), s3 = tsh(cs1, 16 + ddep);
   float y = 0.f;
   if (c.l < NV) {
-    const bool f0 = (c.rowmask & 0xFFFFu) != 0u, f1 = (c.rowmask >> 16) != 0u;
-    const bool f2 = (c.rowmask2 & 0xFFFFu) != 0u, f3 = (c.rowmask2 >> 16) != 0u;
+    const bool f0 = (c.rmb & 1u) != 0u, f1 = (c.rmb & 2u) != 0u;
+    const bool f2 = (c.rmb & 4u) != 0u, f3 = (c.rmb & 8u) != 0u;
     y = Mp + (f0 ? so : 0.f) + (f1 ? sx : 0.f) + (f2 ? s2 : 0.f) + (f3 ? s3 : 0.f);
     if (r.hf && r.actf) y += r.Df * p;
     if (r.anyl && r.hl && r.actl) y += r.Dl * p;
@@ -3794,8 +3800,10 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.dbody = t[TP_DBODY * TEAM];
   c.qadr = t[TP_QADR * TEAM];
   c.act = t[TP_ACT * TEAM];
-  c.rowmask = (uint32_t)t[TP_ROWMASK * TEAM];
-  c.rowmask2 = (uint32_t)t[TP_ROWMASK2 * TEAM];
+  {
+    const uint32_t r0 = (uint32_t)t[TP_ROWMASK * TEAM], r1 = (uint32_t)t[TP_ROWMASK2 * TEAM];
+    c.rmb = (r0 & 1u) | ((r0 >> 15) & 2u) | ((r1 & 1u) << 2) | ((r1 >> 13) & 8u);
+  }
   c.dk0 = t[TP_DK0 * TEAM];
   c.dfree = t[TP_DFREE * TEAM];
   c.chd = t[TP_CHD * TEAM];
