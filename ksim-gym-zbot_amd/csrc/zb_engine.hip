@@ -3952,7 +3952,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
         }
         {
           bool bad = (c.l < NV) && !(isfinite(ls.q) && isfinite(ls.v));
-          if (tmaxi(bad ? 1 : 0)) s.nanflag = 1u;
+          if (tmaxi(bad ? 1 : 0)) s.nanflag |= 1u; /* keeps bit 1 (select_bank2) */
         }
         bool fail;
         float* terms = (live && a.reward_terms && !rollout) ? a.reward_terms + (size_t)vopq(e) * ZB_NUM_TERMS : nullptr;

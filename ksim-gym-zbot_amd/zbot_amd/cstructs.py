@@ -55,6 +55,9 @@ S_RNG_STEP = 169
 S_PREV_CONT = 170
 S_EPISODE = 172
 S_NAN = 173
+# S_NAN's sticky flag bits (include/zbot_layout.h)
+NAN_NONFINITE = 1
+NAN_BANK_OVERFLOW = 2
 S_AIR0_CONT = 174
 S_AIR0_TERM = 175
 S_END = 176

@@ -117,6 +117,19 @@ DBG_STRIDE = 1760
 DBG = dict(qM=0, bias=1024, qacc_smooth=1056, qacc=1088, xpos=1120, cinert=1216, cvel=1536, misc=1728)
 
 
+def state_flags(state) -> dict:
+    """The sticky diagnostic flags of a [n, ZB_STATE_STRIDE] state (get_state()), as boolean [n]
+    tensors (include/zbot_layout.h ZB_S_NAN): `nonfinite` - the env's state went non-finite;
+    `bank_overflow` - in some substep more than two colliders beyond the soles were within reach of
+    the floor, and the extra ones' contacts were not simulated (zb_engine.hip select_bank2).
+    Both are sticky for the life of the env's state row (resets keep them; set_state() can clear
+    them). Works on CPU or device tensors."""
+    import torch
+
+    bits = state[:, cs.S_NAN].contiguous().view(torch.int32)
+    return {"nonfinite": (bits & cs.NAN_NONFINITE) != 0, "bank_overflow": (bits & cs.NAN_BANK_OVERFLOW) != 0}
+
+
 class HipEngine:
     """N Z-Bot environments on one GPU (one handle)."""
 
@@ -230,6 +243,10 @@ class HipEngine:
         out = self.torch.empty(self.n, cs.STATE_STRIDE, dtype=self.torch.float32, device=self.device)
         _check(self.L.zb_get_state(self.h, _ptr(out), self._stream()))
         return out
+
+    def flags(self) -> dict:
+        """state_flags(get_state()): per-env boolean `nonfinite` and `bank_overflow` [n]."""
+        return state_flags(self.get_state())
 
     def set_state(self, state) -> None:
         s = state.to(device=self.device, dtype=self.torch.float32).contiguous()

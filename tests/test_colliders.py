@@ -485,3 +485,17 @@ def test_box_box_oracle_precisions_agree(oracle_mod):
         if len(d64):
             assert (d64 <= 1e-6).all()
             np.testing.assert_allclose(n32, n64, atol=1e-4)
+
+
+def test_state_flags_decodes_the_sticky_bits():
+    """engine.state_flags reads ZB_S_NAN's u32 bits (include/zbot_layout.h): bit 0 non-finite, bit 1 the
+    second bank's overflow (select_bank2), independently."""
+    import torch
+
+    from zbot_amd.engine import state_flags
+
+    st = torch.zeros(4, cs.STATE_STRIDE, dtype=torch.float32)
+    st[:, cs.S_NAN] = torch.tensor([0, 1, 2, 3], dtype=torch.int32).view(torch.float32)
+    f = state_flags(st)
+    assert f["nonfinite"].tolist() == [False, True, False, True]
+    assert f["bank_overflow"].tolist() == [False, False, True, True]

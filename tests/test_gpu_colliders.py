@@ -323,6 +323,7 @@ def test_many_colliders_match_oracle_within_two(torch_gpu, oracle_mod):
     torch.cuda.synchronize()
     gs = eng.get_state().cpu().numpy()
     flag = (gs[:, cs.S_NAN].view(np.int32) & 2) != 0
+    assert np.array_equal(eng.flags()["bank_overflow"].cpu().numpy(), flag)
     assert flag[np.array(cand) > 2].all(), "an env that starts with more than two candidates is flagged"
     keep = ~flag
     err = MaxErr("many colliders one-step (unflagged envs)")
