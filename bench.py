@@ -8,7 +8,8 @@ rank processes itself; under torchrun WORLD_SIZE must equal N; with nccl (RCCL) 
 visible. Any mismatch exits with status 2 before a GPU call. The line reports `ranks_seen`.
 
 A "step" is one zb_step over all E envs of a GPU (20 physics substeps each,
-Newton solver 8 / 8 line-search iterations, observations, rewards, auto-reset)
+CG solver 8 / 8 line-search iterations -- MJX's SolverType.CG, as ksim sets it [U] (DESIGN.md §8);
+`--solver newton` for MuJoCo's Newton -- observations, rewards, auto-reset)
 — the hot path of ksim's step_engine for train.py's ZbotWalkingTask
 (SURVEY.md §3.2). Inputs are synthetic (actions = JOINT_BIASES + 0.05 N(0,1),
 generated on the GPU before timing); the state is resident in HBM. Prints ONE
@@ -35,6 +36,20 @@ CONFIGS = {
     "c2": dict(envs=8192, push=False, randomize=False, name="C2: {n} envs/GPU, flat-floor stand"),
     "c3": dict(envs=32768, push=True, randomize=False, name="C3: {n} envs/GPU, push-perturbation curriculum"),
     "c5": dict(envs=16384, push=False, randomize=True, name="C5: {n} envs/GPU, per-env domain randomization"),
+}
+
+
+# algorithmic FLOPs per env-step counted by the instrumented CPU twin (scripts/count_flops.py) for each
+# (solver, model variant) that the line prices; a variant without its own count gets no roofline_fp32
+FLOPS_FILES = {
+    ("cg", "base"): "r06_flops_count_cg.json",
+    ("newton", "base"): "r06_flops_count_newton.json",
+    ("cg", "mjxbox"): "r06_flops_count_cg_mjxbox.json",
+    ("newton", "mjxbox"): "r05_flops_count_mjxbox.json",
+    ("cg", "eulerdamp"): "r05_flops_count_cg_eulerdamp.json",
+    ("newton", "eulerdamp"): "r05_flops_count_eulerdamp.json",
+    ("cg", "solepair"): "r06_flops_count_cg_solepair.json",
+    ("newton", "solepair"): "r06_flops_count_solepair.json",
 }
 
 
@@ -608,7 +623,10 @@ def launch_ranks(world: int, argv: list) -> int:
     try:
         mp.start_processes(_rank_entry, args=(world, _free_port(), argv), nprocs=world, join=True,
                            start_method="spawn")
-    except Exception as e:  # ProcessRaisedException / ProcessExitedException: a rank failed
+    except mp.ProcessExitedException as e:  # a rank exited non-zero (2: a world / device mismatch)
+        print(f"bench.py: a rank failed: {e}", file=sys.stderr, flush=True)
+        return 2 if e.exit_code == 2 else 1
+    except Exception as e:  # ProcessRaisedException: a rank raised
         print(f"bench.py: a rank failed: {e}", file=sys.stderr, flush=True)
         return 1
     return 0
@@ -616,10 +634,10 @@ def launch_ranks(world: int, argv: list) -> int:
 
 def check_world(args) -> tuple[int, bool]:
     """The world size bench.py will run at, and whether this process must launch the ranks itself.
-    --gpus N is authoritative: under torchrun WORLD_SIZE must equal it, and the nccl backend (RCCL:
-    one rank per GPU) needs N visible devices. Exits with status 2 on a mismatch, before any GPU call."""
-    import torch  # noqa: PLC0415
-
+    --gpus N is authoritative: under torchrun WORLD_SIZE must equal it. Exits with status 2 on a
+    mismatch. No device query here: a self-launching parent must not touch HIP (torch's device count
+    falls back to hipGetDeviceCount when amdsmi is absent), so each rank checks the devices itself
+    (check_devices)."""
     env = os.environ.get("WORLD_SIZE")
     if env is not None and int(env) != args.gpus:
         print(f"bench.py: WORLD_SIZE={env} but --gpus {args.gpus}: launch exactly --gpus ranks", file=sys.stderr)
@@ -627,13 +645,20 @@ def check_world(args) -> tuple[int, bool]:
     if args.gpus < 1:
         print(f"bench.py: --gpus {args.gpus} < 1", file=sys.stderr)
         sys.exit(2)
-    if args.gpus > 1 and args.dist_backend == "nccl" and not args.launch_probe:
+    return args.gpus, env is None and args.gpus > 1
+
+
+def check_devices(args) -> None:
+    """In a rank process (never the self-launching parent): the nccl backend (RCCL, one rank per GPU)
+    needs --gpus visible devices. Exits with status 2 before any other GPU call."""
+    import torch  # noqa: PLC0415
+
+    if args.gpus > 1 and args.dist_backend == "nccl":
         ndev = torch.cuda.device_count()
         if ndev < args.gpus:
             print(f"bench.py: --gpus {args.gpus} with the nccl backend (RCCL, one rank per GPU) but only {ndev} "
                   "device(s) are visible", file=sys.stderr)
             sys.exit(2)
-    return args.gpus, env is None and args.gpus > 1
 
 
 def launch_probe(world: int, backend: str) -> None:
@@ -669,9 +694,9 @@ def main(argv: list | None = None) -> None:
                     help="robot: an MJCF (.xml) or descriptor (.json) file instead of the default Z-Bot-like "
                          "descriptor, e.g. ksim-gym-zbot_amd/assets/zbot_like_limbs.xml (colliders beyond the "
                          "soles: the general-collider kernels); roofline FLOP / traffic stay the default model's")
-    ap.add_argument("--solver", default="newton", choices=["newton", "cg"],
-                    help="constraint solver (ZbEnvConfig.solver): MuJoCo's Newton (default) or CG; which one "
-                         "ksim sets is [U] (DESIGN.md §8)")
+    ap.add_argument("--solver", default="cg", choices=["newton", "cg"],
+                    help="constraint solver (ZbEnvConfig.solver): MJX's CG (default: the one ksim's model setup "
+                         "selects, [U] DESIGN.md §8) or MuJoCo's Newton (the newton_solver leg)")
     ap.add_argument("--groups", type=int, default=2,
                     help="env groups per GPU, each stepping on its own HIP stream (zbot_amd.EnvGroups, "
                          "DESIGN.md §4f); 1 = one handle on the current stream")
@@ -713,12 +738,14 @@ def main(argv: list | None = None) -> None:
     if args.launch_probe:
         launch_probe(world, args.dist_backend)
         return
+    check_devices(args)
 
     import torch  # noqa: PLC0415
     import torch.distributed as dist  # noqa: PLC0415
     from zbot_amd import compile_model, default_config  # noqa: PLC0415
     from zbot_amd import cstructs as cs  # noqa: PLC0415
     from zbot_amd.constants import JOINT_BIASES  # noqa: PLC0415
+    from zbot_amd.dist import reduce_episode_stats  # noqa: PLC0415
     from zbot_amd.engine import EnvGroups, HipEngine  # noqa: PLC0415
     from zbot_amd.metrics import FP32_PEAK_TFLOPS, HBM_PEAK_GBS, bytes_per_env_step  # noqa: PLC0415
 
@@ -761,14 +788,9 @@ def main(argv: list | None = None) -> None:
     acts = bias + 0.05 * torch.randn(min(T, 64), n, cs.NJ, device=dev, generator=g)
 
     def reduce_stats():
-        # per-rollout episode statistics: per-GPU partials summed in fixed env order,
-        # then an RCCL all_gather and a fixed rank-order sum (bit-reproducible)
-        part = eng.get_stats(clear=False).double().sum(0)
-        if dist.is_initialized():
-            allp = [torch.zeros_like(part) for _ in range(world)]
-            dist.all_gather(allp, part)
-            return torch.stack(allp).sum(0)
-        return part
+        # per-rollout episode statistics: per-GPU partials summed in fixed env order, then an RCCL
+        # all_gather and a sequential rank-order sum (zbot_amd.dist.reduce_fixed_order: bit-reproducible)
+        return reduce_episode_stats(eng.get_stats(clear=False))
 
     # The other legs run first: their work (about two seconds of GPU time) brings the GPU to its
     # steady clocks before the headline's own W warm-up steps and K timed steps; in a fresh
@@ -806,8 +828,7 @@ def main(argv: list | None = None) -> None:
         other = "cg" if args.solver == "newton" else "newton"
         extra_legs[f"{other}_solver"] = bench_variant(
             cm, default_config(solver=other), f"the {other.upper() if other == 'cg' else 'Newton'} solver (ZbEnvConfig.solver)",
-            "r03_flops_count_cg.json" if other == "cg" else "r03_flops_count.json", n, args.steps, args.warmup, dev,
-            rank, world, args.seed, G)
+            FLOPS_FILES[(other, "base")], n, args.steps, args.warmup, dev, rank, world, args.seed, G)
         from zbot_amd.model import load_description  # noqa: PLC0415
 
         pdesc = load_description()
@@ -815,19 +836,16 @@ def main(argv: list | None = None) -> None:
         extra_legs["sole_pair"] = bench_variant(
             compile_model(pdesc), default_config(solver=args.solver),
             "the sole-pair model (the soles also collide with each other, box-box; the XG 3 kernels, DESIGN.md §4l)",
-            "r03_flops_count.json" if args.solver == "newton" else "r03_flops_count_cg.json", n, args.steps,
-            args.warmup, dev, rank, world, args.seed, G)
+            FLOPS_FILES[(args.solver, "solepair")], n, args.steps, args.warmup, dev, rank, world, args.seed, G)
         extra_legs["mjx_box_rule"] = bench_variant(
             compile_model(box_rule="mjx"), default_config(solver=args.solver),
             "the box soles collided by MJX's plane_convex manifold (compile_model(box_rule='mjx'): each an 8-corner "
             "convex mesh, the XG 2 kernels, DESIGN.md §8)",
-            "r05_flops_count_mjxbox.json" if args.solver == "newton" else "r05_flops_count_cg_mjxbox.json", n,
-            args.steps, args.warmup, dev, rank, world, args.seed, G)
+            FLOPS_FILES[(args.solver, "mjxbox")], n, args.steps, args.warmup, dev, rank, world, args.seed, G)
         extra_legs["eulerdamp"] = bench_variant(
             cm, default_config(solver=args.solver, eulerdamp=True),
             f"mj_Euler's implicit joint damping (ZB_F_EULERDAMP), {args.solver} solver",
-            "r05_flops_count_eulerdamp.json" if args.solver == "newton" else "r05_flops_count_cg_eulerdamp.json", n,
-            args.steps, args.warmup, dev, rank, world, args.seed, G)
+            FLOPS_FILES[(args.solver, "eulerdamp")], n, args.steps, args.warmup, dev, rank, world, args.seed, G)
 
     eng.reset()
     for t in range(args.warmup):
@@ -891,14 +909,14 @@ def main(argv: list | None = None) -> None:
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("envs") == n and args.solver == "newton":
+        # the PMC passes ran one solver's kernel (the file records which; round-5 files: Newton)
+        if tj.get("envs") == n and tj.get("solver", "newton") == args.solver:
             traffic = tj.get("hbm_bytes_per_launch")
             flop_per_env_step = tj.get("issued_fp32_flop_per_env_step")
     # algorithmic FLOPs per env-step, counted by the instrumented CPU twin on the C2 workload
     # (scripts/count_flops.py)
     algo_flop = None
-    fpath = os.path.join(ROOT, "profiles", "r03_flops_count.json" if args.solver == "newton" else
-                         f"r03_flops_count_{args.solver}.json")
+    fpath = os.path.join(ROOT, "profiles", FLOPS_FILES[(args.solver, "base")])
     if os.path.exists(fpath):
         with open(fpath) as f:
             algo_flop = json.load(f)["as_run"]["flops_per_env_step"]

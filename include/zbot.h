@@ -66,11 +66,16 @@ void zb_default_config(ZbEnvConfig* cfg);
  * (body 1, free joint) branches; nu = 20 hinge actuators, nv = 26; the free
  * joint's 6 dofs form the root of the dof tree and every limb is an
  * unbranched chain of consecutive dofs of at most 6 (dof depth <= 12); body
- * depth <= 8; 1 to 4 floor colliders (boxes, capsules, cylinders, spheres,
- * ellipsoids; model
- * nskip_geom = 0). Exactly two box colliders (the soles) run the two-sole
- * kernels; any other collider set runs the general-collider instantiation
- * (a second bank of 32 contact rows, larger LDS).
+ * depth <= 8; 1 to 16 floor colliders (ZB_MAX_GEOM, model version 9: boxes,
+ * capsules, cylinders, spheres, ellipsoids, convex meshes = geom type 7 with
+ * <= ZB_MAX_MESHV hull vertices; nskip_geom = 0), the touch sensors' geoms
+ * (the soles) first. Exactly two box colliders (the soles) run the two-sole
+ * kernels; any other collider set runs a general-collider instantiation with a
+ * second bank of 32 contact-row lanes (Jacobian rows in per-env global scratch),
+ * which holds, each substep, the first two of the other colliders within reach
+ * of the floor; a substep with more than two within reach sets bit 1 of the
+ * state's flag word (ZB_S_NAN; bit 0: non-finite). npair = 1 (the two box soles
+ * against each other, geom-geom) holds the pair's contacts in that second bank.
  *
  * Create a handle simulating `n_envs` environments whose global ids are
  * [env_offset, env_offset + n_envs) — RNG streams are keyed by global id, so

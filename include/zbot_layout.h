@@ -104,7 +104,8 @@ extern "C" {
 #define ZB_ST_DONE     2   /* number of finished episodes */
 #define ZB_ST_REWARD   3   /* sum of per-step total reward */
 
-/* ZbEnvConfig.solver (mjtSolver order: mjSOL_CG = 1, mjSOL_NEWTON = 2; here 0 is the default) */
+/* ZbEnvConfig.solver (mjtSolver order: mjSOL_CG = 1, mjSOL_NEWTON = 2). zb_default_config() sets
+   ZB_SOLVER_CG (round 6: the solver ksim's MJX model uses); a zero-filled config is Newton */
 #define ZB_SOLVER_NEWTON 0u  /* primal Newton, Hessian M + J'DJ (mj_solNewton) */
 #define ZB_SOLVER_CG     1u  /* primal nonlinear CG, M^-1 preconditioned, Polak-Ribiere (mj_solCG) */
 
@@ -155,8 +156,8 @@ typedef struct ZbEnvConfig {
   float    rand_imu_tilt_std;   /* radians(5)  train.py:1453 */
   float    rand_imu_yaw_std;    /* radians(1)  */
   float    rand_imu_pos_std;    /* 0.005 m     */
-  int32_t  solver;             /* ZB_SOLVER_NEWTON (default) or ZB_SOLVER_CG: the [U] solver type
-                                  ksim sets on the MJX model */
+  int32_t  solver;             /* ZB_SOLVER_CG (zb_default_config) or ZB_SOLVER_NEWTON: the [U] solver
+                                  type ksim sets on the MJX model */
   float    pad[2];
 } ZbEnvConfig;
 

@@ -43,6 +43,8 @@ struct ZbHandle {
   uint32_t* sched; /* chunked step: [2 + npair] counters and per-pair progress (zb_internal.h) */
   int32_t* itpart; /* chunked step: [n] Newton iterations so far */
   float* xj;       /* general colliders: [n + 1, ZB_XJ_STRIDE] second-bank Jacobian rows (zb_internal.h) */
+  int xg;          /* needs_xg(model), decided once in zb_create: every launch uses the instantiation that
+                      xj was (or was not) allocated for, whatever ZB_FORCE_XG says later */
   int nchunk;      /* work units per pair of envs in zb_step (1: unchunked) */
   int air_mark;    /* zb_mark_rollout_start: the next zb_step / zb_rollout is a rollout's step 0 */
   int air_marked;  /* a marked step has been launched since the last zb_feet_airtime_exact */
@@ -135,8 +137,9 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMemset(h->sched, 0, (3 + (n + 1) / 2) * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMalloc(&h->itpart, n * sizeof(int32_t));
   if (e == hipSuccess) e = hipMemset(h->itpart, 0, n * sizeof(int32_t));
-  if (e == hipSuccess && zb::needs_xg(model)) e = hipMalloc(&h->xj, (n + 1) * ZB_XJ_STRIDE * sizeof(float));
-  h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device, zb::needs_xg(model), cfg->solver, (cfg->flags & ZB_F_EULERDAMP) ? 1 : 0));
+  h->xg = zb::needs_xg(model);
+  if (e == hipSuccess && h->xg) e = hipMalloc(&h->xj, (n + 1) * ZB_XJ_STRIDE * sizeof(float));
+  h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device, h->xg, cfg->solver, (cfg->flags & ZB_F_EULERDAMP) ? 1 : 0));
 #if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
   {
     /* phase stamps: ZB_NSTAMP per env; wave times: 4 words per (chunk, pair), up to one chunk per
@@ -192,7 +195,7 @@ static zb::StepArgs base_args(ZbHandle* h) {
   a.sched = h->sched;
   a.itpart = h->itpart;
   a.solver = h->cfg.solver;
-  a.xg = zb::needs_xg(&h->hmodel);
+  a.xg = h->xg;
   a.ed = (h->cfg.flags & ZB_F_EULERDAMP) ? 1 : 0;
   a.xj = h->xj;
   return a;
@@ -324,7 +327,7 @@ int zb_set_step_chunks(ZbHandle* h, int k) {
   if (k == 0) {
     int rc = use_device(h);
     if (rc) return rc;
-    h->nchunk = choose_chunks(h->n, h->cfg.n_substeps, zb::step_resident_blocks(h->device, zb::needs_xg(&h->hmodel), h->cfg.solver, (h->cfg.flags & ZB_F_EULERDAMP) ? 1 : 0));
+    h->nchunk = choose_chunks(h->n, h->cfg.n_substeps, zb::step_resident_blocks(h->device, h->xg, h->cfg.solver, (h->cfg.flags & ZB_F_EULERDAMP) ? 1 : 0));
   } else {
     h->nchunk = k > h->cfg.n_substeps ? h->cfg.n_substeps : k;
   }

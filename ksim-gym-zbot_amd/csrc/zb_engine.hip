@@ -3045,17 +3045,23 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     r.jar = jw;
     r.x.jar = jwx;
   }
+  STAMP(S_WARM);
   r.jf = x - r.af;
   r.jl = r.sl * x - r.al;
   const float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
   float cost = update_constraint<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
+  STAMP(S_UPD0);
   float mg = solve_ldl(c, grad, DinvM);
+  STAMP(S_SOLVE0);
   float search = -mg;
   int it = 0;
-  while (live && it < cfg->iterations) {
+  const int itmax = cfg->iterations;
+  while (live && it < itmax) {
     float Mv;
+    STAMP(S_CHECK);
     const float alpha = line_search<XG, XA>(c, r, jr, search, Ma, fs, grad, Mv);
+    STAMP(S_LS);
     if (alpha == 0.f) break;
     x += alpha * search;
     Ma += alpha * Mv;
@@ -3064,20 +3070,30 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
-    float red[2];
-    red[0] = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
-    red[1] = c.l < NV ? grad * grad : 0.f;
-    tsum_n<2>(red);
-    cost = red[0];
+    const float cl = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
+    STAMP(S_UPD);
     it++;
-    const float improvement = scale * (oldcost - cost);
-    const float gradient = scale * sqrtf(red[1]);
-    if (improvement < cfg->tolerance || gradient < cfg->tolerance || it >= cfg->iterations) break;
-    mg = solve_ldl(c, grad, DinvM);
-    float pr[2] = {c.l < NV ? grad * (mg - mgold) : 0.f, c.l < NV ? gold * mgold : 0.f};
-    tsum_n<2>(pr);
-    const float beta = fmaxf(pr[0] / fmaxf(pr[1], MINVAL), 0.f);
-    search = -mg + beta * search;
+    /* MJX's order (solver.py: _update_gradient, then the Polak-Ribiere beta, then the termination
+       test): the next direction M^-1 grad is solved before the test, so that the iteration's four
+       team sums (cost, |grad|^2 and beta's numerator and denominator) are one interleaved reduction
+       (the same DPP sequence per value: the bits of separate sums). An iteration at the cap skips the
+       solve and the beta sums, which only feed the next iteration. */
+    if (it < itmax) {
+      mg = solve_ldl(c, grad, DinvM);
+      STAMP(S_SOLVE);
+      float red[4] = {cl, c.l < NV ? grad * grad : 0.f, c.l < NV ? grad * (mg - mgold) : 0.f,
+                      c.l < NV ? gold * mgold : 0.f};
+      tsum_n<4>(red);
+      cost = red[0];
+      const float improvement = scale * (oldcost - cost);
+      const float gradient = scale * sqrtf(red[1]);
+      if (improvement < cfg->tolerance || gradient < cfg->tolerance) break;
+      const float beta = fmaxf(red[2] / fmaxf(red[3], MINVAL), 0.f);
+      search = -mg + beta * search;
+    } else {
+      (void)cl; /* the cap: the cost and |grad| feed only a test whose outcome is known */
+      break;
+    }
   }
   iters += it;
   ftot = Ma - grad; /* as solve_newton */

@@ -320,6 +320,7 @@ void zb_default_config(ZbEnvConfig* c) {
   c->ctrl_dt = 0.02f;
   c->tolerance = 1e-8f;
   c->ls_tolerance = 0.01f;
+  c->solver = (int32_t)ZB_SOLVER_CG; /* MJX's CG, as ksim's model setup selects it [U] */
   c->imu_noise_std = (float)(PI / 180.0);
   c->acc_noise_std = 0.5f;
   c->reset_qvel_scale = 0.01f;

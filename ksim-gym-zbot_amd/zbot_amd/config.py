@@ -26,11 +26,12 @@ def default_config(
     dt: float = DT,
     ctrl_dt: float = CTRL_DT,
     max_episode_sec: float = 80.0,
-    solver: str = "newton",
+    solver: str = "cg",
     eulerdamp: bool = False,
 ) -> cs.ZbEnvConfig:
-    """solver: "newton" (MuJoCo's default, mj_solNewton) or "cg" (mj_solCG, which MJX training setups
-    commonly select for speed); which one ksim 0.1.99 sets on the model is [U].
+    """solver: "cg" (default: mj_solCG / MJX SolverType.CG, the solver ksim's MJX model setup selects
+    as DESIGN.md §8 records it [U: ksim 0.1.99 is not on disk]) or "newton" (MuJoCo's own default,
+    mj_solNewton). SURVEY §8a a11 reads "likely CG".
 
     eulerdamp: mj_Euler's implicit joint damping (MuJoCo's default, mjDSBL_EULERDAMP clear): qvel
     advances with (M + dt diag(damping))^-1 (qfrc_smooth + qfrc_constraint). Off by default: ksim

@@ -513,6 +513,10 @@ def compile_model(desc: dict | str | None = None, drop_colliders: bool = False,
             if not (1 <= len(vert) <= cs.MAX_MESHV) or not np.isfinite(vert).all():
                 raise ValueError(f"geom {gd['name']}: a mesh collider needs 1 to {cs.MAX_MESHV} finite hull vertices "
                                  f"(has {len(vert)}; MJCF <mesh maxhullvert> can cap the hull)")
+            if vadr + len(vert) > cs.MAX_MESHVERT:
+                raise ValueError(f"geom {gd['name']}: the mesh colliders' hull vertices exceed the model's pool of "
+                                 f"{cs.MAX_MESHVERT} (ZB_MAX_MESHVERT: {vadr} used before this geom, {len(vert)} more); "
+                                 "cap the hulls with MJCF <mesh maxhullvert> or load_mjcf(maxhullvert=...)")
             m.geom_vertadr[gi] = vadr
             m.geom_vertnum[gi] = len(vert)
             for i, v in enumerate(vert):

@@ -59,14 +59,25 @@ def main():
     ap.add_argument("--eulerdamp", action="store_true", help="mj_Euler's implicit joint damping (ZB_F_EULERDAMP)")
     ap.add_argument("--box-rule", default="mujoco", choices=["mujoco", "mjx"],
                     help="compile_model(box_rule=...): the soles by MJX's plane_convex manifold")
+    ap.add_argument("--sole-pair", action="store_true",
+                    help="the sole-pair model: the two box soles also collide with each other (DESIGN.md §4l)")
     args = ap.parse_args()
-    cm = compile_model(box_rule=args.box_rule)
+    if args.sole_pair:
+        from zbot_amd.model import load_description  # noqa: PLC0415
+
+        desc = load_description()
+        desc["self_pairs"] = [["left_foot_sole", "right_foot_sole"]]
+        cm = compile_model(desc, box_rule=args.box_rule)
+    else:
+        cm = compile_model(box_rule=args.box_rule)
     res = {"workload": f"C2 standing task, {args.envs} envs x {args.steps} env-steps after 20 warm-up steps, "
                        f"JOINT_BIASES + 0.05 N(0,1) actions (zbo_synthetic_actions), {args.solver} 8 / 8"
                        + (", implicit joint damping (eulerdamp)" if args.eulerdamp else "")
-                       + (", box soles by MJX's plane_convex (box_rule mjx)" if args.box_rule == "mjx" else ""),
+                       + (", box soles by MJX's plane_convex (box_rule mjx)" if args.box_rule == "mjx" else "")
+                       + (", sole-pair model (the soles collide with each other)" if args.sole_pair else ""),
            "note": "FMA counted as a multiply and an add; compares listed apart and not in the FLOPs",
-           "solver": args.solver, "eulerdamp": args.eulerdamp, "box_rule": args.box_rule}
+           "solver": args.solver, "eulerdamp": args.eulerdamp, "box_rule": args.box_rule,
+           "sole_pair": args.sole_pair}
     res["as_run"] = count(cm, default_config(solver=args.solver, eulerdamp=args.eulerdamp), args.envs, args.steps)
     fixed = default_config(solver=args.solver, eulerdamp=args.eulerdamp)
     fixed.tolerance = -1.0

@@ -28,7 +28,7 @@ def gap(env, ref64):
 
 
 def main():
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     for name in ("limbs", "cyl"):
         cm = compile_model(getattr(U, name + "_desc")())
         env = O.OracleEnv(cm.cmodel, cfg, 16, seed=3)

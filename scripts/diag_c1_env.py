@@ -33,7 +33,7 @@ def main():
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "c1_64x128_seed0.npz")))
     n, seed = int(g["cfg_n"]), int(g["cfg_seed"])
     cm = compile_model()
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     if a.tol is not None:
         cfg.tolerance = a.tol
     e32 = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)

@@ -17,7 +17,7 @@ from zbot_amd import compile_model, default_config  # noqa: E402
 
 cm = compile_model(getattr(U, sys.argv[1])())
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 12
-cfg = default_config(push=True)
+cfg = default_config(solver="newton", push=True)
 n, seed = 64, 13
 acts = np.stack([O.synthetic_actions(cm.cmodel, seed, n, 0, t, std=0.5) for t in range(steps)])
 e32 = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)

@@ -82,7 +82,7 @@ def main():
         build(tmp)
         oracle.HERE = tmp
         cm = compile_model()
-        env = oracle.OracleEnv(cm.cmodel, default_config(), a.envs)
+        env = oracle.OracleEnv(cm.cmodel, default_config(solver="newton"), a.envs)
         env.L.zbo_cnt_get.argtypes = [C.POINTER(C.c_longlong)]
         env.reset()
         for t in range(a.warmup + a.steps):

@@ -23,7 +23,7 @@ else:
 g = torch.Generator(device="cuda")
 g.manual_seed(0)
 bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
-eng = HipEngine(cm, default_config(), 8192, seed=1, lib_path=lib)
+eng = HipEngine(cm, default_config(solver=os.environ.get("SOLVER", "cg")), 8192, seed=1, lib_path=lib)
 eng.reset()
 for t in range(steps):
     eng.step(bias + 0.05 * torch.randn(8192, 20, device="cuda", generator=g), extras=False)

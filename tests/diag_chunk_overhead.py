@@ -29,7 +29,7 @@ def main():
     for p in a.libs:
         for k in [int(x) for x in a.chunks.split(",")]:
             os.environ["ZB_STEP_CHUNKS"] = str(k)
-            e = HipEngine(cm, default_config(), a.n, lib_path=os.path.abspath(p), seed=0)
+            e = HipEngine(cm, default_config(solver="newton"), a.n, lib_path=os.path.abspath(p), seed=0)
             e.reset()
             for t in range(3):
                 e.step(acts[t])

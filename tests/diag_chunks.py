@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--push", action="store_true")
     a = ap.parse_args()
     cm = compile_model()
-    cfg = default_config(push=a.push, randomize=a.push)
+    cfg = default_config(solver="newton", push=a.push, randomize=a.push)
     bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
     chunks = [int(k) for k in a.chunks.split(",")]
     for n in [int(x) for x in a.sizes.split(",")]:

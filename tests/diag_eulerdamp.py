@@ -23,7 +23,7 @@ ed = bool(int(sys.argv[1])) if len(sys.argv) > 1 else True
 watch = int(sys.argv[2]) if len(sys.argv) > 2 else 23
 cm = compile_model()
 n = 64
-cfg = default_config(eulerdamp=ed)
+cfg = default_config(solver="newton", eulerdamp=ed)
 env = O.OracleEnv(cm.cmodel, cfg, n, seed=7)
 env.reset()
 for t in range(12):
@@ -31,7 +31,7 @@ for t in range(12):
 for t in range(2):
     env.step(O.synthetic_actions(cm.cmodel, 7, n, 0, 100 + t))
 a = O.synthetic_actions(cm.cmodel, 7, n, 0, 102)
-c1 = default_config(eulerdamp=ed, ctrl_dt=0.001)
+c1 = default_config(solver="newton", eulerdamp=ed, ctrl_dt=0.001)
 o32 = O.OracleEnv(cm.cmodel, c1, n, seed=7)
 o64 = O.OracleEnv(cm.cmodel, c1, n, seed=7, precision="f64")
 o32.state[:] = env.state
@@ -73,7 +73,7 @@ np.set_printoptions(precision=5, suppress=True, linewidth=200)
 print(f"replaying substep {ss}: touch {st[watch, cs.S_TOUCH:cs.S_TOUCH + 2]} prev contact "
       f"{st[watch, cs.S_PREV_CONT:cs.S_PREV_CONT + 2]} qpos z {st[watch, 2]:.5f}")
 for e2 in (ed, not ed):
-    c2 = default_config(eulerdamp=e2, ctrl_dt=0.001)
+    c2 = default_config(solver="newton", eulerdamp=e2, ctrl_dt=0.001)
     oo = O.OracleEnv(cm.cmodel, c2, n, seed=7)
     oo.state[:] = st
     oo.rand[:] = o32.rand

@@ -36,7 +36,7 @@ def main():
     args = ap.parse_args()
     cm = compile_model()
     m = cm.cmodel
-    cfg = default_config(obs_noise=True)
+    cfg = default_config(solver="newton", obs_noise=True)
     n = args.n
     orc = O.OracleEnv(m, cfg, n, seed=7)
     orc.reset()

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--lib", default="libzbot_hip_stamps.so")
     ap.add_argument("--nslots", type=int, default=20, help="stamp slots of the build (ZB_NSTAMP)")
+    ap.add_argument("--solver", default="cg", choices=["cg", "newton"])
     ap.add_argument("--names", default="", help="names of the extra slots (scripts/stamp_probe.py)")
     args = ap.parse_args()
     NS = args.nslots
@@ -39,7 +40,7 @@ def main():
         PHASES.extend(args.names.split(","))
     lib = os.path.join(ROOT, "ksim-gym-zbot_amd", "zbot_amd", args.lib)
     cm = compile_model()
-    eng = HipEngine(cm, default_config(), args.n, lib_path=lib)
+    eng = HipEngine(cm, default_config(solver=args.solver), args.n, lib_path=lib)
     eng.L.zb_get_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     eng.reset()
     bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")

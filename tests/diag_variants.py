@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--groups", type=int, default=1, help="env groups on their own streams (EnvGroups)")
     ap.add_argument("--model", default=None, help="an MJCF file (e.g. the limbs asset) instead of the default model")
     ap.add_argument("--box-rule", default="mujoco", choices=["mujoco", "mjx"], help="compile_model(box_rule=...)")
+    ap.add_argument("--solver", default="cg", choices=["cg", "newton"])
     a = ap.parse_args()
     if a.model:
         from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
@@ -33,10 +34,10 @@ def main():
     bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
     acts = [bias + 0.05 * torch.randn(a.n, 20, device="cuda") for _ in range(8)]
     if a.groups > 1:
-        engs = [EnvGroups(cm, default_config(), a.n, groups=a.groups, lib_path=os.path.abspath(p), seed=0)
+        engs = [EnvGroups(cm, default_config(solver=a.solver), a.n, groups=a.groups, lib_path=os.path.abspath(p), seed=0)
                 for p in a.libs]
     else:
-        engs = [HipEngine(cm, default_config(), a.n, lib_path=os.path.abspath(p), seed=0) for p in a.libs]
+        engs = [HipEngine(cm, default_config(solver=a.solver), a.n, lib_path=os.path.abspath(p), seed=0) for p in a.libs]
     for e in engs:
         e.reset()
         for t in range(3):

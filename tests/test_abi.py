@@ -63,6 +63,7 @@ def test_c_default_config_matches_python(hiplib):
     c = cs.ZbEnvConfig()
     hiplib.zb_default_config(C.byref(c))
     p = default_config()
+    assert c.solver == cs.SOLVER_CG and p.solver == cs.SOLVER_CG  # MJX's CG
     for name, _ in cs.ZbEnvConfig._fields_:
         a, b = getattr(c, name), getattr(p, name)
         if hasattr(a, "__len__"):
@@ -76,12 +77,12 @@ def test_model_validation_errors(hiplib, cmodel):
     bad = type(cmodel.cmodel).from_buffer_copy(cmodel.cmodel)
     bad.magic = 0
     h = C.c_void_p()
-    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc == -1
     assert b"magic" in hiplib.zb_last_error()
     bad = type(cmodel.cmodel).from_buffer_copy(cmodel.cmodel)
     bad.nv = 40
-    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc == -4
 
 
@@ -97,19 +98,19 @@ def test_tree_shape_validation(hiplib, cmodel):
     first_leg = [b for b in range(2, nb) if bad.body_parent[b] == 1][0]
     leaf = [b for b in range(2, nb) if all(bad.body_parent[k] != b for k in range(nb))][-1]
     bad.body_parent[leaf] = first_leg + 1  # first_leg + 1 already has a child
-    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc == -4 and b"branches" in hiplib.zb_last_error()
     # a branching limb in the dof tree: hang a limb dof off the middle of another limb
     bad = type(m).from_buffer_copy(m)
     heads = [k for k in range(6, bad.nv) if bad.dof_parent[k] == 5]
     k = heads[1]
     bad.dof_parent[k] = heads[0] + 1
-    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = hiplib.zb_create(C.byref(bad), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc == -4 and b"unbranched" in hiplib.zb_last_error()
 
 
 def test_bad_config_rejected(hiplib, cmodel):
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     cfg.struct_bytes = 4
     h = C.c_void_p()
     rc = hiplib.zb_create(C.byref(cmodel.cmodel), C.byref(cfg), 4, 0, 0, 0, C.byref(h))
@@ -122,7 +123,7 @@ def test_engine_fails_loudly_without_gpu(cmodel):
     if torch.cuda.is_available():
         pytest.skip("GPU present")
     with pytest.raises(E.ZbError):
-        E.HipEngine(cmodel, default_config(), 4)
+        E.HipEngine(cmodel, default_config(solver="newton"), 4)
 
 
 def test_compiled_model_tables(cmodel):

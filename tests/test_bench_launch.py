@@ -52,3 +52,24 @@ def test_nccl_needs_a_gpu_per_rank():
 
 def test_bad_gpu_count_exits():
     assert _run(["--gpus", "0"]).returncode == 2
+
+
+def test_parent_makes_no_device_query(monkeypatch):
+    """The self-launching parent decides the world size without asking HIP for devices (ADVICE r05:
+    torch's device count may initialise HIP when amdsmi is absent); the ranks check the devices."""
+    import argparse
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def boom(*a, **k):
+        raise AssertionError("the parent queried the devices")
+
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    args = argparse.Namespace(gpus=4, dist_backend="nccl", launch_probe=False)
+    assert bench.check_world(args) == (4, True)
+    with __import__("pytest").raises(AssertionError):
+        bench.check_devices(args)

@@ -71,7 +71,7 @@ def test_zb_create_accepts_the_variants(variant):
     _, cm = variant
     L = E.load_library()
     h = C.c_void_p()
-    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc != -4, L.zb_last_error()  # validation passes (no device here: -2)
     if rc == 0:
         L.zb_destroy(h)
@@ -84,7 +84,7 @@ def test_oracle_contact_sets_match_mujoco_rules(variant, oracle_mod, precision):
     capsule: the end spheres; cylinder: up to four rim points; sphere; ellipsoid: the support
     point), and some contacts of every collider occur."""
     name, cm = variant
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     qs = U.touching_states(cm, 96, seed=3).astype(np.float32)
     touched = np.zeros(cm.cmodel.ngeom, int)
     for e in range(len(qs)):
@@ -499,3 +499,24 @@ def test_state_flags_decodes_the_sticky_bits():
     f = state_flags(st)
     assert f["nonfinite"].tolist() == [False, True, False, True]
     assert f["bank_overflow"].tolist() == [False, False, True, True]
+
+
+def test_mesh_vertex_pool_limit_is_a_value_error():
+    """Hulls beyond the 512-vertex pool (ZB_MAX_MESHVERT; up to 64 vertices each, 16 colliders):
+    compile_model names the pool limit instead of failing inside ctypes."""
+    d = U.mesh_desc()
+    tmpl = next(g for g in d["geoms"] if g["type"] == "mesh" and g["name"] != "right_foot_sole")
+    used = sum(len(g["vert"]) for g in d["geoms"] if g["type"] == "mesh")
+    rng = np.random.default_rng(3)
+    extra = []
+    while used + 64 * len(extra) <= 512:
+        v = rng.normal(size=(64, 3))
+        extra.append(dict(tmpl, name=f"hull{len(extra)}", vert=(v / np.linalg.norm(v, axis=1, keepdims=True) * 0.02).tolist()))
+    base = list(d["geoms"])
+    d["geoms"] = base + extra
+    assert len(d["geoms"]) <= 16
+    with pytest.raises(ValueError, match="pool"):
+        compile_model(d)
+    d["geoms"] = base + extra[:-1]  # one hull fewer fits
+    cm = compile_model(d)
+    assert cm.cmodel.geom_vertnum[len(d["geoms"]) - 1] == 64

@@ -37,7 +37,7 @@ def _run_rank(rank, world, port, outdir):
     from zbot_amd.dist import reduce_episode_stats, shard
 
     cm = compile_model()
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     off, n = shard(N_GLOBAL, world, rank)
     env = O.OracleEnv(cm.cmodel, cfg, n, env_offset=off, seed=SEED)
     env.reset()
@@ -62,7 +62,7 @@ def test_sharded_equals_single_process(tmp_path, cmodel, oracle_mod):
     stats = np.load(tmp_path / "stats.npy")
     from zbot_amd import default_config
 
-    env = oracle_mod.OracleEnv(cmodel.cmodel, default_config(), N_GLOBAL, seed=SEED)
+    env = oracle_mod.OracleEnv(cmodel.cmodel, default_config(solver="newton"), N_GLOBAL, seed=SEED)
     env.reset()
     for t in range(STEPS):
         env.step(oracle_mod.synthetic_actions(cmodel.cmodel, SEED, N_GLOBAL, 0, t))

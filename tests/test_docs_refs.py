@@ -31,3 +31,16 @@ def test_cited_profiles_exist(doc):
         if not glob.glob(os.path.join(ROOT, pat)):
             missing.append(p)
     assert not missing, f"{doc} cites missing files: {missing}"
+
+
+def test_boundary_header_states_the_model_limits():
+    """include/zbot.h tells a binding maintainer the collider limits: the number it
+    states is ZB_MAX_GEOM of include/zbot_model.h, and the model version it names is ZB_MODEL_VERSION."""
+    hdr = open(os.path.join(ROOT, "include", "zbot.h")).read()
+    mdl = open(os.path.join(ROOT, "include", "zbot_model.h")).read()
+    max_geom = int(re.search(r"#define ZB_MAX_GEOM\s+(\d+)", mdl).group(1))
+    version = int(re.search(r"#define ZB_MODEL_VERSION\s+(\d+)", mdl).group(1))
+    m = re.search(r"1 to (\d+) floor colliders\s*\*?\s*\(ZB_MAX_GEOM, model version (\d+)", hdr)
+    assert m, "zbot.h no longer states the floor-collider limit"
+    assert int(m.group(1)) == max_geom and int(m.group(2)) == version
+    assert "convex meshes" in hdr and "npair" in hdr

@@ -9,7 +9,7 @@ def test_counting_twin_is_the_twin(cmodel, oracle_mod):
     from zbot_amd import default_config
 
     O = oracle_mod
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     n, seed = 4, 5
     a = O.OracleEnv(cmodel.cmodel, cfg, n, seed=seed)
     b = O.OracleEnv(cmodel.cmodel, cfg, n, seed=seed, precision="flops")

@@ -50,7 +50,7 @@ def test_feet_airtime_exact_rollout_matches_ksim(oracle_mod):
     from zbot_amd import cstructs as cs
     from zbot_amd.engine import HipEngine
 
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     eng = HipEngine(compile_model(), cfg, 256, seed=11)
     eng.reset()
     _rollout(eng, cs, 5, seed=1, mark=False)  # airtime carries and contact history from a first rollout
@@ -87,7 +87,7 @@ def test_feet_airtime_exact_needs_a_marked_step():
     from zbot_amd import compile_model, default_config
     from zbot_amd.engine import HipEngine, ZbError
 
-    eng = HipEngine(compile_model(), default_config(), 8, seed=1)
+    eng = HipEngine(compile_model(), default_config(solver="newton"), 8, seed=1)
     eng.reset()
     r = torch.zeros(8, device="cuda")
     with pytest.raises(ZbError):
@@ -114,7 +114,7 @@ def test_policy_rollout_rows_are_ksim_feet_airtime(oracle_mod):
     cm = compile_model()
     outs = []
     for exact in (True, False):
-        eng = HipEngine(cm, default_config(), 64, seed=3)
+        eng = HipEngine(cm, default_config(solver="newton"), 64, seed=3)
         ro = P.PolicyRollout(eng, P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=4)), seed=6, exact_airtime=exact)
         ro.reset()
         ro.run(12)  # from the reset pose the feet touch down during the first steps: warm up first

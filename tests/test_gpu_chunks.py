@@ -43,7 +43,7 @@ def same(torch, a, b):
 @pytest.mark.parametrize("n,k,push", [(37, 2, True), (37, 7, True), (64, 20, False), (1, 3, True)])
 def test_chunked_step_bit_exact(torch_gpu, cmodel, n, k, push):
     torch = torch_gpu
-    cfg = default_config(push=push, randomize=push)
+    cfg = default_config(solver="newton", push=push, randomize=push)
     ref, chk = make(cmodel, cfg, n, 1), make(cmodel, cfg, n, k)
     ref.reset()
     chk.reset()
@@ -75,7 +75,7 @@ def test_default_chunking(torch_gpu, cmodel, n, push, steps):
     torch = torch_gpu
     from zbot_amd.engine import HipEngine
 
-    cfg = default_config(push=push, randomize=push)
+    cfg = default_config(solver="newton", push=push, randomize=push)
     old = os.environ.pop("ZB_STEP_CHUNKS", None)
     try:
         auto = HipEngine(cmodel, cfg, n, seed=3)
@@ -112,7 +112,7 @@ def test_chunked_step_bit_exact_general_colliders(torch_gpu, oracle_mod, variant
     from zbot_amd import cstructs as cs
 
     cm = compile_model(getattr(U, f"{variant}_desc")())
-    cfg = default_config(push=True, randomize=True)
+    cfg = default_config(solver="newton", push=True, randomize=True)
     n = 37
     ref, chk = make(cm, cfg, n, 1), make(cm, cfg, n, 5)
     env = oracle_mod.OracleEnv(cm.cmodel, cfg, n, seed=3)

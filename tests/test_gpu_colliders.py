@@ -48,7 +48,7 @@ def test_debug_forward_matches_oracle(torch_gpu, variant, oracle_mod):
     from zbot_amd.engine import DBG, HipEngine
 
     name, cm = variant
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     n = 64
     env = contact_env(oracle_mod, cm, cfg, n, seed=5)
     st = env.state.copy()
@@ -152,7 +152,7 @@ def test_rollout_launch_equals_steps(torch_gpu, variant, oracle_mod):
     from zbot_amd.engine import HipEngine
 
     _, cm = variant
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     n, T = 32, 6
     A = torch.from_numpy(np.stack([oracle_mod.synthetic_actions(cm.cmodel, 4, n, 0, t, std=0.5)
                                    for t in range(T)])).cuda()
@@ -187,7 +187,7 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, oracle_mod, name):
     from zbot_amd.engine import HipEngine
 
     cm = compile_model(DESCS[name]())
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     n, steps, seed = 64, 48, 13
     acts = np.stack([oracle_mod.synthetic_actions(cm.cmodel, seed, n, 0, t, std=0.5) for t in range(steps)])
     e32 = oracle_mod.OracleEnv(cm.cmodel, cfg, n, seed=seed)
@@ -250,7 +250,7 @@ def test_full_size_properties(torch_gpu, name):
     from zbot_amd.engine import EnvGroups, HipEngine
 
     cm = compile_model(DESCS[name]())
-    cfg = default_config(push=True, randomize=True)
+    cfg = default_config(solver="newton", push=True, randomize=True)
     n = 8192
     g = torch.Generator(device="cuda")
     g.manual_seed(5)
@@ -293,7 +293,7 @@ def test_many_colliders_match_oracle_within_two(torch_gpu, oracle_mod):
     from zbot_amd.engine import DBG, HipEngine
 
     cm = compile_model(U.many_desc())
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     n = 64
     env = contact_env(oracle_mod, cm, cfg, n, seed=5)
     st = env.state.copy()
@@ -341,7 +341,7 @@ def test_many_colliders_full_size(torch_gpu):
     from zbot_amd.engine import EnvGroups, HipEngine
 
     cm = compile_model(U.many_desc())
-    cfg = default_config(push=True, randomize=True)
+    cfg = default_config(solver="newton", push=True, randomize=True)
     n = 8192
     g = torch.Generator(device="cuda")
     g.manual_seed(5)

@@ -47,7 +47,7 @@ def _run_rank(rank, world, port, outdir):
     from zbot_amd.engine import HipEngine
 
     cm = compile_model()
-    cfg = default_config(push=True, randomize=True)
+    cfg = default_config(solver="newton", push=True, randomize=True)
     off, n = shard(N_GLOBAL, world, rank)
     eng = HipEngine(cm, cfg, n, env_offset=off, seed=SEED)
     eng.reset()
@@ -73,7 +73,7 @@ def test_two_rank_shards_equal_one_process(tmp_path, cmodel, oracle_mod):
 
     mp.start_processes(_run_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
     sharded = np.load(tmp_path / "state.npy")
-    eng = HipEngine(cmodel, default_config(push=True, randomize=True), N_GLOBAL, seed=SEED)
+    eng = HipEngine(cmodel, default_config(solver="newton", push=True, randomize=True), N_GLOBAL, seed=SEED)
     eng.reset()
     for t in range(STEPS):
         eng.step(torch.from_numpy(oracle_mod.synthetic_actions(cmodel.cmodel, SEED, N_GLOBAL, 0, t)).cuda())
@@ -136,7 +136,7 @@ def _run_rccl_rank(rank, world, port, outdir):
     from zbot_amd.engine import HipEngine
 
     cm = compile_model()
-    cfg = default_config(push=True, randomize=True)
+    cfg = default_config(solver="newton", push=True, randomize=True)
     eng = HipEngine(cm, cfg, 64, seed=SEED)
     eng.reset()
     for t in range(STEPS):

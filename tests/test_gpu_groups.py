@@ -36,7 +36,7 @@ def test_grouped_steps_bit_identical(torch_gpu, cmodel, n, G):
     torch = torch_gpu
     from zbot_amd.engine import EnvGroups, HipEngine
 
-    cfg = default_config(push=True, randomize=True, max_episode_sec=0.3)
+    cfg = default_config(solver="newton", push=True, randomize=True, max_episode_sec=0.3)
     one = HipEngine(cmodel, cfg, n, seed=7)
     grp = EnvGroups(cmodel, cfg, n, groups=G, seed=7)
     assert [b - a for a, b in grp.bounds] and grp.bounds[-1][1] == n
@@ -64,7 +64,7 @@ def test_grouped_rollout_and_state_io(torch_gpu, cmodel):
     torch = torch_gpu
     from zbot_amd.engine import EnvGroups, HipEngine
 
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     n = 130
     one = HipEngine(cmodel, cfg, n, seed=4)
     grp = EnvGroups(cmodel, cfg, n, groups=2, seed=4)
@@ -97,7 +97,7 @@ def test_grouped_policy_rollout_bit_identical(torch_gpu, cmodel):
     from zbot_amd import policy as P
     from zbot_amd.engine import EnvGroups, HipEngine
 
-    cfg = default_config(max_episode_sec=0.2)
+    cfg = default_config(solver="newton", max_episode_sec=0.2)
     n, T = 200, 14
     actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0))
     outs = []
@@ -124,7 +124,7 @@ def test_in_loop_critic_matches_post_hoc(torch_gpu, cmodel, G):
     from zbot_amd import policy as P
     from zbot_amd.engine import EnvGroups, HipEngine
 
-    cfg = default_config(max_episode_sec=0.2)
+    cfg = default_config(solver="newton", max_episode_sec=0.2)
     n, T = 150, 12
     actor = P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0), layout=P.LAYOUT_WAVE)
     crit_in = P.GruPolicy(P.CRITIC, P.init_params(P.CRITIC, seed=1), layout=P.LAYOUT_WAVE)
@@ -150,7 +150,7 @@ def test_set_step_chunks_same_bits(torch_gpu, cmodel):
     torch = torch_gpu
     from zbot_amd.engine import HipEngine, ZbError
 
-    cfg = default_config(push=True, max_episode_sec=0.3)
+    cfg = default_config(solver="newton", push=True, max_episode_sec=0.3)
     n = 90
     acts = _actions(torch, cmodel, 8, n, 11)
     states = []
@@ -176,7 +176,7 @@ def test_converted_actions_outlive_step_without_join(torch_gpu, cmodel):
     from zbot_amd.engine import EnvGroups, HipEngine
 
     n = 256
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     one = HipEngine(cmodel, cfg, n, seed=5)
     grp = EnvGroups(cmodel, cfg, n, groups=2, seed=5)
     one.reset()
@@ -202,7 +202,7 @@ def test_airtime_patch_orders_after_caller_writes(torch_gpu, cmodel):
     from zbot_amd.engine import EnvGroups, HipEngine
 
     n, T = 300, 12
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     acts = _actions(torch, cmodel, T, n, 5)
     out = {}
     for name, eng in (("one", HipEngine(cmodel, cfg, n, seed=11)), ("grp", EnvGroups(cmodel, cfg, n, groups=3, seed=11))):

@@ -137,7 +137,7 @@ class MaxErr:
 def test_engine_loads_native_library(torch_gpu, cmodel):
     from zbot_amd import engine as E
 
-    eng = engine(cmodel, default_config(), 4)
+    eng = engine(cmodel, default_config(solver="newton"), 4)
     assert E._lib is not None and os.path.basename(E.LIB_PATH) == "libzbot_hip.so"
     del eng
 
@@ -146,7 +146,7 @@ def test_forward_stages_match_oracle(torch_gpu, cmodel, oracle_mod):
     torch = torch_gpu
     from zbot_amd.engine import DBG
 
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     n = 48
     env = warm_states(oracle_mod, cmodel, cfg, n)
     st = env.state.copy()
@@ -308,11 +308,11 @@ def touchdown_state(oracle_mod, cmodel):
     env 23 of the one-step parity states after the first substep of the third step, where a foot
     corner lies within 1e-7 m above the floor. Returns (state, ctrl, config with one substep)."""
     n = 64
-    cfg = default_config(eulerdamp=True)
+    cfg = default_config(solver="newton", eulerdamp=True)
     env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
     for t in range(2):
         env.step(oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100 + t))
-    c1 = default_config(eulerdamp=True, ctrl_dt=0.001)
+    c1 = default_config(solver="newton", eulerdamp=True, ctrl_dt=0.001)
     o = oracle_mod.OracleEnv(cmodel.cmodel, c1, n, seed=7)
     o.state[:] = env.state
     o.rand[:] = env.rand
@@ -354,7 +354,7 @@ def test_eulerdamp_changes_the_step(torch_gpu, cmodel, oracle_mod):
     qvel by far more than the one-step bound, and the oracle agrees on the difference."""
     torch = torch_gpu
     n = 64
-    on, off = default_config(eulerdamp=True), default_config()
+    on, off = default_config(solver="newton", eulerdamp=True), default_config(solver="newton")
     env = warm_states(oracle_mod, cmodel, off, n, steps=12)
     qv = {}
     for name, cfg in (("on", on), ("off", off)):
@@ -434,7 +434,7 @@ def test_one_step_parity_without_early_exit(torch_gpu, cmodel, oracle_mod):
     tolerance 0 its error is 1.2e-7 (profiles/r04_v1_diag_rand_tol0.log)."""
     torch = torch_gpu
     for push in (False, True):
-        cfg = default_config(push=push, randomize=True)
+        cfg = default_config(solver="newton", push=push, randomize=True)
         cfg.tolerance = 0.0
         n = 64
         env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
@@ -569,7 +569,7 @@ def test_golden_rollout(torch_gpu, cmodel, oracle_mod, name):
 
 def test_deterministic_and_shard_invariant(torch_gpu, cmodel, oracle_mod):
     torch = torch_gpu
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     n = 64
     acts = [torch.from_numpy(oracle_mod.synthetic_actions(cmodel.cmodel, 5, n, 0, t, std=0.1)).cuda() for t in range(6)]
     states = []
@@ -608,7 +608,7 @@ def test_rollout_launch_equals_steps(torch_gpu, cmodel, oracle_mod, solver):
 
 def test_reset_mask_and_autoreset(torch_gpu, cmodel, oracle_mod):
     torch = torch_gpu
-    cfg = default_config(obs_noise=False)
+    cfg = default_config(solver="newton", obs_noise=False)
     n = 16
     eng = engine(cmodel, cfg, n, seed=2)
     eng.reset()
@@ -639,7 +639,7 @@ def test_reset_mask_and_autoreset(torch_gpu, cmodel, oracle_mod):
 
 def test_full_size_properties(torch_gpu, cmodel):
     torch = torch_gpu
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     n = 8192
     g = torch.Generator(device="cuda")
     g.manual_seed(0)
@@ -672,7 +672,7 @@ def test_full_size_configs(torch_gpu, cmodel, n, push, randomize):
     shard-invariant (two half-size handles with env_offset give the same bits), finite,
     unit quaternions, and the standing task keeps nearly every env up."""
     torch = torch_gpu
-    cfg = default_config(push=push, randomize=randomize)
+    cfg = default_config(solver="newton", push=push, randomize=randomize)
     g = torch.Generator(device="cuda")
     g.manual_seed(3)
     bias = torch.tensor([cmodel.cmodel.joint_bias[i] for i in range(20)], device="cuda")
@@ -728,7 +728,7 @@ def test_mjcf_variant_model_parity(torch_gpu, cmodel_mjcf, oracle_mod):
     the oracle on the same model (tolerances as test_one_step_parity)."""
     torch = torch_gpu
     cm = cmodel_mjcf
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     n = 32
     env = warm_states(oracle_mod, cm, cfg, n, steps=8)
     eng = engine(cm, cfg, n, seed=7)
@@ -763,7 +763,7 @@ def test_team_divergence_is_exact(torch_gpu, cmodel, oracle_mod):
     (The contact Hessian's J'DJ runs on the matrix cores with operands from all 64
     lanes, so a team that sits out must still run forward() as a ghost.)"""
     torch = torch_gpu
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     acts = [torch.from_numpy(oracle_mod.synthetic_actions(cmodel.cmodel, 3, 34, 0, t)).cuda() for t in range(4)]
     res = {}
     for n in (33, 34):
@@ -788,7 +788,7 @@ def test_team_divergence_is_exact(torch_gpu, cmodel, oracle_mod):
     sa, sb = A.get_state().cpu().numpy(), B.get_state().cpu().numpy()
     assert np.array_equal(sa[::2], sb[::2]) and np.array_equal(oa[::2], ob[::2])
     # one env of a wave auto-resets while its partner steps on: both match the oracle
-    cfg2 = default_config(obs_noise=False)
+    cfg2 = default_config(solver="newton", obs_noise=False)
     n = 8
     env = warm_states(oracle_mod, cmodel, cfg2, n, steps=6)
     st = env.state.copy()
@@ -813,7 +813,7 @@ def test_empty_and_single_env_handles(torch_gpu, cmodel, oracle_mod):
     whose shard is empty), and a single env (one team of a wave, the other a ghost) steps like
     the oracle."""
     torch = torch_gpu
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     e0 = engine(cmodel, cfg, 0, seed=1)
     out = e0.reset()
     out = e0.step(torch.zeros(0, 20, device="cuda"))

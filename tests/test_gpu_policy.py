@@ -91,7 +91,7 @@ def test_policy_in_the_rollout_loop(pol, cmodel):
 
     runs = []
     for _ in range(2):
-        eng = HipEngine(cmodel, default_config(), 64, seed=2)
+        eng = HipEngine(cmodel, default_config(solver="newton"), 64, seed=2)
         ro = pol.PolicyRollout(eng, pol.GruPolicy(ACTOR, init_params(ACTOR, seed=8)), seed=5)
         out = ro.run(6)
         torch.cuda.synchronize()
@@ -147,7 +147,7 @@ def test_rollout_step_graph_capture(pol):
     P = init_params(ACTOR, seed=2)
     runs = []
     for mode in ("eager", "graph"):
-        eng = HipEngine(cm, default_config(), n, seed=4)
+        eng = HipEngine(cm, default_config(solver="newton"), n, seed=4)
         eng.reset()
         actor = pol.GruPolicy(ACTOR, P)
         carry = actor.initial_carry(n)
@@ -183,7 +183,7 @@ def test_rollout_records_critic_obs_of_acted_states(pol, cmodel):
     from zbot_amd import default_config
     from zbot_amd.engine import HipEngine, ZbError
 
-    eng = HipEngine(cmodel, default_config(), 32, seed=6)
+    eng = HipEngine(cmodel, default_config(solver="newton"), 32, seed=6)
     ro = pol.PolicyRollout(eng, pol.GruPolicy(ACTOR, init_params(ACTOR, seed=1)), seed=2)
     ro.reset()
     reset_c = eng.obs_critic.clone()

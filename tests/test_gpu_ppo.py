@@ -90,7 +90,7 @@ def test_rollout_buffers_from_zb_step(ppo, oracle_mod, cmodel):
     from zbot_amd.engine import HipEngine
 
     T, n = 12, 64
-    eng = HipEngine(cmodel, default_config(), n, seed=4)
+    eng = HipEngine(cmodel, default_config(solver="newton"), n, seed=4)
     eng.reset()
     rew = torch.zeros(T, n, device="cuda")
     done = torch.zeros(T, n, dtype=torch.uint8, device="cuda")

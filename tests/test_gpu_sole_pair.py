@@ -125,7 +125,7 @@ def test_rollout_launch_equals_steps(torch_gpu, pair_model, oracle_mod):
     from zbot_amd.engine import HipEngine
 
     cm = pair_model
-    cfg = default_config(push=True)
+    cfg = default_config(solver="newton", push=True)
     n, T = 32, 6
     A = torch.from_numpy(np.stack([oracle_mod.synthetic_actions(cm.cmodel, 4, n, 0, t, std=0.3)
                                    for t in range(T)])).cuda()
@@ -214,7 +214,7 @@ def test_full_size_properties(torch_gpu, pair_model):
     from zbot_amd.engine import EnvGroups, HipEngine
 
     cm = pair_model
-    cfg = default_config(push=True, randomize=True)
+    cfg = default_config(solver="newton", push=True, randomize=True)
     n = 8192
     g = torch.Generator(device="cuda")
     g.manual_seed(5)

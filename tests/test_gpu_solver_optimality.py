@@ -21,7 +21,7 @@ def test_engine_qacc_is_the_minimizer(cmodel, oracle_mod):
         pytest.skip("no GPU")
     from zbot_amd.engine import DBG, HipEngine
 
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     st = P.states(oracle_mod, cmodel, cfg)
     n = st.shape[0]
     rng = np.random.default_rng(0)

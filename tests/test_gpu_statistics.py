@@ -29,7 +29,7 @@ def runs(request, cmodel, oracle_mod):
     from zbot_amd.engine import HipEngine
 
     push, randomize = request.param
-    cfg = default_config(push=push, randomize=randomize)
+    cfg = default_config(solver="newton", push=push, randomize=randomize)
     ref = oracle_mod.OracleEnv(cmodel.cmodel, cfg, N, seed=11)
     ref.reset()
     eng = HipEngine(cmodel, cfg, N, seed=11)
@@ -98,7 +98,7 @@ def test_long_soak_full_size(cmodel):
     from zbot_amd.engine import HipEngine
 
     n, steps = 8192, 1500
-    cfg = default_config(push=True, randomize=True)
+    cfg = default_config(solver="newton", push=True, randomize=True)
     eng = HipEngine(cmodel, cfg, n, seed=5)
     eng.reset()
     g = torch.Generator(device="cuda")

@@ -31,7 +31,7 @@ def test_success_flags_match_oracle(torch_gpu, cmodel, oracle_mod):
     torch = torch_gpu
     from zbot_amd.engine import HipEngine
 
-    cfg = default_config(max_episode_sec=MAX_SEC)
+    cfg = default_config(solver="newton", max_episode_sec=MAX_SEC)
     n = 40
     ref = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=5)
     ref.reset()
@@ -61,7 +61,7 @@ def test_rollout_success_is_last_step(torch_gpu, cmodel):
     torch = torch_gpu
     from zbot_amd.engine import HipEngine
 
-    cfg = default_config(max_episode_sec=MAX_SEC)
+    cfg = default_config(solver="newton", max_episode_sec=MAX_SEC)
     n = 16
     a = torch.from_numpy(np.tile(_bias(cmodel, n), (5, 1, 1))).cuda()
     e1 = HipEngine(cmodel, cfg, n, seed=2)
@@ -84,7 +84,7 @@ def test_policy_rollout_successes_feed_gae(torch_gpu, cmodel, oracle_mod):
     from zbot_amd import ppo
     from zbot_amd.engine import HipEngine
 
-    cfg = default_config(max_episode_sec=MAX_SEC)
+    cfg = default_config(solver="newton", max_episode_sec=MAX_SEC)
     n, T = 64, 12
     eng = HipEngine(cmodel, cfg, n, seed=9)
     ro = P.PolicyRollout(eng, P.GruPolicy(P.ACTOR, P.init_params(P.ACTOR, seed=0)), seed=1)
@@ -113,7 +113,7 @@ def test_bad_buffers_raise_before_the_kernel(torch_gpu, cmodel):
     from zbot_amd.cstructs import RAND_STRIDE
     from zbot_amd.engine import HipEngine, ZbError
 
-    eng = HipEngine(cmodel, default_config(), 8)
+    eng = HipEngine(cmodel, default_config(solver="newton"), 8)
     eng.reset()
     with pytest.raises(ZbError):
         eng.set_rand(torch.zeros(4, RAND_STRIDE))  # short: would read past its end

@@ -470,12 +470,12 @@ def test_skipped_colliders_are_rejected_by_zb_create():
     assert [g["name"] for g in desc["skipped_geoms"]] == ["shin_col"]
     cm = compile_model(desc)
     assert cm.cmodel.nskip_geom == 1
-    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc == -4 and b"colliding geoms" in L.zb_last_error()
     for cm in (compile_model(desc, drop_colliders=True), compile_model(with_shin("capsule")),
                compile_model(with_shin("cylinder")), compile_model(with_shin("ellipsoid"))):
         assert cm.cmodel.nskip_geom == 0
-        rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+        rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
         assert rc != -4, L.zb_last_error()  # validation passes (no device here: -2)
         if rc == 0:
             L.zb_destroy(h)
@@ -591,7 +591,7 @@ def test_self_contacts_are_rejected_by_zb_create():
     h = C.c_void_p()
     cm = compile_model(desc)
     assert cm.cmodel.nskip_pair == 0 and cm.cmodel.npair == 1
-    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc != -4, L.zb_last_error()
     if rc == 0:
         L.zb_destroy(h)
@@ -603,11 +603,11 @@ def test_self_contacts_are_rejected_by_zb_create():
     assert len(desc["self_pairs"]) >= 2
     cm = compile_model(desc)
     assert cm.cmodel.nskip_pair == len(desc["self_pairs"]) and cm.cmodel.npair == 0
-    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc == -4 and b"pairs of its own geoms" in L.zb_last_error()
     cm = compile_model(desc, drop_self_contacts=True)
     assert cm.cmodel.nskip_pair == 0 and cm.cmodel.npair == 0
-    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = L.zb_create(C.byref(cm.cmodel), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc != -4, L.zb_last_error()
     if rc == 0:
         L.zb_destroy(h)

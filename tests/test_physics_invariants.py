@@ -28,7 +28,7 @@ def _random_qpos(cm, rng, scale=0.3):
 
 
 def test_free_fall_exact(oracle_mod, cmodel):
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     q = cmodel.reset_qpos().astype(np.float32)
     q[2] = 2.0
     n = 100
@@ -44,7 +44,7 @@ def test_free_fall_exact(oracle_mod, cmodel):
 def test_mass_matrix_matches_jacobian_form(oracle_mod, cmodel, seed):
     rng = np.random.default_rng(seed)
     q = _random_qpos(cmodel, rng)
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     d = oracle_mod.forward_debug(cmodel.cmodel, cfg, q, np.zeros(26), precision="f64")
     arm = np.array([cmodel.cmodel.dof_armature[i] for i in range(26)])
     M_ref = mass_matrix(cmodel.bodies, q, 26, cmodel.dof_body, arm)
@@ -58,7 +58,7 @@ def test_mass_matrix_matches_jacobian_form(oracle_mod, cmodel, seed):
 def test_gravity_bias_matches_jacobian_form(oracle_mod, cmodel, seed):
     rng = np.random.default_rng(seed)
     q = _random_qpos(cmodel, rng)
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     d = oracle_mod.forward_debug(cmodel.cmodel, cfg, q, np.zeros(26), precision="f64")
     xpos, xmat = _kinematics(cmodel.bodies, q)
     g = np.array([0.0, 0.0, -9.81])
@@ -81,7 +81,7 @@ def test_mjcf_variant_dynamics_match_jacobian_form(oracle_mod, cmodel_mjcf, seed
     assert any(list(cm.cmodel.body_iquat[i]) != [1.0, 0.0, 0.0, 0.0] for i in range(len(cm.bodies)))
     rng = np.random.default_rng(seed)
     q = _random_qpos(cm, rng)
-    d = oracle_mod.forward_debug(cm.cmodel, default_config(), q, np.zeros(26), precision="f64")
+    d = oracle_mod.forward_debug(cm.cmodel, default_config(solver="newton"), q, np.zeros(26), precision="f64")
     arm = np.array([cm.cmodel.dof_armature[i] for i in range(26)])
     np.testing.assert_allclose(d["qM"], mass_matrix(cm.bodies, q, 26, cm.dof_body, arm), rtol=1e-5, atol=1e-7)
     xpos, xmat = _kinematics(cm.bodies, q)
@@ -105,7 +105,7 @@ def _conservative_model(cmodel):
 
 def test_energy_and_momentum_conservation(oracle_mod, cmodel):
     m = _conservative_model(cmodel)
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     rng = np.random.default_rng(5)
     q = cmodel.reset_qpos().astype(np.float64)
     q[2] = 3.0
@@ -125,7 +125,7 @@ def test_energy_and_momentum_conservation(oracle_mod, cmodel):
 
 
 def test_static_stand_supports_weight(oracle_mod, cmodel):
-    cfg = default_config(obs_noise=False)
+    cfg = default_config(solver="newton", obs_noise=False)
     env = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 4, seed=0)
     env.reset()
     bias = np.array([cmodel.cmodel.joint_bias[a] for a in range(20)], np.float32)
@@ -140,7 +140,7 @@ def test_static_stand_supports_weight(oracle_mod, cmodel):
 
 
 def test_quaternion_norm_preserved(oracle_mod, cmodel):
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     env = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 8, seed=1)
     env.reset()
     for t in range(10):
@@ -151,7 +151,7 @@ def test_quaternion_norm_preserved(oracle_mod, cmodel):
 
 def test_f32_oracle_tracks_f64(oracle_mod, cmodel):
     """The fp32 oracle (CPU baseline) stays close to the fp64 build for one env-step."""
-    cfg = default_config(obs_noise=False)
+    cfg = default_config(solver="newton", obs_noise=False)
     a = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 8, seed=2)
     b = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 8, seed=2, precision="f64")
     a.reset()
@@ -175,7 +175,7 @@ def test_eulerdamp_is_mj_euler_implicit_damping(oracle_mod, cmodel):
     qv = np.concatenate([rng.normal(0, 0.3, 6), rng.normal(0, 2.0, 20)]).astype(np.float32)
     ctrl = rng.normal(0, 0.5, 20).astype(np.float32)
     dt = 0.001
-    on, off = default_config(eulerdamp=True), default_config()
+    on, off = default_config(solver="newton", eulerdamp=True), default_config(solver="newton")
     assert on.flags & cs.F_EULERDAMP and not off.flags & cs.F_EULERDAMP
     p = oracle_mod.constraint_problem(cmodel.cmodel, on, q, qv, ctrl=ctrl, precision="f64")
     M, qacc = p["qM"].astype(np.float64), p["qacc"].astype(np.float64)
@@ -202,7 +202,7 @@ def test_eulerdamp_stable_past_the_explicit_limit(oracle_mod, cmodel):
     q[2] = 2.0
     qv = np.zeros(26, np.float32)
     qv[6:] = 1.0
-    _, v_on, _ = oracle_mod.simulate(m, default_config(eulerdamp=True), q, qv, 50, precision="f64")
-    _, v_off, _ = oracle_mod.simulate(m, default_config(), q, qv, 50, precision="f64")
+    _, v_on, _ = oracle_mod.simulate(m, default_config(solver="newton", eulerdamp=True), q, qv, 50, precision="f64")
+    _, v_off, _ = oracle_mod.simulate(m, default_config(solver="newton"), q, qv, 50, precision="f64")
     assert np.isfinite(v_on).all() and np.abs(v_on[6:]).max() < 1.0
     assert not (np.isfinite(v_off).all() and np.abs(v_off[6:]).max() < 1e3)

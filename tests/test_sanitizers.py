@@ -25,7 +25,7 @@ def _blobs(tmp_path, cm, **cfg_kw):
 
     m, c = tmp_path / "model.bin", tmp_path / "config.bin"
     m.write_bytes(bytes(cm.cmodel))
-    c.write_bytes(bytes(default_config(**cfg_kw)))
+    c.write_bytes(bytes(default_config(solver="newton", **cfg_kw)))
     return str(m), str(c)
 
 
@@ -63,7 +63,7 @@ def test_host_validation_rejects_bad_indices(tmp_path, cmodel):
         else:
             getattr(bad, field)[idx] = val
         h = C.c_void_p()
-        rc = L.zb_create(C.byref(bad), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+        rc = L.zb_create(C.byref(bad), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
         assert rc == -4, (field, rc, L.zb_last_error())
 
 

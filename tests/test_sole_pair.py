@@ -43,10 +43,10 @@ def test_other_self_pairs_are_still_refused():
     assert m.npair == 0 and m.nskip_pair == 2
     L = E.load_library()
     h = C.c_void_p()
-    assert L.zb_create(C.byref(m), C.byref(default_config()), 4, 0, 0, 0, C.byref(h)) == -4
+    assert L.zb_create(C.byref(m), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h)) == -4
     # the sole pair alone passes the model checks (no GPU here: zb_create stops at the device, not at -4)
     ok = compile_model(U.sole_pair_desc()).cmodel
-    rc = L.zb_create(C.byref(ok), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    rc = L.zb_create(C.byref(ok), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h))
     assert rc != -4, L.zb_last_error()
     if rc == 0:
         L.zb_destroy(h)
@@ -58,7 +58,7 @@ def test_pair_rows_are_internal_and_repulsive(oracle_mod):
     few substeps reduce the soles' interpenetration."""
     cm = compile_model(U.sole_pair_desc())
     free = compile_model(U.sole_pair_desc(), drop_self_contacts=True)
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     qs = U.crossing_states(cm, 12, seed=3)
     seen = 0
     for q in qs:

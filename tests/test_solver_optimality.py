@@ -15,7 +15,7 @@ from zbot_amd import default_config
 
 
 def test_oracle_newton_solution_is_the_minimizer(oracle_mod, cmodel):
-    cfg = default_config()
+    cfg = default_config(solver="newton")
     st = P.states(oracle_mod, cmodel, cfg)
     rng = np.random.default_rng(0)
     kinds = np.zeros(3, int)

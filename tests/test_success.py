@@ -18,7 +18,7 @@ def _bias(cm, n):
 
 
 def test_time_limit_sets_success_unless_failed(oracle_mod, cmodel):
-    cfg = default_config(obs_noise=False, max_episode_sec=MAX_SEC)
+    cfg = default_config(solver="newton", obs_noise=False, max_episode_sec=MAX_SEC)
     n = 6
     env = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=0)
     env.reset()
@@ -36,7 +36,7 @@ def test_time_limit_sets_success_unless_failed(oracle_mod, cmodel):
 
 
 def test_failure_alone_is_not_success(oracle_mod, cmodel):
-    cfg = default_config(obs_noise=False)
+    cfg = default_config(solver="newton", obs_noise=False)
     env = oracle_mod.OracleEnv(cmodel.cmodel, cfg, 2, seed=0)
     env.reset()
     env.state[1, 2] = 0.7
