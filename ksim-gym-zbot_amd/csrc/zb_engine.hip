@@ -1258,6 +1258,41 @@ __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
  * factor_ldl (slots NROOT.. of the stored rows): forward z_p = b_p +
  * sum_{k > p} W(p, k) b_k, backward x_p = v_p + sum_{a < p} W(a, p) v_a. The
  * root chain is dense and redundant in every lane. */
+/* The root block's coupling of this lane for solve_ldl<true> (CG: the factor of M is fixed for the
+ * substep's ~10 solves). R^-1 = L_r^-1 D_r^-1 L_r^-T is the inverse of the factored 6 x 6 root block
+ * (the dense passes of solve_ldl); root lane j stores u = R^-1 e_j (row j of the symmetric R^-1), a
+ * limb lane u = -R^-1 w with w its root entries L(j, root), a non-dof lane zero, in Hs[lane][0..5]
+ * (CG builds no Hessian; the rows share memory with sub[], so the caller runs this after the last
+ * subtree sum of the smooth phase, rne_project, and before the sensors'). A solve then ends in
+ * x_j = [limb] x_j / D_j + sum_k u_k sr_k, sr the root right-hand sides of the team reduction: one
+ * 6-term product instead of the dense passes' dependent chain (the same arithmetic, another order). */
+__device__ __forceinline__ void root_coupling(const Ctx& c) {
+  EnvL* L = c.L;
+  const bool isroot = c.l < NROOT, ischain = c.chd >= 0;
+  float w[CAP];
+  ld_row(&L->L[c.l & 31][0], w);
+  float xr[RMAX];
+#pragma unroll
+  for (int k = 0; k < RMAX; k++) xr[k] = isroot ? (c.l == k ? 1.f : 0.f) : (ischain ? -w[k] : 0.f);
+#pragma unroll
+  for (int k = RMAX - 1; k >= 1; k--)
+#pragma unroll
+    for (int i = 0; i < k; i++) xr[i] -= L->L[k][i] * xr[k];
+#pragma unroll
+  for (int k = 0; k < RMAX; k++) xr[k] *= L->Di[k];
+#pragma unroll
+  for (int k = 1; k < RMAX; k++)
+#pragma unroll
+    for (int a = 0; a < k; a++) xr[k] -= L->L[k][a] * xr[a];
+  tsync(); /* sub[] (same memory) is read by other lanes up to here */
+  static_assert(RMAX == 6, "u in one 16-byte and one 8-byte store");
+  *reinterpret_cast<v4f*>(&L->Hs[c.l & 31][0]) = v4f{xr[0], xr[1], xr[2], xr[3]};
+  L->Hs[c.l & 31][4] = xr[4];
+  L->Hs[c.l & 31][5] = xr[5];
+  tsync();
+}
+
+template <bool PRE = false>
 __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   EnvL* L = c.L;
   const int nroot = NROOT;
@@ -1289,6 +1324,16 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
     float sr[RMAX];
 #pragma unroll
     for (int k = 0; k < RMAX; k++) sr[k] = c.l == k ? x : -w[k] * xs;
+    if constexpr (PRE) {
+      /* root_coupling's u: loaded while the reduction runs */
+      const v4f u4 = *reinterpret_cast<const v4f*>(&L->Hs[c.l & 31][0]);
+      const float u[RMAX] = {u4[0], u4[1], u4[2], u4[3], L->Hs[c.l & 31][4], L->Hs[c.l & 31][5]};
+      tsum_n<RMAX>(sr);
+      float y = xs * Dinv; /* limb lanes; a root lane's value is all coupling, a non-dof lane's zero */
+#pragma unroll
+      for (int k = 0; k < RMAX; k++) y += u[k] * sr[k];
+      x = y;
+    } else {
     tsum_n<RMAX>(sr);
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
@@ -1314,6 +1359,7 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
       if (c.l == k && k < nroot) x = xr[k];
+    }
   } else {
     x *= Dinv;
   }
@@ -2496,7 +2542,9 @@ __device__ __forceinline__ float colsum16(JP Jrow, float fr) {
 /* forces/activity at current jar, qfrc_constraint, grad, total cost */
 /* returns this lane's cost share; the caller reduces it over the team (alone, or together with
    the Newton loop's other per-iteration sums in one tsum_n) */
-template <int XG, bool XA = true>
+/* HS: the rows' force and active D are also stored in LDS for the Newton Hessian (hessian_factor,
+   jdj_mfma); CG builds no Hessian and skips the stores */
+template <int XG, bool XA = true, bool HS = true>
 __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, const float jr[CAP], float qacc,
                                                        float qs, float fs, float Ma, float& grad) {
   const int ddep = vopq(c.ddep);
@@ -2524,8 +2572,10 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
       r.actl = r.hl ? a2 : r.actl;
     }
   }
-  if (r.ex) L->rowF[c.l] = r.f;
-  L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
+  if constexpr (HS) {
+    if (r.ex) L->rowF[c.l] = r.f;
+    L->rowDA[c.l] = (r.ex && r.act) ? r.D : 0.f; /* every row: read by jdj_mfma */
+  }
   float sx0 = 0.f, sx1 = 0.f;
   if (XG && XA && r.x.any) {
     float f3;
@@ -2557,10 +2607,10 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
   grad = Ma - fs - qc;
   return cost;
 }
-template <int XG, bool XA = true>
+template <int XG, bool XA = true, bool HS = true>
 __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, const float jr[CAP], float qacc, float qs,
                                                   float fs, float Ma, float& grad) {
-  return tsum(update_constraint_lane<XG, XA>(c, r, jr, qacc, qs, fs, Ma, grad));
+  return tsum(update_constraint_lane<XG, XA, HS>(c, r, jr, qacc, qs, fs, Ma, grad));
 }
 
 /* G_f = sum_{r in foot f} D_r J_r J_r' (depth-indexed 12x12) for both feet of
@@ -3050,9 +3100,9 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   r.jl = r.sl * x - r.al;
   const float scale = 1.0f / (m->meaninertia * (float)(NV > 1 ? NV : 1));
   float grad;
-  float cost = update_constraint<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
+  float cost = update_constraint<XG, XA, false>(c, r, jr, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
-  float mg = solve_ldl(c, grad, DinvM);
+  float mg = solve_ldl<true>(c, grad, DinvM);
   STAMP(S_SOLVE0);
   float search = -mg;
   int it = 0;
@@ -3070,7 +3120,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
-    const float cl = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
+    const float cl = update_constraint_lane<XG, XA, false>(c, r, jr, x, qs, fs, Ma, grad);
     STAMP(S_UPD);
     it++;
     /* MJX's order (solver.py: _update_gradient, then the Polak-Ribiere beta, then the termination
@@ -3079,7 +3129,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
        (the same DPP sequence per value: the bits of separate sums). An iteration at the cap skips the
        solve and the beta sums, which only feed the next iteration. */
     if (it < itmax) {
-      mg = solve_ldl(c, grad, DinvM);
+      mg = solve_ldl<true>(c, grad, DinvM);
       STAMP(S_SOLVE);
       float red[4] = {cl, c.l < NV ? grad * grad : 0.f, c.l < NV ? grad * (mg - mgold) : 0.f,
                       c.l < NV ? gold * mgold : 0.f};
@@ -3177,7 +3227,9 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   const float damp = keepf(c.L->par[P_DAMP][c.l & 31]);
   float fs = (c.l < NV) ? (-damp * ls.v - bias + act) : 0.f;
   STAMP(S_RNE);
-  float qs = solve_ldl(c, fs, DinvM);
+  constexpr bool PRE = SOLVER == ZB_SOLVER_CG; /* CG's ~10 solves with M's factor per substep */
+  if constexpr (PRE) root_coupling(c);
+  float qs = solve_ldl<PRE>(c, fs, DinvM);
   STAMP(S_SOLVES);
   /* constraints */
   make_constraints<XG>(c, s, ls, B, cm, r);

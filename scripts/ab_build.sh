@@ -10,6 +10,12 @@ NAME=$1; REV=${2:-cur}; shift 2 || true
 mkdir -p "$OUT"
 make -C "$CSRC" -s
 SRC=$CSRC/zb_engine.hip
+if [ "$REV" = cur ] && [ $# -eq 0 ] && [ -z "${SLP+x}" ]; then
+  # the working tree with the product flags: the product library just built is that variant
+  cp "$ROOT/ksim-gym-zbot_amd/zbot_amd/libzbot_hip.so" "$OUT/libeng_$NAME.so"
+  echo "built $OUT/libeng_$NAME.so (the product build)"
+  exit 0
+fi
 if [ "$REV" = file ]; then SRC=$1; shift;
 elif [ "$REV" != cur ]; then SRC=$OUT/zb_engine_$NAME.hip; git -C "$ROOT" show "$REV:ksim-gym-zbot_amd/csrc/zb_engine.hip" > "$SRC"; fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -I"$CSRC" -fno-signed-zeros \

@@ -59,6 +59,8 @@ def main() -> None:
     ap.add_argument("--out", default=None)
     ap.add_argument("--kernel", default="step_kernel", help="kernel name substring (gae_kernel for the PPO leg)")
     ap.add_argument("--T", type=int, default=0, help="rollout length of a gae_kernel launch")
+    ap.add_argument("--solver", default=None, help="the step kernel's solver (recorded; bench.py reads traffic only "
+                                                   "for a matching --solver)")
     args = ap.parse_args()
     global KERNEL
     KERNEL = args.kernel
@@ -84,6 +86,8 @@ def main() -> None:
         "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section), WRITE_SIZE as read; "
                       "Infinity-Cache hits included (upper bound on DRAM bytes)",
     }
+    if args.solver:
+        res["solver"] = args.solver
     if args.T:
         res["T"] = args.T
         res["hbm_bytes_per_element"] = hbm / (args.T * args.envs)
@@ -95,6 +99,9 @@ def main() -> None:
             if name in va:
                 fl[name] = med(va[name])
         res["valu_insts_per_launch"] = {k: med(v) for k, v in va.items()}
+        if "SQ_WAVES" in va:
+            w = med(va["SQ_WAVES"])
+            res["insts_per_wave"] = {k.replace("SQ_INSTS_", ""): med(v) / w for k, v in va.items() if k != "SQ_WAVES"}
         if fl:
             flop = sum(fl[k] * (128 if k.endswith("FMA_F32") else 64) for k in fl)
             res["issued_fp32_flop_per_launch"] = flop

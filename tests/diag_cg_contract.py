@@ -42,6 +42,18 @@ def main():
         eng.set_state(torch.from_numpy(env.state.copy()))
         eng.set_rand(torch.from_numpy(env.rand.copy()))
         act = O.synthetic_actions(cm.cmodel, 7, n, 0, 100 + t)
+        # the step's sensitivity to a rounding-level input change: the fp32 oracle from the state with
+        # qvel scaled by 1 +- 2^-23 per component (3 draws), the largest output change per env
+        pert = []
+        rng = np.random.default_rng(100 + t)
+        for _ in range(3):
+            ep = O.OracleEnv(cm.cmodel, cfg, n, seed=7)
+            ep.state[:] = env.state
+            ep.rand[:] = env.rand
+            sgn = rng.choice([-1.0, 1.0], size=(n, 26)).astype(np.float32)
+            ep.state[:, 32:58] *= (1.0 + sgn * np.float32(2.0 ** -23))
+            rp = ep.step(act)
+            pert.append({k: want for k, _, want in one_step_outputs(ep.state, rp, ep.state, rp)})
         ref, ref64 = oracle_steps(O, cm, cfg, env, act, 7)
         out = eng.step(torch.from_numpy(act).cuda())
         torch.cuda.synchronize()
@@ -52,6 +64,9 @@ def main():
             w64 = np.asarray(ref64[key], np.float64).reshape(n, -1)
             tol = ONE_STEP_TOL[key][0]
             gap = np.abs(w32 - w64).max(1)
+            pg = np.max([np.abs(np.asarray(pp[key], np.float64).reshape(n, -1) - w32).max(1) for pp in pert], axis=0)
+            sens = np.maximum(gap, pg)
+            overs = [int((np.abs(got - w32).max(1) > tol + k * sens).sum()) for k in ks]
             e32 = np.abs(got - w32).max(1)
             e64 = np.abs(got - w64).max(1)
             over32 = [int((e32 > tol + k * gap).sum()) for k in ks]
@@ -59,7 +74,8 @@ def main():
             ratio = np.max((e64 - tol) / np.maximum(gap, 1e-30))
             print(f"step {t} {key:12s} tol {tol:.0e} | max e32 {e32.max():.2e} e64 {e64.max():.2e} gap {gap.max():.2e} "
                   f"| over tol+k*gap vs f32 {over32} vs f64 {over64} | worst (e64-tol)/gap {ratio:.2f} "
-                  f"| envs e64>tol+2gap {np.flatnonzero(e64 > tol + 2 * gap).tolist()[:8]}")
+                  f"| envs e64>tol+2gap {np.flatnonzero(e64 > tol + 2 * gap).tolist()[:8]} | pert {pg.max():.2e} over tol+k*sens vs f32 {overs} "
+                  f"envs {np.flatnonzero(e32 > tol + 2 * sens).tolist()[:8]}")
 
 
 if __name__ == "__main__":

@@ -80,20 +80,25 @@ class MaxErr:
         self.max_ill = max_ill
         self.over = set()  # envs over the bound in the last add() calls (cleared by take_over())
 
-    def add(self, key, got, ref, tol, rtol=0.0, ref64=None, loose_abs=None):
+    def add(self, key, got, ref, tol, rtol=0.0, ref64=None, loose_abs=None, sens=None):
         """Record |got - ref| against tol + rtol |ref| elementwise (rows = envs; asserted in
         report(), after every output has been measured). ref64: the fp64 oracle's value of the same
         step. An env whose fp32 and fp64 oracles already disagree sits at a discontinuity of the
         step (a contact or active-set switch) where any rounding picks a side: its rows get
         2 |ref - ref64| of slack, and the report counts them. loose_abs: the budget envs' absolute
-        limit for this output (default loose x tol)."""
+        limit for this output (default loose x tol). sens: a per-env sensitivity of the step to a
+        rounding-level input change (oracle_sensitivity); the slack is then twice the larger of it and
+        the fp32/fp64 gap."""
         got = np.asarray(got, np.float64)
         ref = np.asarray(ref, np.float64)
         d = np.abs(got - ref)
         slack = 0.0
         if ref64 is not None:
             gap = np.abs(ref - np.asarray(ref64, np.float64))
-            slack = 2.0 * gap.reshape(gap.shape[0], -1).max(1).reshape((-1,) + (1,) * (gap.ndim - 1))
+            gap = gap.reshape(gap.shape[0], -1).max(1)
+            if sens is not None:
+                gap = np.maximum(gap, np.asarray(sens, np.float64).reshape(-1))
+            slack = 2.0 * gap.reshape((-1,) + (1,) * (ref.ndim - 1))
             ill = np.asarray(slack).reshape(-1) > tol
             if self.exempt_ill:
                 slack = np.where(ill.reshape(slack.shape), np.inf, slack)
@@ -240,6 +245,29 @@ def oracle_steps(O, cm, cfg, env, a, seed):
     ref64 = {k: want for k, _, want in one_step_outputs(e64.state, r64, e64.state, r64)}
     ref64["_iters"] = e64.iters.copy()
     return ref, ref64
+
+
+def oracle_sensitivity(O, cm, cfg, state, rand, a, seed, ref, draws=3):
+    """The step's sensitivity to a rounding-level change of its input, per output and env: the fp32
+    oracle stepped from the same state with every qvel component scaled by 1 +- 2^-23 (one fp32 ulp,
+    `draws` random sign patterns), the largest |output - ref| over the draws (ref: the unperturbed
+    fp32 step's outputs, {output: value}). For CG this is the scale of the disagreement between any
+    two fp32 implementations of the same unconverged 8-iteration solve: an
+    env whose solve amplifies one ulp into 1e-4 of qvel would part from any other fp32 CG by as much."""
+    rng = np.random.default_rng(seed * 7919 + int(state[:, cs.S_RNG_STEP].view(np.uint32).sum()) % 65521)
+    n = state.shape[0]
+    sens = {}
+    for _ in range(draws):
+        ep = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
+        ep.state[:] = state
+        ep.rand[:] = rand
+        sgn = rng.choice([-1.0, 1.0], size=(n, 26)).astype(np.float32)
+        ep.state[:, 32:58] *= (np.float32(1.0) + sgn * np.float32(2.0 ** -23))
+        rp = ep.step(a)
+        for key, _, want in one_step_outputs(ep.state, rp, ep.state, rp):
+            d = np.abs(np.asarray(want, np.float64) - np.asarray(ref[key], np.float64)).reshape(n, -1).max(1)
+            sens[key] = np.maximum(sens.get(key, 0.0), d)
+    return sens
 
 
 def print_budget_envs(err, t, eng, env, ref64, gs):
