@@ -400,12 +400,17 @@ def bench_general_colliders(cfg, n: int, steps: int, warmup: int, dev, rank: int
 
     wall = _timed_steps(lambda t: eng.step(acts[t % 64], extras=False), steps, warmup, dev, world)
     eng.check()
-    return {
+    out = {
         "workload": f"C2 on {os.path.relpath(path, ROOT)} ({len(cm.geom_names)} floor colliders "
                     f"{cm.geom_names}), {n} envs/GPU, {groups} env groups, {steps} timed steps (after {warmup})",
         "env_steps_per_s": world * n * steps / wall,
         "ms_per_step": 1e3 * wall / steps,
     }
+    if len(cm.geom_names) > 4:
+        # the second bank's two-geom cap (select_bank2): envs that ever had more than two colliders beyond
+        # the soles within reach of the floor in a substep of the run (their contacts not simulated)
+        out["bank2_overflow_envs"] = int(eng.flags()["bank_overflow"].sum().item())
+    return out
 
 
 def bench_variant(cm, cfg, label: str, flops_file: str, n: int, steps: int, warmup: int, dev, rank: int, world: int,

@@ -1258,19 +1258,26 @@ __device__ __forceinline__ float load_mrow(const Ctx& c, float X[CAP]) {
  * factor_ldl (slots NROOT.. of the stored rows): forward z_p = b_p +
  * sum_{k > p} W(p, k) b_k, backward x_p = v_p + sum_{a < p} W(a, p) v_a. The
  * root chain is dense and redundant in every lane. */
-/* The root block's coupling of this lane for solve_ldl<true> (CG: the factor of M is fixed for the
- * substep's ~10 solves). R^-1 = L_r^-1 D_r^-1 L_r^-T is the inverse of the factored 6 x 6 root block
- * (the dense passes of solve_ldl); root lane j stores u = R^-1 e_j (row j of the symmetric R^-1), a
- * limb lane u = -R^-1 w with w its root entries L(j, root), a non-dof lane zero, in Hs[lane][0..5]
- * (CG builds no Hessian; the rows share memory with sub[], so the caller runs this after the last
- * subtree sum of the smooth phase, rne_project, and before the sensors'). A solve then ends in
- * x_j = [limb] x_j / D_j + sum_k u_k sr_k, sr the root right-hand sides of the team reduction: one
- * 6-term product instead of the dense passes' dependent chain (the same arithmetic, another order). */
-__device__ __forceinline__ void root_coupling(const Ctx& c) {
+/* Per-lane solve data for solve_pre (CG: M's factor is fixed for the substep's ~10 solves).
+ * With W = (I + Lt)^-1 the chain inverses of factor_ldl (Wf: W with its unit diagonal), Lr the limb
+ * rows' root entries L(j, root), D the pivots and R^-1 = L_r^-1 D_r^-1 L_r^-T the inverse of the
+ * factored 6 x 6 root block, the tree solve x = L^-1 D^-1 L^-T b is, for limb dof p of a chain,
+ *   x_p = sum_k Q(p, k) b_k + sum_e U(p, e) sr_e,   sr_e = b_e(root) - sum_j g_j[e] b_j,
+ *   Q = Wf' D^-1 Wf (the chain block), U(p, .) = sum_{m <= p} Wf(m, p) u_m, g_j[e] = sum_{m <= j} Lr(m, e) Wf(m, j),
+ * u_m = -R^-1 Lr(m, .)' (a root lane e: u = R^-1 e_e, x_e = sum u sr; Q = g = 0). So a solve is one
+ * gather of the lane's chain values and one team reduction, both of b, in flight together, then 12
+ * products: the limb passes' two dependent exchange rounds and the root block's dense passes leave
+ * the solve (the same arithmetic, another order). Stored after the last reader of the factor's rows:
+ * Q, g in L[lane][0..11] (CG reads no factor row past this point), U in Hs[lane][0..5] (CG builds no
+ * Hessian; Hs shares memory with sub[], so the caller runs this after the smooth phase's last subtree
+ * sum, rne_project, and the sensors' first one comes after the solver). */
+__device__ __forceinline__ void solve_prep(const Ctx& c) {
   EnvL* L = c.L;
   const bool isroot = c.l < NROOT, ischain = c.chd >= 0;
+  const int lr = c.l & 31;
+  /* u: this lane's row of the root coupling (the dense passes of solve_ldl on e_l or -Lr(l, .)) */
   float w[CAP];
-  ld_row(&L->L[c.l & 31][0], w);
+  ld_row(&L->L[lr][0], w);
   float xr[RMAX];
 #pragma unroll
   for (int k = 0; k < RMAX; k++) xr[k] = isroot ? (c.l == k ? 1.f : 0.f) : (ischain ? -w[k] : 0.f);
@@ -1284,15 +1291,81 @@ __device__ __forceinline__ void root_coupling(const Ctx& c) {
   for (int k = 1; k < RMAX; k++)
 #pragma unroll
     for (int a = 0; a < k; a++) xr[k] -= L->L[k][a] * xr[a];
-  tsync(); /* sub[] (same memory) is read by other lanes up to here */
-  static_assert(RMAX == 6, "u in one 16-byte and one 8-byte store");
-  *reinterpret_cast<v4f*>(&L->Hs[c.l & 31][0]) = v4f{xr[0], xr[1], xr[2], xr[3]};
-  L->Hs[c.l & 31][4] = xr[4];
-  L->Hs[c.l & 31][5] = xr[5];
+  tsync(); /* sub[] (same memory as Hs) is read by other lanes up to here */
+  static_assert(RMAX == 6 && NLIMBLV == 6, "six-entry rows");
+  *reinterpret_cast<v4f*>(&L->Hs[lr][0]) = v4f{xr[0], xr[1], xr[2], xr[3]};
+  L->Hs[lr][4] = xr[4];
+  L->Hs[lr][5] = xr[5];
+  tsync();
+  /* the chain sums over the shallower-or-equal chain positions m <= p */
+  const int p = ischain ? vopq(c.cps) : -1;
+  const int chd = ischain ? c.chd : 0;
+  float Q[NLIMBLV], U[RMAX], g[RMAX];
+#pragma unroll
+  for (int k = 0; k < NLIMBLV; k++) Q[k] = 0.f;
+#pragma unroll
+  for (int e = 0; e < RMAX; e++) {
+    U[e] = isroot ? xr[e] : 0.f;
+    g[e] = 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < NLIMBLV; m++) {
+    const int lm = chd + m; /* a valid lane for every lane (chd + 5 <= 31) */
+    float wm[CAP];
+    ld_row(&L->L[lm][0], wm); /* Lr(m, .) in 0..5, W(m, k) in NROOT + k (zero for k <= m) */
+    const v4f um4 = *reinterpret_cast<const v4f*>(&L->Hs[lm][0]);
+    const float um[RMAX] = {um4[0], um4[1], um4[2], um4[3], L->Hs[lm][4], L->Hs[lm][5]};
+    const float dinv = 1.f / fmaxf(L->Dk[lm], MINVAL);
+    /* Wf(m, p): 1 on the diagonal, the stored entry past it, 0 for m > p (and off the chains) */
+    float wmp = 0.f;
+#pragma unroll
+    for (int k = 0; k < NLIMBLV; k++) wmp = (p == k) ? wm[NROOT + k] : wmp;
+    wmp = m == p ? 1.f : (m < p ? wmp : 0.f);
+    const float wd = wmp * dinv;
+#pragma unroll
+    for (int k = 0; k < NLIMBLV; k++) Q[k] += wd * (k == m ? 1.f : wm[NROOT + k]);
+#pragma unroll
+    for (int e = 0; e < RMAX; e++) {
+      U[e] += wmp * um[e];
+      g[e] += wm[e] * wmp;
+    }
+  }
+  tsync(); /* every lane's reads of the factor rows and of u are done */
+  *reinterpret_cast<v4f*>(&L->L[lr][0]) = v4f{Q[0], Q[1], Q[2], Q[3]};
+  *reinterpret_cast<v4f*>(&L->L[lr][4]) = v4f{Q[4], Q[5], g[0], g[1]};
+  *reinterpret_cast<v4f*>(&L->L[lr][8]) = v4f{g[2], g[3], g[4], g[5]};
+  *reinterpret_cast<v4f*>(&L->Hs[lr][0]) = v4f{U[0], U[1], U[2], U[3]};
+  L->Hs[lr][4] = U[4];
+  L->Hs[lr][5] = U[5];
   tsync();
 }
 
-template <bool PRE = false>
+/* x <- M^-1 x with solve_prep's per-lane data (CG): the chain gather and the root sums of b in
+   flight together, then x_p = sum_k Q(p, k) b_k + sum_e U(p, e) sr_e (solve_prep) */
+__device__ __forceinline__ float solve_pre(const Ctx& c, float x) {
+  EnvL* L = c.L;
+  const int lr = c.l & 31;
+  const bool ischain = c.chd >= 0;
+  const int chd = ischain ? c.chd : 0;
+  float qg[CAP];
+  ld_row(&L->L[lr][0], qg); /* Q[0..5], g[0..5] */
+  const v4f u4 = *reinterpret_cast<const v4f*>(&L->Hs[lr][0]);
+  const float U[RMAX] = {u4[0], u4[1], u4[2], u4[3], L->Hs[lr][4], L->Hs[lr][5]};
+  float bk[NLIMBLV];
+#pragma unroll
+  for (int k = 0; k < NLIMBLV; k++) bk[k] = tsh(x, chd + k);
+  float sr[RMAX];
+#pragma unroll
+  for (int e = 0; e < RMAX; e++) sr[e] = (c.l == e ? x : 0.f) - qg[NLIMBLV + e] * x;
+  tsum_n<RMAX>(sr);
+  float y = 0.f;
+#pragma unroll
+  for (int k = 0; k < NLIMBLV; k++) y += qg[k] * bk[k];
+#pragma unroll
+  for (int e = 0; e < RMAX; e++) y += U[e] * sr[e];
+  return y;
+}
+
 __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
   EnvL* L = c.L;
   const int nroot = NROOT;
@@ -1324,16 +1397,6 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
     float sr[RMAX];
 #pragma unroll
     for (int k = 0; k < RMAX; k++) sr[k] = c.l == k ? x : -w[k] * xs;
-    if constexpr (PRE) {
-      /* root_coupling's u: loaded while the reduction runs */
-      const v4f u4 = *reinterpret_cast<const v4f*>(&L->Hs[c.l & 31][0]);
-      const float u[RMAX] = {u4[0], u4[1], u4[2], u4[3], L->Hs[c.l & 31][4], L->Hs[c.l & 31][5]};
-      tsum_n<RMAX>(sr);
-      float y = xs * Dinv; /* limb lanes; a root lane's value is all coupling, a non-dof lane's zero */
-#pragma unroll
-      for (int k = 0; k < RMAX; k++) y += u[k] * sr[k];
-      x = y;
-    } else {
     tsum_n<RMAX>(sr);
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
@@ -1359,7 +1422,6 @@ __device__ __forceinline__ float solve_ldl(const Ctx& c, float x, float Dinv) {
 #pragma unroll
     for (int k = 0; k < RMAX; k++)
       if (c.l == k && k < nroot) x = xr[k];
-    }
   } else {
     x *= Dinv;
   }
@@ -2326,8 +2388,9 @@ __device__ __forceinline__ void pair_rows(const Ctx& c, const EnvS& s, const Bod
    distance, geom_size[0]); the first two within reach of the margin (+1 mm against rounding), in
    geom order, take the bank's halves (EnvS.xsel, -1: none). Any other geom is then off the floor, so
    the contacts are MuJoCo's, except when more than two such geoms are within reach in one substep:
-   their contacts beyond the first two are not simulated, and the sticky state flag records it
-   (EnvS.nanflag bit 1, ZB_S_NAN). */
+   their contacts beyond the first two are not simulated, and the state's flag word records it
+   (EnvS.nanflag, ZB_S_NAN: bit 1 sticky, bit 2 for the current control step, so a caller can tell a
+   step that overflowed, the step that ends an episode included). */
 template <int XG>
 __device__ __forceinline__ void select_bank2(const Ctx& c, const BodyK& B) {
   MP m = c.m;
@@ -2361,7 +2424,7 @@ __device__ __forceinline__ void select_bank2(const Ctx& c, const BodyK& B) {
   /* team-uniform values, written by every lane of the team */
   c.L->s.xsel[0] = sel0;
   c.L->s.xsel[1] = sel1;
-  if (mk) c.L->s.nanflag |= 2u;
+  if (mk) c.L->s.nanflag |= 2u | 4u; /* sticky, and this control step's (cleared at its start) */
   tsync();
 }
 
@@ -3102,7 +3165,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
   float grad;
   float cost = update_constraint<XG, XA, false>(c, r, jr, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
-  float mg = solve_ldl<true>(c, grad, DinvM);
+  float mg = solve_pre(c, grad);
   STAMP(S_SOLVE0);
   float search = -mg;
   int it = 0;
@@ -3129,7 +3192,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
        (the same DPP sequence per value: the bits of separate sums). An iteration at the cap skips the
        solve and the beta sums, which only feed the next iteration. */
     if (it < itmax) {
-      mg = solve_ldl<true>(c, grad, DinvM);
+      mg = solve_pre(c, grad);
       STAMP(S_SOLVE);
       float red[4] = {cl, c.l < NV ? grad * grad : 0.f, c.l < NV ? grad * (mg - mgold) : 0.f,
                       c.l < NV ? gold * mgold : 0.f};
@@ -3228,8 +3291,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   float fs = (c.l < NV) ? (-damp * ls.v - bias + act) : 0.f;
   STAMP(S_RNE);
   constexpr bool PRE = SOLVER == ZB_SOLVER_CG; /* CG's ~10 solves with M's factor per substep */
-  if constexpr (PRE) root_coupling(c);
-  float qs = solve_ldl<PRE>(c, fs, DinvM);
+  if constexpr (PRE) solve_prep(c);
+  float qs = PRE ? solve_pre(c, fs) : solve_ldl(c, fs, DinvM);
   STAMP(S_SOLVES);
   /* constraints */
   make_constraints<XG>(c, s, ls, B, cm, r);
@@ -3988,6 +4051,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
       if constexpr (TGT_LDS<XG>) c.L->tgt[c.l] = at;
       else ls.tgt = at;
     }
+    if (ch == 0) s.nanflag &= ~4u; /* bit 2: a bank-2 overflow in this control step (select_bank2) */
     if (ch == 0 && (cfg->flags & ZB_F_PUSH)) push_event(c, s, ls, a.curriculum);
     float total = 0.f;
     int ss = ch * cfg->n_substeps / K;

@@ -58,6 +58,7 @@ S_NAN = 173
 # S_NAN's sticky flag bits (include/zbot_layout.h)
 NAN_NONFINITE = 1
 NAN_BANK_OVERFLOW = 2
+NAN_BANK_OVERFLOW_STEP = 4  # the same, in the last control step only
 S_AIR0_CONT = 174
 S_AIR0_TERM = 175
 S_END = 176

@@ -123,11 +123,14 @@ def state_flags(state) -> dict:
     `bank_overflow` - in some substep more than two colliders beyond the soles were within reach of
     the floor, and the extra ones' contacts were not simulated (zb_engine.hip select_bank2).
     Both are sticky for the life of the env's state row (resets keep them; set_state() can clear
-    them). Works on CPU or device tensors."""
+    them). `bank_overflow_step`: the same overflow in the last control step alone (the kernel clears
+    it at the start of every step), so the step that ends an episode still shows it. Works on CPU or
+    device tensors."""
     import torch
 
     bits = state[:, cs.S_NAN].contiguous().view(torch.int32)
-    return {"nonfinite": (bits & cs.NAN_NONFINITE) != 0, "bank_overflow": (bits & cs.NAN_BANK_OVERFLOW) != 0}
+    return {"nonfinite": (bits & cs.NAN_NONFINITE) != 0, "bank_overflow": (bits & cs.NAN_BANK_OVERFLOW) != 0,
+            "bank_overflow_step": (bits & cs.NAN_BANK_OVERFLOW_STEP) != 0}
 
 
 class HipEngine:
@@ -478,6 +481,10 @@ class EnvGroups:
         m = None if mask is None else mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
         self._each(lambda e, lo, hi: e.reset(None if m is None else m[lo:hi], extras=extras))
         return self.outputs()
+
+    def flags(self) -> dict:
+        """state_flags(get_state()) over all groups' envs (HipEngine.flags)."""
+        return state_flags(self.get_state())
 
     def get_state(self):
         return self.torch.cat(self._each(lambda e, lo, hi: e.get_state()))

@@ -204,11 +204,29 @@ class ZbotWalkingEnv:
         if self._last_done is None:
             raise RuntimeError("update_curriculum() needs a rollout: step() first")
         self.engine.join()
-        length = rollout_episode_length(self.engine.get_stats(), self.engine.get_state(), self._last_done,
-                                        self.cfg.ctrl_dt)
+        state = self.engine.get_state()
+        self.check_bank_overflow(state)
+        length = rollout_episode_length(self.engine.get_stats(), state, self._last_done, self.cfg.ctrl_dt)
         self.curriculum_state = self.curriculum.update(self.curriculum_state, length)
         self.curriculum_level = self.curriculum_state.level
         return self.curriculum_level
+
+    def check_bank_overflow(self, state=None) -> int:
+        """Envs whose second contact-row bank overflowed at some substep (more than two colliders beyond
+        the soles within reach of the floor; the extra ones' contacts were not simulated: zb_engine.hip
+        select_bank2, engine.state_flags). Warns once per env object the first time any env has; called
+        by update_curriculum() after every rollout. Returns the count."""
+        from .engine import state_flags  # noqa: PLC0415
+
+        n = int(state_flags(self.engine.get_state() if state is None else state)["bank_overflow"].sum().item())
+        if n and not getattr(self, "_overflow_warned", False):
+            import warnings  # noqa: PLC0415
+
+            warnings.warn(f"{n} env(s) had more than two colliders beyond the soles within reach of the floor in one "
+                          "substep; the contacts beyond the first two were not simulated (DESIGN.md §4j)", RuntimeWarning,
+                          stacklevel=2)
+            self._overflow_warned = True
+        return n
 
     def default_action(self):
         """FeetechActuators.get_default_action: current joint positions (train.py:1282-1283)."""

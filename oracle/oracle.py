@@ -61,6 +61,9 @@ def lib(precision: str = "f32") -> C.CDLL:
     L.zbo_plane_mesh.argtypes = [fp, C.c_int, fp, fp, C.c_float, C.POINTER(C.c_int32), fp, fp]
     L.zbo_plane_mesh.restype = C.c_int
     L.zbo_struct_bytes.restype = C.c_size_t
+    L.zbo_set_clearance_out.argtypes = [fp]
+    L.zbo_contact_count.argtypes = [C.c_void_p, C.c_void_p, fp, fp]
+    L.zbo_contact_count.restype = C.c_int
     if precision == "flops":
         L.zbo_flops_get.argtypes = [C.POINTER(C.c_uint64)]
         L.zbo_flops_reset.argtypes = []
@@ -229,6 +232,25 @@ def forward_debug(cmodel, cfg, qpos, qvel, ctrl=None, precision: str = "f32") ->
                                      _p(out["cinert"]), _p(out["cvel"]), nn, _p(out["touch"]))
     out["nefc"], out["ncon"] = nn[0], nn[1]
     return out
+
+
+def step_clearance(env, action, curriculum: float = 1.0):
+    """env.step(action) that also returns each env's smallest floor-contact clearance over the step's
+    substeps, min |distance - margin| of a contact candidate (zbo_set_clearance_out): (outputs, [n])."""
+    out = np.full(env.n, np.inf, np.float32)
+    env.L.zbo_set_clearance_out(_p(out))
+    try:
+        res = env.step(action, curriculum)
+    finally:
+        env.L.zbo_set_clearance_out(None)
+    return res, out
+
+
+def contact_count(cmodel, cfg, qpos, rnd=None, precision: str = "f64") -> int:
+    """Contacts of the collision stage at qpos (the env's randomization row rnd applied)."""
+    q = np.ascontiguousarray(qpos, dtype=np.float32)
+    r = None if rnd is None else np.ascontiguousarray(rnd, dtype=np.float32)
+    return int(lib(precision).zbo_contact_count(C.byref(cmodel), C.byref(cfg), _p(q), _p(r)))
 
 
 def constraint_problem(cmodel, cfg, qpos, qvel, ctrl=None, qaccw=None, precision: str = "f32") -> dict:

@@ -270,7 +270,17 @@ typedef struct {
   /* sensors */
   real imu_framequat[4], imu_gyro[3], imu_acc[3], touch[2], force[2][3];
   int solver_iters;
+  /* test infrastructure (zbo_set_clearance_out): the smallest |distance - margin| of a floor contact
+     candidate over a control step's substeps: a contact that close to its activation boundary starts
+     or not by rounding */
+  real clearance;
 } ZbData;
+
+static float* g_clearance_out = NULL; /* zbo_set_clearance_out; NULL: not recorded */
+static inline void track_clearance(ZbData* d, real dist, real margin) {
+  const real c = dist > margin ? dist - margin : margin - dist;
+  if (c < d->clearance) d->clearance = c;
+}
 
 /* ----------------------------- mj_kinematics ------------------------------ */
 static void kinematics(const ZbModel* m, ZbData* d) {
@@ -986,6 +996,7 @@ static void collision(const ZbModel* m, ZbData* d) {
         real loc[3] = {(i & 1) ? sz[0] : -sz[0], (i & 2) ? sz[1] : -sz[1], (i & 4) ? sz[2] : -sz[2]}, w[3];
         mulmv3(w, R, loc);
         const real dist = c[2] + w[2];
+        if (w[2] <= 0) track_clearance(d, dist, margin);
         if (dist > margin || w[2] > 0) continue;
         real p[3] = {c[0] + w[0], c[1] + w[1], c[2] + w[2]};
         add_contact(m, d, g, p, dist, ty);
@@ -1006,12 +1017,14 @@ static void collision(const ZbModel* m, ZbData* d) {
         const real sg = e == 0 ? 1 : -1;
         real p[3] = {c[0] + sg * sz[1] * ax[0], c[1] + sg * sz[1] * ax[1], c[2] + sg * sz[1] * ax[2] - sz[0]};
         const real dist = p[2];
+        track_clearance(d, dist, margin);
         if (dist > margin) continue;
         add_contact(m, d, g, p, dist, t1);
       }
     } else if (m->geom_type[g] == ZB_GEOM_SPHERE) {
       real p[3] = {c[0], c[1], c[2] - sz[0]};
       const real dist = p[2];
+      track_clearance(d, dist, margin);
       if (dist <= margin) add_contact(m, d, g, p, dist, ty);
     } else if (m->geom_type[g] == ZB_GEOM_ELLIPSOID) {
       /* R' n with n = +z: the z components of the geom's axes, row 2 of R */
@@ -1022,6 +1035,7 @@ static void collision(const ZbModel* m, ZbData* d) {
       mulmv3(w, R, loc);
       real p[3] = {c[0] + w[0], c[1] + w[1], c[2] + w[2]};
       const real dist = p[2];
+      track_clearance(d, dist, margin);
       if (dist <= margin) add_contact(m, d, g, p, dist, ty);
     } else if (m->geom_type[g] == ZB_GEOM_CYLINDER) {
       /* the plane: normal n = +z through the origin, so dot(x, n) = x[2] */
@@ -1045,6 +1059,7 @@ static void collision(const ZbModel* m, ZbData* d) {
       for (int k = 0; k < 3; k++) a[k] *= sz[1];
       prja *= sz[1];
       const real d1 = dist0 + prja + prjv;
+      track_clearance(d, d1, margin);
       if (d1 <= margin) {
         real p[3] = {c[0] + v[0] + a[0], c[1] + v[1] + a[1], c[2] + v[2] + a[2]};
         add_contact(m, d, g, p, d1, ty);
@@ -1071,8 +1086,10 @@ static void collision(const ZbModel* m, ZbData* d) {
       int idx[4];
       real dist[4], pos[4][3];
       plane_mesh((const float(*)[4])m->mesh_vert[m->geom_vertadr[g]], m->geom_vertnum[g], R, c, margin, idx, dist, pos);
-      for (int q = 0; q < 4; q++)
+      for (int q = 0; q < 4; q++) {
+        if (dist[q] < (real)1e29) track_clearance(d, dist[q], margin);
         if (dist[q] <= margin) add_contact(m, d, g, pos[q], dist[q], ty);
+      }
     }
   }
   pair_collision(m, d);
@@ -2033,6 +2050,10 @@ int zbo_reset(const ZbModel* m, const ZbEnvConfig* cfg, int n, int env_offset, u
   return 0;
 }
 
+/* test infrastructure: record each env's smallest floor-contact clearance over the next zbo_step calls'
+   substeps into out[e] (NULL: stop) */
+void zbo_set_clearance_out(float* out) { g_clearance_out = out; }
+
 int zbo_step(const ZbModel* m, const ZbEnvConfig* cfg, int n, int env_offset, uint64_t seed, float* state,
              float* rnd, const float* action, float* obs_actor, float* obs_critic, float* obs_extra,
              float* reward_terms, float* reward, uint8_t* done, uint8_t* success, float curriculum, float* stats,
@@ -2048,10 +2069,12 @@ int zbo_step(const ZbModel* m, const ZbEnvConfig* cfg, int n, int env_offset, ui
     state_to_data(m, st, d);
     if (cfg->flags & ZB_F_PUSH) push_event(&c, d, st, curriculum);
     const float* act = action + (size_t)e * ZB_NJ;
+    d->clearance = (real)1e30;
     for (int s = 0; s < cfg->n_substeps; s++) {
       feetech_ctrl(m, d, st + ZB_S_PLAN_POS, st + ZB_S_PLAN_VEL, st + ZB_S_PLAN_TAU, act, cfg->dt);
       physics_substep(m, d, cfg, s == cfg->n_substeps - 1, 1);
     }
+    if (g_clearance_out) g_clearance_out[e] = (float)d->clearance;
     if (nonfinite(m, d)) st[ZB_S_NAN] = bitsf(1);
     data_to_state(m, d, st);
     float rew;
@@ -2125,6 +2148,25 @@ int zbo_forward_debug(const ZbModel* m, const ZbEnvConfig* cfg, const float* qpo
   if (touch) { touch[0] = (float)d->touch[0]; touch[1] = (float)d->touch[1]; }
   free(d);
   return 0;
+}
+
+/*
+ * Contacts of the collision stage alone at qpos, with the env's randomization row (rnd may be NULL):
+ * kinematics, com_pos, collision; returns ncon. The GPU parity tests count them at the root lowered
+ * and raised by a few fp32 ulps to find envs whose step starts with a contact at its activation
+ * boundary (tests/test_gpu_parity.py boundary_envs).
+ */
+int zbo_contact_count(const ZbModel* m, const ZbEnvConfig* cfg, const float* qpos, const float* rnd) {
+  ZbData* d = (ZbData*)calloc(1, sizeof(ZbData));
+  EnvCtx c = {m, cfg, 0, 0};
+  load_params(&c, d, rnd);
+  for (int q = 0; q < m->nq; q++) d->qpos[q] = qpos[q];
+  kinematics(m, d);
+  com_pos(m, d);
+  collision(m, d);
+  const int n = d->ncon;
+  free(d);
+  return n;
 }
 
 /*

@@ -26,7 +26,7 @@ PATCHES = [
      "long long g_cnt[8];\nvoid zbo_cnt_get(long long* o) { for (int i = 0; i < 8; i++) o[i] = g_cnt[i]; }\n"
      "void zbo_cnt_reset(void) { for (int i = 0; i < 8; i++) g_cnt[i] = 0; }\n"
      "static real update_constraint(const ZbModel* m, ZbData* d, Solver* s) {", 1),
-    ("  int solver_iters;\n} ZbData;", "  int solver_iters;\n  int g_n, g_key[MAXEFC], g_act[MAXEFC], g_valid;\n} ZbData;", 1),
+    ("  int solver_iters;\n", "  int solver_iters;\n  int g_n, g_key[MAXEFC], g_act[MAXEFC], g_valid;\n", 1),
     ("    ls_eval(m, d, s, c1, c2, alpha, &d1, &d2);\n    if (FABS(d1) <= gtol) break;",
      "    ls_eval(m, d, s, c1, c2, alpha, &d1, &d2);\n    __atomic_add_fetch(&g_cnt[1], 1, __ATOMIC_RELAXED);\n"
      "    if (FABS(d1) <= gtol) break;", 1),

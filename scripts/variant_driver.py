@@ -23,9 +23,10 @@ else:
 g = torch.Generator(device="cuda")
 g.manual_seed(0)
 bias = torch.tensor([cm.cmodel.joint_bias[i] for i in range(20)], device="cuda")
-eng = HipEngine(cm, default_config(solver=os.environ.get("SOLVER", "cg")), 8192, seed=1, lib_path=lib)
+n = int(os.environ.get("N", "8192"))  # 512: train.py's size, one wave per CU (scripts/pmc_latency.sh)
+eng = HipEngine(cm, default_config(solver=os.environ.get("SOLVER", "cg")), n, seed=1, lib_path=lib)
 eng.reset()
 for t in range(steps):
-    eng.step(bias + 0.05 * torch.randn(8192, 20, device="cuda", generator=g), extras=False)
+    eng.step(bias + 0.05 * torch.randn(n, 20, device="cuda", generator=g), extras=False)
 torch.cuda.synchronize()
 print("iters/env-step", eng.solver_iters().float().mean().item())

@@ -39,7 +39,7 @@ def test_documented_binding_steps_like_hipengine(cmodel):
     exec(compile(src, "INTEGRATION.md:ZbotHipEnv", "exec"), ns)  # noqa: S102 - our own document
     n, T = 8, 12
     env = ns["ZbotHipEnv"](n, seed=5)
-    ref = HipEngine(cmodel, default_config(solver="newton"), n, seed=5)
+    ref = HipEngine(cmodel, default_config(), n, seed=5)  # zb_default_config: CG, as default_config()
     oa, oc = env.reset()
     r = ref.reset()
     torch.cuda.synchronize()

@@ -68,8 +68,9 @@ class MaxErr:
     lands further away (that env: 2.8x the qpos bound, 6.3x the planner bound); the budget admits
     one such env per output and step, within 10x the bound."""
 
-    def __init__(self, name, budget=1, loose=10.0, max_ill=3, exempt_ill=False):
+    def __init__(self, name, budget=1, loose=10.0, max_ill=3, exempt_ill=False, k_slack=2.0):
         self.name, self.err, self.bad, self.err_well = name, {}, [], {}
+        self.k_slack = k_slack  # the slack: k_slack x the env's fp32/fp64 gap (or its sensitivity, add(sens=))
         # exempt_ill: an env at a discontinuity is not bounded at all (still at most max_ill of them):
         # for a contact rule whose tie-breaks pick among equally valid branches by rounding (MJX's
         # manifold on a flat face, tests/test_gpu_colliders.py ENSEMBLE_ONLY), a third fp32
@@ -79,8 +80,9 @@ class MaxErr:
         # envs per output and step that may take the discontinuity slack (measured 0-3 of 64 in r03)
         self.max_ill = max_ill
         self.over = set()  # envs over the bound in the last add() calls (cleared by take_over())
+        self.exempted = set()  # (output, env, excess / tol) of boundary envs over the bound (add exempt=)
 
-    def add(self, key, got, ref, tol, rtol=0.0, ref64=None, loose_abs=None, sens=None):
+    def add(self, key, got, ref, tol, rtol=0.0, ref64=None, loose_abs=None, sens=None, exempt=None):
         """Record |got - ref| against tol + rtol |ref| elementwise (rows = envs; asserted in
         report(), after every output has been measured). ref64: the fp64 oracle's value of the same
         step. An env whose fp32 and fp64 oracles already disagree sits at a discontinuity of the
@@ -88,7 +90,8 @@ class MaxErr:
         2 |ref - ref64| of slack, and the report counts them. loose_abs: the budget envs' absolute
         limit for this output (default loose x tol). sens: a per-env sensitivity of the step to a
         rounding-level input change (oracle_sensitivity); the slack is then twice the larger of it and
-        the fp32/fp64 gap."""
+        the fp32/fp64 gap. exempt: envs whose step starts with a contact at its activation boundary
+        (boundary_envs): counted in the budget, but not held to the loose limit (the cause is shown)."""
         got = np.asarray(got, np.float64)
         ref = np.asarray(ref, np.float64)
         d = np.abs(got - ref)
@@ -98,7 +101,7 @@ class MaxErr:
             gap = gap.reshape(gap.shape[0], -1).max(1)
             if sens is not None:
                 gap = np.maximum(gap, np.asarray(sens, np.float64).reshape(-1))
-            slack = 2.0 * gap.reshape((-1,) + (1,) * (ref.ndim - 1))
+            slack = self.k_slack * gap.reshape((-1,) + (1,) * (ref.ndim - 1))
             ill = np.asarray(slack).reshape(-1) > tol
             if self.exempt_ill:
                 slack = np.where(ill.reshape(slack.shape), np.inf, slack)
@@ -117,7 +120,13 @@ class MaxErr:
         n_over = int((rows > tol).sum())
         self.over |= set(np.nonzero(rows > tol)[0].tolist())
         self.nout[key] = max(self.nout.get(key, 0), n_over)
-        worst = float(rows.max())
+        held = np.ones(rows.shape[0], bool)
+        if exempt is not None and len(exempt):
+            held[np.asarray(sorted(exempt), int)] = False
+            for ex in sorted(exempt):
+                if rows[ex] > tol:
+                    self.exempted.add((key, int(ex), float(rows[ex] / tol)))
+        worst = float(rows[held].max()) if held.any() else 0.0
         lim = self.loose * tol if loose_abs is None else loose_abs
         if n_over > self.budget or not worst <= lim:
             self.bad.append(f"{key} max error {e:.3e}: {n_over} envs over {tol:.1e} + {rtol:.0e} |ref| "
@@ -136,6 +145,9 @@ class MaxErr:
         if self.err_well:
             print(f"[{self.name}] envs at a discontinuity (fp32 / fp64 oracles disagree): {self.ill}; max |error| "
                   "elsewhere: " + ", ".join(f"{k} {v:.2e}" for k, v in self.err_well.items()))
+        if self.exempted:
+            print(f"[{self.name}] budget envs whose step starts with a contact at its activation boundary (no loose "
+                  "limit): " + ", ".join(f"{k} env {e} {x:.0f}x" for k, e, x in sorted(self.exempted)))
         assert not self.bad, f"{self.name}: " + "; ".join(self.bad)
 
 
@@ -200,11 +212,19 @@ ONE_STEP_TOL = {
     "reward_terms": (5e-6, 0.0),
 }
 
-# The CG solver stops after train.py's 8 iterations well before convergence (tests/
-# test_solver_optimality.py: 0.5 % median cost gap), so the two implementations' rounding
-# differences ride along its unconverged path: a wider contract, ~5x the measured error (round 3,
-# profiles/r03_v4_gpu_tests.log: qpos 1.8e-5, qvel 5.1e-4, planner 3.8e-4, obs_critic 3.8e-3,
-# obs_extra 0.12 (the accelerations), reward 2.8e-4, terms 8.9e-5).
+# CG (round 6): CG stops after train.py's 8 iterations well before convergence, and
+# fp32 CG stalls at an accuracy set by M^-1 H's conditioning times the fp32 epsilon: any
+# two fp32 implementations of it part by about as much as fp32 and fp64 do, env by env. The contract is
+# Newton's bounds (ONE_STEP_TOL) plus, per env, CG_SLACK x the step's own measured sensitivity: the larger
+# of the fp32/fp64 oracle gap and the spread of the fp32 oracle under 1-ulp perturbations of its input
+# (oracle_sensitivity, 4 draws; the engine is one more such draw, so a small multiple of the largest of
+# them). At most CG_BUDGET envs per output and step may exceed that, within CG_LOOSE x
+# Newton's bound beyond the slack, unless their step starts with a contact at its activation boundary
+# (boundary_envs: the cause, shown per env). Measured on MI355X (r06, tests/diag_cg_contract.py): 0-2
+# envs per output and step over the slack for the explicit step, 0-3 with implicit damping at 3x.
+CG_BUDGET, CG_LOOSE, CG_SLACK = 3, 10.0, 3.0
+# the flat contract of rounds 3-5 (about 5x the measured error), kept for the multi-step golden
+# rollouts' first-step scale only (GOLDEN_TOL_CG) and as the reference for what the sensitivity adds
 ONE_STEP_TOL_CG = {
     "qpos": (1e-4, 0.0),
     "qvel": (2.5e-3, 0.0),
@@ -240,14 +260,15 @@ def oracle_steps(O, cm, cfg, env, a, seed):
     e64 = O.OracleEnv(cm.cmodel, cfg, env.state.shape[0], seed=seed, precision="f64")
     e64.state[:] = env.state
     e64.rand[:] = env.rand
-    r64 = e64.step(a)
+    r64, clear = O.step_clearance(e64, a)
     ref = env.step(a)
     ref64 = {k: want for k, _, want in one_step_outputs(e64.state, r64, e64.state, r64)}
     ref64["_iters"] = e64.iters.copy()
+    ref64["_clearance"] = clear  # per env: the closest floor-contact candidate to its activation boundary
     return ref, ref64
 
 
-def oracle_sensitivity(O, cm, cfg, state, rand, a, seed, ref, draws=3):
+def oracle_sensitivity(O, cm, cfg, state, rand, a, seed, ref, draws=4):
     """The step's sensitivity to a rounding-level change of its input, per output and env: the fp32
     oracle stepped from the same state with every qvel component scaled by 1 +- 2^-23 (one fp32 ulp,
     `draws` random sign patterns), the largest |output - ref| over the draws (ref: the unperturbed
@@ -268,6 +289,21 @@ def oracle_sensitivity(O, cm, cfg, state, rand, a, seed, ref, draws=3):
             d = np.abs(np.asarray(want, np.float64) - np.asarray(ref[key], np.float64)).reshape(n, -1).max(1)
             sens[key] = np.maximum(sens.get(key, 0.0), d)
     return sens
+
+
+# A floor-contact candidate closer than this to its activation boundary (distance = margin) at some
+# substep: which side it lands on is decided by how an implementation rounds the point's height (the
+# engine's quaternion rotations against the oracle's matrices; a few fp32 ulps of a 0.3 m height
+# through the kinematic chain)
+BOUNDARY_EPS = 2e-7
+
+
+def boundary_envs(ref64) -> set:
+    """Envs whose step has a contact at its activation boundary: the fp64 oracle's closest contact
+    candidate over the step's substeps (oracle step_clearance) is within BOUNDARY_EPS of it. The
+    contact then starts (or not) by rounding, and its first impulse moves the whole step
+    (test_eulerdamp_budget_env_is_a_touchdown, test_cg_budget_env_is_a_touchdown)."""
+    return set(np.flatnonzero(np.asarray(ref64["_clearance"]) < BOUNDARY_EPS).tolist())
 
 
 def print_budget_envs(err, t, eng, env, ref64, gs):
@@ -294,41 +330,23 @@ def test_one_step_parity(torch_gpu, cmodel, oracle_mod, push, randomize, solver)
 # mj_Euler's implicit damping advances qvel with (M + dt B)^-1 (qfrc_smooth + qfrc_constraint): the
 # constraint force at the solver's LAST iterate, not its qacc. Where the solve is unconverged the force
 # residual (the gradient) enters the velocity, scaled by the contact stiffness, so rounding differences
-# along the solver path weigh more than in the explicit form (MuJoCo has the same sensitivity).
-# Newton: the explicit contract, except the solver exit-iteration env (engine and fp32 oracle leave the
-# loop a few iterations apart), which may be 50x off (measured r05: 33x, env 23: 66 vs 63 iterations);
-# with the early exit off the whole contract holds with no exception
-# (test_one_step_parity_eulerdamp_without_early_exit). CG (8 unconverged iterations): about 5x the
-# maximum error measured on MI355X (r05: qpos 1.7e-4, qvel 3.2e-3, planner 4.0e-3, obs_critic 1.1e-2,
-# obs_extra 0.76, reward 9.6e-4, terms 3.9e-4), up to 12 of 64 envs at a discontinuity (measured 8).
-ONE_STEP_TOL_CG_ED = {
-    "qpos": (1e-3, 0.0),
-    "qvel": (1.5e-2, 0.0),
-    "planner": (2e-2, 0.0),
-    "obs_actor": (1.5e-2, 0.0),
-    "obs_critic": (5e-2, 0.0),
-    "obs_extra": (4.0, 0.0),
-    "reward": (4e-3, 0.0),
-    "reward_terms": (2e-3, 0.0),
-}
+# along the solver path weigh more than in the explicit form (MuJoCo has the same sensitivity); the
+# per-env sensitivity of the CG contract (oracle_sensitivity) measures exactly that. Both solvers are
+# held to the explicit form's contracts (round 6: the wider ONE_STEP_TOL_CG_ED of round 5, qpos 1e-3 and
+# up to 30x / 100x for budget envs, is gone): Newton to ONE_STEP_TOL with the usual one-env budget
+# within 10x, CG to the CG contract. A budget env past the loose limit must start its step with a
+# contact at its activation boundary (boundary_envs): env 23 of the Newton case is one
+# (test_eulerdamp_budget_env_is_a_touchdown, where the corner is 1e-7 m above the floor).
 
 
 @pytest.mark.parametrize("solver", ["newton", "cg"])
 @pytest.mark.parametrize("push,randomize", [(False, False), (True, True)])
 def test_one_step_parity_eulerdamp(torch_gpu, cmodel, oracle_mod, push, randomize, solver):
-    """ZB_F_EULERDAMP (mj_Euler's implicit joint damping, the step kernel's ED instantiation): Newton
-    under the explicit form's contract with a wider exit-iteration budget, CG under ONE_STEP_TOL_CG_ED."""
+    """ZB_F_EULERDAMP (mj_Euler's implicit joint damping, the step kernel's ED instantiation) under the
+    explicit form's contracts (Newton: ONE_STEP_TOL; CG: the CG contract)."""
     cfg = default_config(push=push, randomize=randomize, solver=solver, eulerdamp=True)
-    name = f"one-step eulerdamp {solver} push={push} randomize={randomize}"
-    if solver == "cg":
-        # the budget env of push+randomize (r05d: obs_critic 25x, obs_extra 16x the bound; qpos / qvel
-        # inside) carries an accelerations jump through the critic's observation
-        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, name, solver, tol=ONE_STEP_TOL_CG_ED,
-                         err_kw=dict(max_ill=12, loose=30.0))
-    else:
-        # one env (23) is a sole corner touching down within 1e-7 m of the floor, the contact set
-        # itself parting (test_eulerdamp_budget_env_is_a_touchdown); measured at 59x the planner bound
-        _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, name, solver, err_kw=dict(loose=100.0))
+    _one_step_parity(torch_gpu, cmodel, oracle_mod, cfg, f"one-step eulerdamp {solver} push={push} randomize={randomize}",
+                     solver)
 
 
 def touchdown_state(oracle_mod, cmodel):
@@ -377,6 +395,45 @@ def test_eulerdamp_budget_env_is_a_touchdown(torch_gpu, cmodel, oracle_mod):
     assert e <= 1e-3 * max(1.0, np.abs(ref["qacc"]).max())
 
 
+def test_cg_budget_env_is_a_touchdown(torch_gpu, cmodel, oracle_mod):
+    """The cause of the CG contract's largest budget env (push + randomize one-step states, step 0: env
+    63, qpos 1.8e-5 and reward 2.8e-4 from the fp32 oracle while both oracles agree to 2.4e-6 / 1.5e-5,
+    tests/diag_cg_env.py: the engine parts from them in the first substep, 2e-3 in qvel). Its step
+    starts with a sole corner 3e-9 m above the floor: the fp64 collision stage counts one contact more
+    with the root lowered by 5e-8 m. The engine's step lands on that side: the fp64 oracle stepped from
+    the lowered state is several times closer to the engine than the oracle stepped from the state."""
+    torch = torch_gpu
+    cfg = default_config(push=True, randomize=True)
+    n = 64
+    env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
+    st0, rd0 = env.state.copy(), env.rand.copy()
+    a = oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100)
+    e64 = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=7, precision="f64")
+    e64.state[:], e64.rand[:] = st0, rd0
+    _, clear = oracle_mod.step_clearance(e64, a)
+    w = int(np.argmin(clear))
+    q = st0[w, :27].copy()
+    lo = q.copy()
+    lo[2] -= 5e-8
+    n_at, n_lo = (oracle_mod.contact_count(cmodel.cmodel, cfg, x, rd0[w]) for x in (q, lo))
+    low = oracle_mod.OracleEnv(cmodel.cmodel, cfg, n, seed=7, precision="f64")
+    low.state[:], low.rand[:] = st0, rd0
+    low.state[w, 2] -= np.float32(5e-8)
+    low.step(a)
+    eng = engine(cmodel, cfg, n, seed=7)
+    eng.set_state(torch.from_numpy(st0.copy()))
+    eng.set_rand(torch.from_numpy(rd0.copy()))
+    eng.step(torch.from_numpy(a).cuda())
+    torch.cuda.synchronize()
+    gs = eng.get_state().cpu().numpy()
+    d_at = float(np.abs(gs[w, 32:58] - e64.state[w, 32:58]).max())
+    d_lo = float(np.abs(gs[w, 32:58] - low.state[w, 32:58]).max())
+    print(f"\n[cg touchdown] env {w}: clearance {clear[w]:.2e} m, contacts {n_at} at the state, {n_lo} lowered 5e-8 m; "
+          f"engine qvel vs fp64 oracle {d_at:.2e}, vs the fp64 oracle from the lowered state {d_lo:.2e}")
+    assert clear[w] < 1e-8 and n_lo == n_at + 1
+    assert d_lo * 3 < d_at
+
+
 def test_eulerdamp_changes_the_step(torch_gpu, cmodel, oracle_mod):
     """The flag reaches the kernel: from the same state the implicit and explicit steps differ in
     qvel by far more than the one-step bound, and the oracle agrees on the difference."""
@@ -401,55 +458,37 @@ def test_eulerdamp_changes_the_step(torch_gpu, cmodel, oracle_mod):
 
 
 def _one_step_parity(torch, cmodel, oracle_mod, cfg, name, solver, tol=None, err_kw=None):
+    """Three control steps from the warm states of 64 envs, each from the fp32 oracle's state. Newton:
+    ONE_STEP_TOL (fp64 slack at discontinuities, one budget env within 10x); CG: the CG contract
+    (Newton's bounds + CG_SLACK x each env's sensitivity, CG_BUDGET envs within CG_LOOSE x). Either way a
+    budget env whose step starts with a contact at its activation boundary (boundary_envs) is exempt
+    from the loose limit and printed."""
     n = 64
+    cg = solver == "cg"
     env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
     eng = engine(cmodel, cfg, n, seed=7)
-    err = MaxErr(name, **(err_kw or {}))
+    kw = dict(budget=CG_BUDGET, loose=CG_LOOSE, max_ill=n, k_slack=CG_SLACK) if cg else {}
+    err = MaxErr(name, **{**kw, **(err_kw or {})})
+    tl = tol or ONE_STEP_TOL
     for t in range(3):
-        eng.set_state(torch.from_numpy(env.state.copy()))
-        eng.set_rand(torch.from_numpy(env.rand.copy()))
+        st0, rd0 = env.state.copy(), env.rand.copy()
+        eng.set_state(torch.from_numpy(st0.copy()))
+        eng.set_rand(torch.from_numpy(rd0.copy()))
         a = oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100 + t)
         ref, ref64 = oracle_steps(oracle_mod, cmodel, cfg, env, a, 7)
+        ref32 = {k: want for k, _, want in one_step_outputs(env.state, ref, env.state, ref)}
+        sens = oracle_sensitivity(oracle_mod, cmodel, cfg, st0, rd0, a, 7, ref32) if cg else {}
+        bnd = boundary_envs(ref64)
         out = eng.step(torch.from_numpy(a).cuda())
         torch.cuda.synchronize()
         gs = eng.get_state().cpu().numpy()
         np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
-        tl = tol or (ONE_STEP_TOL_CG if solver == "cg" else ONE_STEP_TOL)
         for key, got, want in one_step_outputs(gs, out, env.state, ref):
-            err.add(key, got, want, *tl[key], ref64=ref64[key])
+            err.add(key, got, want, *tl[key], ref64=ref64[key], sens=sens.get(key), exempt=bnd)
         print_budget_envs(err, t, eng, env, ref64, gs)
         # integer bookkeeping is exact
         for w in (cs.S_EP_STEPS, cs.S_RNG_STEP, cs.S_EPISODE):
             assert np.array_equal(gs[:, w].view(np.uint32), env.state[:, w].view(np.uint32))
-    err.report()
-
-
-@pytest.mark.parametrize("push,randomize", [(False, False), (True, True)])
-def test_one_step_parity_cg_conditioned(torch_gpu, cmodel, oracle_mod, push, randomize):
-    """The CG solver held to Newton's one-step bounds (ONE_STEP_TOL) for most envs. CG stops after
-    train.py's 8 iterations well short of the minimum, so a rounding difference rides along its
-    unconverged path. Each env gets twice its own fp32/fp64 oracle gap on top (the step's measured
-    sensitivity, MaxErr.add ref64); per output and step at least 56 of the 64 envs must then be
-    within Newton's bound, and the rest within ONE_STEP_TOL_CG, the flat contract of
-    test_one_step_parity[cg]. Measured (r04 v9): 0-5 envs per output and step outside Newton's
-    bound + 2 x gap; without the gap term (a flat Newton bound) 22-32 envs would be."""
-    torch = torch_gpu
-    cfg = default_config(push=push, randomize=randomize, solver="cg")
-    n = 64
-    env = warm_states(oracle_mod, cmodel, cfg, n, steps=12)
-    eng = engine(cmodel, cfg, n, seed=7)
-    err = MaxErr(f"one-step cg conditioned push={push} randomize={randomize}", budget=8, max_ill=n)
-    for t in range(3):
-        eng.set_state(torch.from_numpy(env.state.copy()))
-        eng.set_rand(torch.from_numpy(env.rand.copy()))
-        a = oracle_mod.synthetic_actions(cmodel.cmodel, 7, n, 0, 100 + t)
-        ref, ref64 = oracle_steps(oracle_mod, cmodel, cfg, env, a, 7)
-        out = eng.step(torch.from_numpy(a).cuda())
-        torch.cuda.synchronize()
-        gs = eng.get_state().cpu().numpy()
-        np.testing.assert_array_equal(out["done"].cpu().numpy(), ref["done"])
-        for key, got, want in one_step_outputs(gs, out, env.state, ref):
-            err.add(key, got, want, *ONE_STEP_TOL[key], ref64=ref64[key], loose_abs=ONE_STEP_TOL_CG[key][0])
     err.report()
 
 
