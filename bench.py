@@ -465,7 +465,7 @@ def bench_variant(cm, cfg, label: str, flops_file: str, n: int, steps: int, warm
                      "kernel_avg_ms": avg_ms, "rate_ms": rate_ms, "algorithmic_bytes_per_env_step": bpe},
     }
     fpath = os.path.join(ROOT, "profiles", flops_file)
-    if os.path.exists(fpath):
+    if flops_file and os.path.exists(fpath):
         with open(fpath) as f:
             fl = json.load(f)["as_run"]["flops_per_env_step"]
         tf = fl * n / (rate_ms * 1e-3) / 1e12
@@ -719,7 +719,7 @@ def main(argv: list | None = None) -> None:
                     help="skip the ksim_env (ZbotWalkingEnv.step), train_defaults (512 x 200), c1_gpu, "
                          "general_colliders (limbs model), cylinder_colliders (cyl model), mesh_colliders (mesh "
                          "model), many_colliders (nine colliders), the other solver's "
-                         "(cg_solver / newton_solver), sole_pair and eulerdamp legs")
+                         "(cg_solver / newton_solver), sole_pair, sole_pair_limbs, mjx_box_rule and eulerdamp legs")
     ap.add_argument("--inloop-critic", type=int, default=0,
                     help="rollout-pipeline leg: run the critic inside the group chains with this policy layout "
                          "(1 one-wave, 2 two-wave, 3 four-wave; DESIGN.md §4f); 0 = the 8-wave critic afterwards")
@@ -834,6 +834,7 @@ def main(argv: list | None = None) -> None:
         extra_legs[f"{other}_solver"] = bench_variant(
             cm, default_config(solver=other), f"the {other.upper() if other == 'cg' else 'Newton'} solver (ZbEnvConfig.solver)",
             FLOPS_FILES[(other, "base")], n, args.steps, args.warmup, dev, rank, world, args.seed, G)
+        from zbot_amd.mjcf import load_mjcf  # noqa: PLC0415
         from zbot_amd.model import load_description  # noqa: PLC0415
 
         pdesc = load_description()
@@ -842,6 +843,13 @@ def main(argv: list | None = None) -> None:
             compile_model(pdesc), default_config(solver=args.solver),
             "the sole-pair model (the soles also collide with each other, box-box; the XG 3 kernels, DESIGN.md §4l)",
             FLOPS_FILES[(args.solver, "solepair")], n, args.steps, args.warmup, dev, rank, world, args.seed, G)
+        ldesc = load_mjcf(os.path.join(ROOT, "ksim-gym-zbot_amd", "assets", "zbot_like_limbs.xml"))
+        ldesc["self_pairs"] = [["left_foot_sole", "right_foot_sole"]]
+        extra_legs["sole_pair_limbs"] = bench_variant(
+            compile_model(ldesc), default_config(solver=args.solver),
+            "the sole pair beside the limbs model's shin box and hand capsule (the XG 4 kernels: floor colliders in "
+            "the second bank, the pair in a third; DESIGN.md §4l)",
+            "", n, args.steps, args.warmup, dev, rank, world, args.seed, G)
         extra_legs["mjx_box_rule"] = bench_variant(
             compile_model(box_rule="mjx"), default_config(solver=args.solver),
             "the box soles collided by MJX's plane_convex manifold (compile_model(box_rule='mjx'): each an 8-corner "

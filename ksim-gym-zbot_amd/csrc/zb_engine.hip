@@ -519,6 +519,11 @@ typedef __attribute__((address_space(1))) xv4f gfloat4_t;
 __device__ __forceinline__ gfloat_t* xrows(const EnvL* L) {
   return (gfloat_t*)(((uint64_t)L->s.xj_hi << 32) | (uint64_t)L->s.xj_lo);
 }
+/* XG 4: the third bank's rows follow the second bank's in the env's block */
+__device__ __forceinline__ gfloat_t* yrows(const EnvL* L) { return xrows(L) + 32 * CAP; }
+/* floats of StepArgs::xj per env: one [32][CAP] block per extra bank */
+template <int XG>
+constexpr int XJ_STRIDE = ZB_XJ_STRIDE * (XG == 4 ? 2 : 1);
 __device__ __forceinline__ void set_xrows(EnvL* L, float* base) {
   L->s.xj_lo = (uint32_t)(uint64_t)base;
   L->s.xj_hi = (uint32_t)((uint64_t)base >> 32);
@@ -702,6 +707,7 @@ struct Rows {
   int nrow;
   uint32_t exmask; /* team-uniform: existing contact rows */
   XRow x;          /* second bank (XG kernels only) */
+  XRow y;          /* third bank: the sole pair beside floor colliders (XG 4 only) */
 };
 
 /* 16-byte LDS row access (rows are 12 floats = 48 B, 16-B aligned) */
@@ -1496,6 +1502,9 @@ __device__ __forceinline__ float row_dot(const Ctx& c, const Rows& r, int slot) 
 __device__ __forceinline__ float row_dot_x(const Ctx& c, const Rows& r, int slot) {
   return row_dot(c, (const gfloat_t*)xrows(c.L) + c.l * CAP, r.x.chd, slot);
 }
+__device__ __forceinline__ float row_dot_y(const Ctx& c, const Rows& r, int slot) {
+  return row_dot(c, (const gfloat_t*)yrows(c.L) + c.l * CAP, r.y.chd, slot);
+}
 
 /* row_dot with the lane's row already in registers (jr) */
 __device__ __forceinline__ float row_dot_pre(const Ctx& c, const float jr[CAP], int chd, int slot) {
@@ -1691,13 +1700,21 @@ __device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, floa
   aref = -bb * vel - kk * imp * pos;
 }
 
-/* The second contact-row bank's role by kernel instantiation (zb_host.cpp needs_xg): XG 1 / 2 the
-   general floor colliders (geoms 2-3; XG 2 with cylinders / ellipsoids), XG 3 the sole pair (the two
-   box soles against each other, pair_rows). XG 0: the two soles alone. */
+/* The extra contact-row banks by kernel instantiation (zb_host.cpp needs_xg): XG 1 / 2 the second bank
+   (Rows::x) holds the general floor colliders (the first two beyond the soles within reach, select_bank2;
+   XG 2 compiles cylinders, ellipsoids and meshes), XG 3 the sole pair (the two box soles against each
+   other, pair_rows), XG 4 both: the floor colliders in the second bank and the sole pair in a third
+   (Rows::y, round 6). XG 0: the two soles alone. */
 template <int XG>
-constexpr bool XFLOOR = XG == 1 || XG == 2;
+constexpr bool XFLOOR = XG == 1 || XG == 2 || XG == 4;
 template <int XG>
-constexpr bool XPAIR = XG == 3;
+constexpr bool XPAIR = XG == 3; /* the pair in the second bank */
+template <int XG>
+constexpr bool YPAIR = XG == 4; /* the pair in the third bank */
+template <int XG>
+constexpr bool XRICH = XG == 2 || XG == 4; /* cylinder / ellipsoid / mesh rules compiled */
+template <int XG>
+constexpr bool ANYPAIR = XPAIR<XG> || YPAIR<XG>;
 
 /* The collider of team lane l in contact-row bank `bank`: geom 2 bank + l / 16 (general colliders), or
    sole l / 16 (the two-sole and sole-pair kernels). gb: its body; false when the model has no such geom. */
@@ -1753,8 +1770,8 @@ __device__ __forceinline__ float contact_point(const Ctx& c, const EnvS& s, cons
   /* XG 2: the instantiation for models with cylinders or ellipsoids (zb_host.cpp needs_xg), so that
      the others carry no code for them */
   const bool box = !XFLOOR<XG> || ty == ZB_GEOM_BOX, cap = XFLOOR<XG> && ty == ZB_GEOM_CAPSULE,
-             cyl = XG == 2 && ty == ZB_GEOM_CYLINDER, ell = XG == 2 && ty == ZB_GEOM_ELLIPSOID,
-             msh = XG == 2 && ty == ZB_GEOM_MESH;
+             cyl = XRICH<XG> && ty == ZB_GEOM_CYLINDER, ell = XRICH<XG> && ty == ZB_GEOM_ELLIPSOID,
+             msh = XRICH<XG> && ty == ZB_GEOM_MESH;
   /* the lane's point relative to the geom centre, geom frame -> body frame -> world */
   float gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]};
   float gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
@@ -2461,7 +2478,12 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
     /* the second bank's work is skipped, bit for bit, while no row of it exists in the wave (the
        usual case: shins and hands off the floor) */
     r.x.any = __ballot(r.x.ex) != 0ull;
-    if (r.x.any) {
+    bool yany = false;
+    if constexpr (YPAIR<XG>) {
+      pair_rows(c, s, B, cm, r.y, yrows(c.L) + l * CAP);
+      r.y.any = yany = __ballot(r.y.ex) != 0ull;
+    }
+    if (r.x.any || yany) {
       /* the rows just stored are read by other lanes from here on */
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2546,7 +2568,8 @@ __device__ __forceinline__ float eval_one(float jar, float D, float& force, int&
 
 /* row costs at given jar values (no state change); jx: the second bank's contact row (XG) */
 template <int XG, bool XA = true>
-__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jl_, float jx) {
+__device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc, float jf_, float jl_, float jx,
+                                           float jy = 0.f) {
   float f;
   int a;
   const float k0 = eval_one(jc, r.D, f, a);
@@ -2562,6 +2585,10 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
     const float k3 = eval_one(jx, r.x.D, f, a);
     /* the sole pair's row is held by two lanes (its halves): counted once */
     cost += (r.x.ex && (!XPAIR<XG> || c.l < 16)) ? k3 : 0.f;
+  }
+  if constexpr (YPAIR<XG> && XA) {
+    const float k4 = eval_one(jy, r.y.D, f, a);
+    cost += (r.y.ex && c.l < 16) ? k4 : 0.f; /* the pair's halves: once */
   }
   return cost;
 }
@@ -2651,6 +2678,20 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
     sx0 = tsh(cx, ddep);
     sx1 = tsh(cx, 16 + ddep);
   }
+  float sy0 = 0.f, sy1 = 0.f;
+  if constexpr (YPAIR<XG> && XA) {
+    if (r.y.any) {
+      float f4;
+      int a4;
+      const float k4 = eval_one(r.y.jar, r.y.D, f4, a4);
+      cost += (r.y.ex && c.l < 16) ? k4 : 0.f; /* the pair's halves: once */
+      r.y.f = r.y.ex ? f4 : r.y.f;
+      r.y.act = r.y.ex ? a4 : r.y.act;
+      const float cy = colsum16((const gfloat_t*)yrows(c.L) + c.l * CAP, r.y.ex ? r.y.f : 0.f);
+      sy0 = tsh(cy, ddep);
+      sy1 = tsh(cy, 16 + ddep);
+    }
+  }
   /* J'f per dof: a dof adds the column sum at its depth of every geom whose chain holds it */
   const float colsum = colsum16_pre(jr, r.ex ? r.f : 0.f);
   const float so = tsh(colsum, ddep), sx = tsh(colsum, 16 + ddep);
@@ -2663,6 +2704,10 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
       const uint32_t rm2 = XPAIR<XG> ? rm_rows(c.rmb >> 2) : r.x.rowmask;
       const bool f2 = (rm2 & 0xFFFFu) != 0u, f3 = (rm2 >> 16) != 0u;
       qc += (f2 ? sx0 : 0.f) + (f3 ? sx1 : 0.f);
+    }
+    if constexpr (YPAIR<XG> && XA) {
+      const bool f4 = (c.rmb & 16u) != 0u, f5 = (c.rmb & 32u) != 0u; /* the pair's static row masks */
+      qc += (f4 ? sy0 : 0.f) + (f5 ? sy1 : 0.f);
     }
     if (r.hf) qc += r.ff;
     if (r.anyl && r.hl) qc += r.sl * r.flim;
@@ -2855,6 +2900,11 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
     if constexpr (XPAIR<XG>) jx += xor16f(jx); /* the pair's row: both halves */
     r.x.Jv = jx;
   }
+  if constexpr (YPAIR<XG> && XA) {
+    float jy = r.y.any ? row_dot_y(c, r, V_TMP) : 0.f;
+    jy += xor16f(jy);
+    r.y.Jv = jy;
+  }
   tsync();
   /* the quadratic's coefficients and the slope/curvature at alpha = 0 in one reduction:
      d1(0) = search . grad (the gradient update_constraint left for the current active
@@ -2868,6 +2918,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   /* XA: the second bank has rows in the wave; without, its terms are exact zeros and its row state is
      not carried through the loop (fewer live registers in the common copy) */
   if constexpr (XG && XA) g20 += (r.x.ex && r.x.act && xprim) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
+  if constexpr (YPAIR<XG> && XA) g20 += (r.y.ex && r.y.act && c.l < 16) ? r.y.D * r.y.Jv * r.y.Jv : 0.f;
   float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
   tsum_n<4>(cc);
   const float c1 = cc[0], c2 = cc[1];
@@ -2884,6 +2935,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
     DlJ2 = DlJ * sv;
   }
   const float DXJ = (XG && XA && r.x.ex && xprim) ? r.x.D * r.x.Jv : 0.f, DXJ2 = (XG && XA) ? DXJ * r.x.Jv : 0.f;
+  const float DYJ = (YPAIR<XG> && XA && r.y.ex && c.l < 16) ? r.y.D * r.y.Jv : 0.f,
+              DYJ2 = (YPAIR<XG> && XA) ? DYJ * r.y.Jv : 0.f;
   float d1 = cc[2], d2 = c2 + cc[3];
   if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
   const float gtol = cfg->ls_tolerance * (-d1);
@@ -2922,6 +2975,11 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
         const float x = r.x.jar + alpha * r.x.Jv;
         g1 += DXJ * fminf(x, 0.f);
         g2 += x < 0.f ? DXJ2 : 0.f;
+        if constexpr (YPAIR<XG>) {
+          const float xy = r.y.jar + alpha * r.y.Jv;
+          g1 += DYJ * fminf(xy, 0.f);
+          g2 += xy < 0.f ? DYJ2 : 0.f;
+        }
       }
       float gg[2] = {g1, g2};
       tsum_n<2>(gg);
@@ -2945,24 +3003,44 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
 }
 
 /* H p for the sole-pair kernels' Newton direction (hsolve_pair): M p, the floor rows' and dof rows'
-   D J J' p over the current active set (the terms of the factored tree Hessian H_t, hessian_factor),
-   plus the pair's active rows' D u u' p (u: the row over both limbs, held as two half rows). */
+   D J J' p over the current active set (the terms of the factored tree Hessian H_t, hessian_factor:
+   the soles' bank and, XG 4, the floor colliders' bank), plus the pair's active rows' D u u' p (u: the
+   row over both limbs, held as two half rows: the second bank in XG 3, the third in XG 4). */
+template <int XG>
 __device__ __forceinline__ float hmul_pair(const Ctx& c, const Rows& r, const float jr[CAP], float p) {
   const int ddep = vopq(c.ddep);
   float jv, unused_;
   const float Mp = mul_m_dot(c, r, jr, p, V_TMP, jv, -1, unused_);
-  float jx = row_dot_x(c, r, V_TMP);
-  jx += xor16f(jx);
+  const XRow& pr = YPAIR<XG> ? r.y : r.x;
+  float jp = row_dot(c, (const gfloat_t*)(YPAIR<XG> ? yrows(c.L) : xrows(c.L)) + c.l * CAP, pr.chd, V_TMP);
+  jp += xor16f(jp);
   const float w0 = (r.ex && r.act) ? r.D * jv : 0.f;
-  const float wx = (r.x.ex && r.x.act) ? r.x.D * jx : 0.f;
+  const float wp = (pr.ex && pr.act) ? pr.D * jp : 0.f;
   const float cs0 = colsum16_pre(jr, w0);
-  const float cs1 = colsum16((const gfloat_t*)xrows(c.L) + c.l * CAP, wx);
+  const float cs1 = colsum16((const gfloat_t*)(YPAIR<XG> ? yrows(c.L) : xrows(c.L)) + c.l * CAP, wp);
   const float so = tsh(cs0, ddep), sx = tsh(cs0, 16 + ddep), s2 = tsh(cs1, ddep), s3 = tsh(cs1, 16 + ddep);
+  float s4 = 0.f, s5 = 0.f;
+  if constexpr (YPAIR<XG>) {
+    /* XG 4: the floor colliders' bank is part of H_t */
+    if (r.x.any) {
+      const float jf = row_dot_x(c, r, V_TMP);
+      const float wf = (r.x.ex && r.x.act) ? r.x.D * jf : 0.f;
+      const float cs2 = colsum16((const gfloat_t*)xrows(c.L) + c.l * CAP, wf);
+      s4 = tsh(cs2, ddep);
+      s5 = tsh(cs2, 16 + ddep);
+    }
+  }
   float y = 0.f;
   if (c.l < NV) {
     const bool f0 = (c.rmb & 1u) != 0u, f1 = (c.rmb & 2u) != 0u;
-    const bool f2 = (c.rmb & 4u) != 0u, f3 = (c.rmb & 8u) != 0u;
+    /* the pair's static row masks: rmb bits 2-3 (XG 3) or 4-5 (XG 4) */
+    const uint32_t pb = YPAIR<XG> ? (c.rmb >> 4) : (c.rmb >> 2);
+    const bool f2 = (pb & 1u) != 0u, f3 = (pb & 2u) != 0u;
     y = Mp + (f0 ? so : 0.f) + (f1 ? sx : 0.f) + (f2 ? s2 : 0.f) + (f3 ? s3 : 0.f);
+    if constexpr (YPAIR<XG>) {
+      const bool f4 = (r.x.rowmask & 0xFFFFu) != 0u, f5 = (r.x.rowmask >> 16) != 0u;
+      y += (f4 ? s4 : 0.f) + (f5 ? s5 : 0.f);
+    }
     if (r.hf && r.actf) y += r.Df * p;
     if (r.anyl && r.hl && r.actl) y += r.Dl * p;
   }
@@ -2977,17 +3055,19 @@ __device__ __forceinline__ float hmul_pair(const Ctx& c, const Rows& r, const fl
    arithmetic; it stops at a relative residual |r|^2 <= 1e-12 |g|^2 or after 16. Without an active pair
    row it is the tree solve. [The oracle factors the dense H, mju_cholFactor; the two agree to the
    residual.] Team-uniform loop (no matrix cores inside). */
+template <int XG>
 __device__ __forceinline__ float hsolve_pair(const Ctx& c, const Rows& r, const float jr[CAP], float g, float Dinv) {
   const bool isd = c.l < NV;
   float z = solve_ldl(c, g, Dinv);
-  if (team_ballot(r.x.ex && r.x.act) == 0u) return z;
+  const XRow& pr = YPAIR<XG> ? r.y : r.x;
+  if (team_ballot(pr.ex && pr.act) == 0u) return z;
   float x = 0.f, rr = isd ? g : 0.f, p = isd ? z : 0.f;
   float dd[2] = {isd ? rr * z : 0.f, isd ? g * g : 0.f};
   tsum_n<2>(dd);
   float rz = dd[0];
   const float g2 = dd[1];
   for (int it = 0; it < 16; it++) {
-    const float Hp = hmul_pair(c, r, jr, p);
+    const float Hp = hmul_pair<XG>(c, r, jr, p);
     const float pHp = tsum(isd ? p * Hp : 0.f);
     if (!(pHp > 0.f)) break;
     const float alpha = rz / pHp;
@@ -3034,9 +3114,20 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     jwx -= r.x.aref;
     jsx -= r.x.aref;
   }
+  float jwy = 0.f, jsy = 0.f;
+  if constexpr (YPAIR<XG> && XA) {
+    if (r.y.any) {
+      jwy = row_dot_y(c, r, V_TMP);
+      jsy = row_dot_y(c, r, V_TMP2);
+      jwy += xor16f(jwy);
+      jsy += xor16f(jsy);
+      jwy -= r.y.aref;
+      jsy -= r.y.aref;
+    }
+  }
   tsync();
-  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
-                  rows_cost<XG, XA>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx, jwy),
+                  rows_cost<XG, XA>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx, jsy)};
   tsum_n<2>(cws);
   const float cw = cws[0], cs = cws[1];
   if (cw > cs) {
@@ -3044,9 +3135,11 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     Ma = mul_m(c, x, V_TMP);
     r.jar = js;
     r.x.jar = jsx;
+    r.y.jar = jsy;
   } else {
     r.jar = jw;
     r.x.jar = jwx;
+    r.y.jar = jwy;
   }
   STAMP(S_WARM);
   r.jf = x - r.af;
@@ -3058,7 +3151,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float Dinv = hessian_factor<XG, XA>(c, r, true, 0, 0, 0, 0);
   STAMP(S_HESS0);
   float search;
-  if constexpr (XPAIR<XG> && XA) search = -hsolve_pair(c, r, jr, grad, Dinv);
+  if constexpr (ANYPAIR<XG> && XA) search = -hsolve_pair<XG>(c, r, jr, grad, Dinv);
   else search = -solve_ldl(c, grad, Dinv);
   STAMP(S_SOLVE0);
   int it = 0;
@@ -3072,6 +3165,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
     if constexpr (XG && XA) r.x.jar += alpha * r.x.Jv;
+    if constexpr (YPAIR<XG> && XA) r.y.jar += alpha * r.y.Jv;
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     float oldcost = cost;
@@ -3099,7 +3193,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     if (changed) Dinv = hessian_factor<XG, XA>(c, r, false, pa, pf, plo, pa2);
     STAMP(S_HESS);
     float mg;
-    if constexpr (XPAIR<XG> && XA) mg = hsolve_pair(c, r, jr, grad, Dinv);
+    if constexpr (ANYPAIR<XG> && XA) mg = hsolve_pair<XG>(c, r, jr, grad, Dinv);
     else mg = solve_ldl(c, grad, Dinv);
     STAMP(S_SOLVE);
     search = -mg;
@@ -3145,18 +3239,31 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     jwx -= r.x.aref;
     jsx -= r.x.aref;
   }
+  float jwy = 0.f, jsy = 0.f;
+  if constexpr (YPAIR<XG> && XA) {
+    if (r.y.any) {
+      jwy = row_dot_y(c, r, V_TMP);
+      jsy = row_dot_y(c, r, V_TMP2);
+      jwy += xor16f(jwy);
+      jsy += xor16f(jsy);
+      jwy -= r.y.aref;
+      jsy -= r.y.aref;
+    }
+  }
   tsync();
-  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx),
-                  rows_cost<XG, XA>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx)};
+  float cws[2] = {(c.l < NV ? 0.5f * (Ma - fs) * (x - qs) : 0.f) + rows_cost<XG, XA>(c, r, jw, x - r.af, r.sl * x - r.al, jwx, jwy),
+                  rows_cost<XG, XA>(c, r, js, qs - r.af, r.sl * qs - r.al, jsx, jsy)};
   tsum_n<2>(cws);
   if (cws[0] > cws[1]) {
     x = qs;
     Ma = mul_m(c, x, V_TMP);
     r.jar = js;
     r.x.jar = jsx;
+    r.y.jar = jsy;
   } else {
     r.jar = jw;
     r.x.jar = jwx;
+    r.y.jar = jwy;
   }
   STAMP(S_WARM);
   r.jf = x - r.af;
@@ -3180,6 +3287,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
     if constexpr (XG && XA) r.x.jar += alpha * r.x.Jv;
+    if constexpr (YPAIR<XG> && XA) r.y.jar += alpha * r.y.Jv;
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
@@ -3297,7 +3405,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   /* constraints */
   make_constraints<XG>(c, s, ls, B, cm, r);
   STAMP(S_CON);
-  int nrows = tmaxi(r.nrow + (XG ? r.x.nrow : 0) + (r.hf || r.hl ? 1 : 0));
+  int nrows = tmaxi(r.nrow + (XG ? r.x.nrow : 0) + (YPAIR<XG> ? r.y.nrow : 0) + (r.hf || r.hl ? 1 : 0));
   float qacc;
   /* entered by the whole wave when either env has rows (the full Hessian
      build runs on the matrix cores and needs every lane); an env without
@@ -3314,7 +3422,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
       return SOLVER == ZB_SOLVER_CG ? solve_cg<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM, ft)
                                     : solve_newton<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, ft);
     };
-    const float qn = (XG != 0 && r.x.any) ? solve(BoolC<true>{}) : solve(BoolC<false>{});
+    const bool xa = XG != 0 && (r.x.any || (YPAIR<XG> && r.y.any)); /* wave-uniform */
+    const float qn = xa ? solve(BoolC<true>{}) : solve(BoolC<false>{});
     if (nrows > 0) {
       qacc = qn;
       ftot = ft;
@@ -3331,31 +3440,36 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   float fext[6] = {0, 0, 0, 0, 0, 0};
   float cpos[3], cdir[3], cmu;
   (void)contact_point<XG>(c, s, B, 0, cpos, cdir, cmu);
-  float xpos[3], xdir[3];
-  if constexpr (XPAIR<XG>) {
-    if (r.x.any) {
-      /* the pair's row direction n +- mu t; the half on geom1's limb (lanes 16-31) takes -F */
-      float n[3], t1[3], t2[3];
-      (void)pair_contact(c, B, xpos, n, t1, t2);
-      const int edge = c.l & 3;
-      const float sg = (edge & 1) ? -m->pair_friction[0] : m->pair_friction[0];
-      const float hs = (c.l >> 4) ? -1.f : 1.f;
+  float xpos[3], xdir[3], ypos[3], ydir[3];
+  /* the pair's row direction n +- mu t; the half on geom1's limb (lanes 16-31) takes -F */
+  auto pair_dir = [&](float* pos, float* dir) {
+    float n[3], t1[3], t2[3];
+    (void)pair_contact(c, B, pos, n, t1, t2);
+    const int edge = c.l & 3;
+    const float sg = (edge & 1) ? -m->pair_friction[0] : m->pair_friction[0];
+    const float hs = (c.l >> 4) ? -1.f : 1.f;
 #pragma unroll
-      for (int k = 0; k < 3; k++) xdir[k] = hs * (n[k] + sg * (edge < 2 ? t1[k] : t2[k]));
-    }
+    for (int k = 0; k < 3; k++) dir[k] = hs * (n[k] + sg * (edge < 2 ? t1[k] : t2[k]));
+  };
+  if constexpr (XPAIR<XG>) {
+    if (r.x.any) pair_dir(xpos, xdir);
   } else if (XG && r.x.any) {
     (void)contact_point<XG>(c, s, B, 1, xpos, xdir, cmu);
   }
+  if constexpr (YPAIR<XG>) {
+    if (r.y.any) pair_dir(ypos, ydir);
+  }
   const int rgeom = c.l >> 4;
   float tch0 = 0.f, tch1 = 0.f;
-  for (int g = 0; g < (XG ? 2 * NGEOM : NGEOM); g++) {
-    /* geom g: bank g / 2, lanes 16 (g % 2) .. + 15 */
-    const bool b1 = XG && g >= NGEOM;
+  for (int g = 0; g < (YPAIR<XG> ? 3 * NGEOM : XG ? 2 * NGEOM : NGEOM); g++) {
+    /* geom g: bank g / 2, lanes 16 (g % 2) .. + 15 (XG 4: bank 2 = the pair's halves) */
+    const bool b1 = XG && g >= NGEOM && g < 2 * NGEOM, b2 = YPAIR<XG> && g >= 2 * NGEOM;
     if (b1 && !r.x.any) continue; /* wave-uniform */
-    const bool mine = (b1 ? r.x.ex : r.ex) && rgeom == (g & 1);
-    const float rf = b1 ? r.x.f : r.f;
-    const float* pp = b1 ? xpos : cpos;
-    const float* dd = b1 ? xdir : cdir;
+    if (b2 && !r.y.any) continue;
+    const bool mine = (b2 ? r.y.ex : b1 ? r.x.ex : r.ex) && rgeom == (g & 1);
+    const float rf = b2 ? r.y.f : b1 ? r.x.f : r.f;
+    const float* pp = b2 ? ypos : b1 ? xpos : cpos;
+    const float* dd = b2 ? ydir : b1 ? xdir : cdir;
     float F[3] = {0, 0, 0}, tq[3] = {0, 0, 0};
     float fn = 0.f;
     if (mine) {
@@ -3370,7 +3484,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     float fnt = ex7[6];
     /* the pair's halves: g = 2 geom2's body (+F), g = 3 geom1's (-F, in xdir); each foot's touch
        sensor takes the pair's normal force (its geom is in the contact) */
-    const int gg = (XPAIR<XG> && b1) ? m->pair_geom[g == NGEOM ? 1 : 0]
+    const int gg = b2 ? m->pair_geom[g == 2 * NGEOM ? 1 : 0]
+                   : (XPAIR<XG> && b1) ? m->pair_geom[g == NGEOM ? 1 : 0]
                    : (XFLOOR<XG> && b1) ? c.L->s.xsel[g - NGEOM] : g;
     if (gg >= 0 && gg < m->ngeom && c.l == m->geom_body[gg]) {
 #pragma unroll
@@ -3933,7 +4048,8 @@ __device__ __forceinline__ void make_ctx(Ctx& c, const ZbModel* m, const ZbEnvCo
   c.act = t[TP_ACT * TEAM];
   {
     const uint32_t r0 = (uint32_t)t[TP_ROWMASK * TEAM], r1 = (uint32_t)t[TP_ROWMASK2 * TEAM];
-    c.rmb = (r0 & 1u) | ((r0 >> 15) & 2u) | ((r1 & 1u) << 2) | ((r1 >> 13) & 8u);
+    const uint32_t r2 = (uint32_t)t[TP_ROWMASK3 * TEAM]; /* the sole pair's rows beside the floor bank (XG 4) */
+    c.rmb = (r0 & 1u) | ((r0 >> 15) & 2u) | ((r1 & 1u) << 2) | ((r1 >> 13) & 8u) | ((r2 & 1u) << 4) | ((r2 >> 11) & 32u);
   }
   c.dk0 = t[TP_DK0 * TEAM];
   c.dfree = t[TP_DFREE * TEAM];
@@ -4015,7 +4131,7 @@ __global__ __launch_bounds__(64, ZB_WAVES_PER_EU) void step_kernel(StepArgs a) {
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
   /* the env's second-bank rows (a team past n: the spare block n) */
-  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(live ? e : a.n_envs) * ZB_XJ_STRIDE);
+  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(live ? e : a.n_envs) * XJ_STRIDE<XG>);
   /* per-env row addresses are formed where they are used, from an opaque copy of the env
      index: held across the substep loop they were 64-bit values spilled to scratch */
   auto state_row = [&]() { return a.state + (size_t)vopq(ee) * ZB_STATE_STRIDE; };
@@ -4197,7 +4313,7 @@ __global__ __launch_bounds__(64) void reset_kernel(StepArgs a) {
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
   /* the env's second-bank rows (a team past n: the spare block n) */
-  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(inb ? e : a.n_envs) * ZB_XJ_STRIDE);
+  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(inb ? e : a.n_envs) * XJ_STRIDE<XG>);
   float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   float* rnd = live && (cfg->flags & ZB_F_RANDOMIZE) && a.rnd ? a.rnd + (size_t)ee * ZB_RAND_STRIDE : nullptr;
   EnvS& s = c.L->s;
@@ -4229,7 +4345,7 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
   Ctx c;
   make_ctx(c, m, cfg, a.topo, &g_lds[team], a.seed, (uint32_t)(a.env_offset + ee));
   /* the env's second-bank rows (a team past n: the spare block n) */
-  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(live ? e : a.n_envs) * ZB_XJ_STRIDE);
+  if constexpr (XG) set_xrows(c.L, a.xj + (size_t)(live ? e : a.n_envs) * XJ_STRIDE<XG>);
   float* st = a.state + (size_t)ee * ZB_STATE_STRIDE;
   EnvS& s = c.L->s;
   LaneS ls;
@@ -4265,11 +4381,11 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     for (int k = 0; k < 10; k++) d[ZB_DBG_CINERT + 10 * l + k] = c.L->ci[l][k];
     for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
   }
-  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (XG && r.x.ex && (!XPAIR<XG> || l < 16) ? 1 : 0) + (r.hf ? 1 : 0) +
-                               (r.hl ? 1 : 0)));
+  int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (XG && r.x.ex && (!XPAIR<XG> || l < 16) ? 1 : 0) +
+                               (YPAIR<XG> && r.y.ex && l < 16 ? 1 : 0) + (r.hf ? 1 : 0) + (r.hl ? 1 : 0)));
   if (l == 0) {
     d[ZB_DBG_MISC + 0] = (float)nefc;
-    d[ZB_DBG_MISC + 1] = (float)((r.nrow + (XG ? r.x.nrow / (XPAIR<XG> ? 2 : 1) : 0)) / 4);
+    d[ZB_DBG_MISC + 1] = (float)((r.nrow + (XG ? r.x.nrow / (XPAIR<XG> ? 2 : 1) : 0) + (YPAIR<XG> ? r.y.nrow / 2 : 0)) / 4);
     d[ZB_DBG_MISC + 2] = sen.touch[0];
     d[ZB_DBG_MISC + 3] = sen.touch[1];
     for (int k = 0; k < 4; k++) d[ZB_DBG_MISC + 4 + k] = sen.fq[k];
@@ -4300,13 +4416,14 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
 }
 
 /* the kernel instantiation for a handle: solver x collider set (zb_host.cpp needs_xg: 0 two soles,
-   1 / 2 general floor colliders, 3 the sole pair) x implicit damping (ZB_F_EULERDAMP, step kernel
+   1 / 2 general floor colliders, 3 the sole pair, 4 both) x implicit damping (ZB_F_EULERDAMP, step kernel
    only). f(S, X, D) is called with std::integral_constant values. */
 template <typename F>
 __host__ void with_variant(int solver, int xg, int ed, F&& f) {
   using std::integral_constant;
   auto by_xg = [&](auto S, auto D) {
     switch (xg) {
+      case 4: f(S, integral_constant<int, 4>{}, D); break;
       case 3: f(S, integral_constant<int, 3>{}, D); break;
       case 2: f(S, integral_constant<int, 2>{}, D); break;
       case 1: f(S, integral_constant<int, 1>{}, D); break;

@@ -99,9 +99,9 @@ int check_model(const ZbModel* m) {
                            "them knowingly", m->nskip_geom);
   if (m->nskip_pair != 0)
     return fail(ZB_EMODEL, "the source model collides %d pairs of its own geoms with each other; the engine "
-                           "collides the robot with itself only as the two box soles against each other, with no "
-                           "other floor collider: compile_model(..., drop_self_contacts=True) to simulate without "
-                           "them knowingly", m->nskip_pair);
+                           "collides the robot with itself only as the two box soles against each other: "
+                           "compile_model(..., drop_self_contacts=True) to simulate without them knowingly",
+                m->nskip_pair);
   if (m->nbody > 32 || m->nv > 32 || m->nq > ZB_MAX_QPOS)
     return fail(ZB_EMODEL, "model too large for a 32-lane team (nbody=%d nv=%d nq=%d)", m->nbody, m->nv, m->nq);
   /* colliders: two banks of 32 contact-row lanes, 16 rows (4 contacts x 4 pyramid edges) per geom; the
@@ -132,11 +132,12 @@ int check_model(const ZbModel* m) {
   if (m->max_depth > ZB_MAX_DEPTH) return fail(ZB_EMODEL, "dof depth %d > %d", m->max_depth, ZB_MAX_DEPTH);
   if (m->npair < 0 || m->npair > 1) return fail(ZB_EMODEL, "npair=%d: the sole pair at most", m->npair);
   if (m->npair == 1) {
-    /* the sole pair (zb_engine.hip pair_rows): the two box soles, the only floor colliders, on two
-       different limbs (its contact rows are one half-row per limb chain) */
+    /* the sole pair (zb_engine.hip pair_rows): the two box soles (geoms 0 and 1, the touch sensors'),
+       on two different limbs (its contact rows are one half-row per limb chain); with other floor
+       colliders beside them its rows take a bank of their own (XG 4) */
     const int g1 = m->pair_geom[0], g2 = m->pair_geom[1];
-    if (m->ngeom != 2 || !((g1 == 0 && g2 == 1) || (g1 == 1 && g2 == 0)))
-      return fail(ZB_EMODEL, "the sole pair needs exactly the two soles as colliders (ngeom=%d, pair %d-%d)",
+    if (m->ngeom < 2 || !((g1 == 0 && g2 == 1) || (g1 == 1 && g2 == 0)))
+      return fail(ZB_EMODEL, "the sole pair collides the two soles, geoms 0 and 1 (ngeom=%d, pair %d-%d)",
                   m->ngeom, g1, g2);
     if (m->geom_type[0] != ZB_GEOM_BOX || m->geom_type[1] != ZB_GEOM_BOX)
       return fail(ZB_EMODEL, "the sole pair collides two boxes (box-box)");
@@ -194,7 +195,9 @@ int check_model(const ZbModel* m) {
 }
 
 int needs_xg(const ZbModel* m) {
-  if (m->npair > 0) return 3; /* the two soles and their pair (the second bank holds the pair's rows) */
+  /* the sole pair: alone with the soles (XG 3, the second bank holds the pair's rows), or beside other
+     floor colliders (XG 4: the floor bank and a third bank for the pair's rows) */
+  if (m->npair > 0) return m->ngeom > 2 ? 4 : 3;
   /* ZB_FORCE_XG=1 (profiling only): the two-sole model on the general-collider instantiation, whose
      second bank then stays empty, to time that kernel's overhead on the headline's work */
   const char* fx = getenv("ZB_FORCE_XG");
@@ -272,17 +275,23 @@ void build_topology(const ZbModel* m, int32_t t[zb::TP_NF][zb::TOPO_LANES]) {
       const int kd = m->body_lastdof[m->geom_body[g]];
       if (isd && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm[g / 2] |= 0xFFFFu << (16 * (g % 2));
     }
+    uint32_t rp = 0u;
     if (m->npair > 0) {
-      /* the sole pair's rows (second bank): lanes 0-15 the half rows on geom2's limb (+J), lanes 16-31
-         those on geom1's limb (-J); the root dofs' columns cancel, so a limb dof only */
-      rm[1] = 0u;
+      /* the sole pair's rows (the second bank with the soles alone, XG 3; a third bank beside other
+         floor colliders, XG 4): lanes 0-15 the half rows on geom2's limb (+J), lanes 16-31 those on
+         geom1's limb (-J); the root dofs' columns cancel, so a limb dof only */
       for (int h = 0; h < 2; h++) {
         const int kd = m->body_lastdof[m->geom_body[m->pair_geom[1 - h]]];
-        if (isd && l >= 6 && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rm[1] |= 0xFFFFu << (16 * h);
+        if (isd && l >= 6 && kd >= 0 && (kd == l || ((desc >> kd) & 1u))) rp |= 0xFFFFu << (16 * h);
+      }
+      if (m->ngeom == 2) {
+        rm[1] = rp;
+        rp = 0u;
       }
     }
     t[TP_ROWMASK][l] = (int32_t)rm[0];
     t[TP_ROWMASK2][l] = (int32_t)rm[1];
+    t[TP_ROWMASK3][l] = (int32_t)rp;
     t[TP_DK0][l] = isd ? l - m->body_dofadr[dbody] : 0;
     t[TP_DFREE][l] = (isd && m->body_jnttype[dbody] == ZB_JNT_FREE) ? 1 : 0;
     int hd = -1, ln = 0;

@@ -18,7 +18,7 @@ namespace zb {
    [TP_NF][32] int32 */
 enum {
   TP_BPAR, TP_BDEP, TP_BJT, TP_BDOFADR, TP_BLAST, TP_NCH, TP_CH0, TP_CH1, TP_LVL_LO, TP_LVL_HI,
-  TP_DDEP, TP_DBODY, TP_QADR, TP_ACT, TP_ROWMASK, TP_ROWMASK2, TP_DK0, TP_DFREE, TP_CHD, TP_CPS, TP_CLN, TP_NF
+  TP_DDEP, TP_DBODY, TP_QADR, TP_ACT, TP_ROWMASK, TP_ROWMASK2, TP_ROWMASK3, TP_DK0, TP_DFREE, TP_CHD, TP_CPS, TP_CLN, TP_NF
 };
 constexpr int TOPO_LANES = 32;
 constexpr int TOPO_NROOT = 6;  /* root dof chain (the free joint), zb_engine.hip NROOT */
@@ -31,7 +31,7 @@ int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int check_model(const ZbModel* m);
 int check_cfg(const ZbEnvConfig* c);
 /* the model needs the general-collider kernels (anything but exactly two box soles) */
-int needs_xg(const ZbModel* m); /* 0 two-sole, 1 general colliders, 2 with cylinders / ellipsoids */
+int needs_xg(const ZbModel* m); /* 0 two-sole, 1 general colliders, 2 with cylinders / ellipsoids / meshes, 3 the sole pair alone, 4 the sole pair beside other colliders */
 /* requires check_model(m) == ZB_OK */
 void build_topology(const ZbModel* m, int32_t t[TP_NF][TOPO_LANES]);
 

@@ -665,8 +665,9 @@ GEOM_SOLIMP = (0.9, 0.95, 0.001, 0.5, 2.0)
 
 def _compile_pairs(m, desc: dict, geoms: list, geom_names: list, drop: bool) -> None:
     """The robot's own colliding pairs (desc["self_pairs"]): the engine simulates the two box soles
-    against each other (ZbModel.npair = 1; box-box) when that is the only pair and the soles are the
-    only floor colliders; any other pair is counted into nskip_pair, which zb_create refuses.
+    against each other (ZbModel.npair = 1; box-box), beside any other floor colliders (round 6: their
+    rows in a bank of their own, the XG 4 kernels); any other pair is counted into nskip_pair, which
+    zb_create refuses.
     drop=True: none of them (npair = nskip_pair = 0). The pair's parameters are MuJoCo's mix for two
     geoms of equal priority (mj_contactParam): friction the larger per component, solref / solimp the
     mean (solmix 1 each), margin the larger [U: MuJoCo's mixing rule restated from its documentation]."""
@@ -674,12 +675,12 @@ def _compile_pairs(m, desc: dict, geoms: list, geom_names: list, drop: bool) -> 
     pairs = [] if drop else [list(p) for p in desc.get("self_pairs", [])]
     soles = {geom_names[m.geom_left_foot], geom_names[m.geom_right_foot]}
     by_name = {g["name"]: g for g in geoms}
-    if (len(pairs) == 1 and set(pairs[0]) == soles and len(geoms) == 2
-            and all(by_name[n].get("type", "box") == "box" for n in soles)):
-        g1, g2 = (geom_names.index(n) for n in pairs[0])
+    sole = [p for p in pairs if set(p) == soles]
+    if sole and all(by_name[n].get("type", "box") == "box" for n in soles):
+        g1, g2 = (geom_names.index(n) for n in sole[0])
         m.npair = 1
         m.pair_geom[0], m.pair_geom[1] = g1, g2
-        a, b = by_name[pairs[0][0]], by_name[pairs[0][1]]
+        a, b = by_name[sole[0][0]], by_name[sole[0][1]]
         fa, fb = a.get("friction", GEOM_FRICTION), b.get("friction", GEOM_FRICTION)
         for k in range(3):
             m.pair_friction[k] = max(float(fa[k]), float(fb[k]))
@@ -690,7 +691,7 @@ def _compile_pairs(m, desc: dict, geoms: list, geom_names: list, drop: bool) -> 
         for k in range(5):
             m.pair_solimp[k] = 0.5 * (float(ia[k]) + float(ib[k]))
         m.pair_margin = max(float(a.get("margin", 0.0)), float(b.get("margin", 0.0)))
-        pairs = []
+        pairs = [p for p in pairs if set(p) != soles]
     m.nskip_pair = len(pairs)
 
 

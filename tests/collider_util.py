@@ -434,3 +434,32 @@ def crossing_states(cm, n: int, seed: int, air: bool = True) -> np.ndarray:
     if air:
         out[:, 2] = 1.0
     return out
+
+
+def limbs_pair_desc() -> dict:
+    """The limbs model (soles + right shin box + left hand capsule) whose two soles also collide with
+    each other (round 6: the sole pair beside other floor colliders, the XG 4 kernels)."""
+    d = limbs_desc()
+    d["self_pairs"] = [["left_foot_sole", "right_foot_sole"]]
+    return d
+
+
+def crossing_touching_states(cm, n: int, seed: int, depth=0.003) -> np.ndarray:
+    """qpos [n, 27] with the legs crossed as in crossing_states (the soles interpenetrate) and the
+    robot on the floor: even envs standing at the reset height, odd envs lying (a random heading,
+    pitched or rolled 45..135 degrees, as touching_states) with the lowest collider point U(0, depth)
+    below the floor, so that the shin or hand colliders touch it while the soles cross."""
+    rng = np.random.default_rng(seed + 1000)
+    out = crossing_states(cm, n, seed, air=False)
+    for e in range(1, n, 2):
+        yaw, tilt, ax = rng.uniform(-np.pi, np.pi), rng.uniform(np.pi / 4, 3 * np.pi / 4), rng.integers(2)
+        qy = np.array([np.cos(yaw / 2), 0, 0, np.sin(yaw / 2)])
+        qt = np.array([np.cos(tilt / 2), np.sin(tilt / 2) * (ax == 0), np.sin(tilt / 2) * (ax == 1), 0])
+        w1, x1, y1, z1 = qy
+        w2, x2, y2, z2 = qt
+        quat = np.array([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                         w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2])
+        out[e, 3:7] = quat / np.linalg.norm(quat)
+        out[e, 2] = 0.0
+        out[e, 2] = -lowest_point(cm, out[e]) - rng.uniform(0.0, depth)
+    return out

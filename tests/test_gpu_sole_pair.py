@@ -23,18 +23,30 @@ def torch_gpu():
     return torch
 
 
-@pytest.fixture(scope="module")
-def pair_model():
-    return compile_model(U.sole_pair_desc())
+# "pair": the soles alone (the XG 3 kernels); "limbs_pair" (round 6): the pair beside
+# the limbs model's shin box and hand capsule (the XG 4 kernels: the floor colliders in the second bank,
+# the pair in a third)
+PAIR_MODELS = {"pair": U.sole_pair_desc, "limbs_pair": U.limbs_pair_desc}
+
+
+@pytest.fixture(scope="module", params=list(PAIR_MODELS))
+def pair_model(request):
+    cm = compile_model(PAIR_MODELS[request.param]())
+    cm.variant = request.param
+    return cm
 
 
 def crossing_env(O, cm, cfg, n, seed):
-    """An oracle env at crossing_states: half in the air, half at the reset height (the soles on the
-    floor as well), at rest, no warm start."""
+    """An oracle env at crossing states, at rest, no warm start: "pair" half in the air, half at the
+    reset height (the soles on the floor as well); "limbs_pair" half standing, half lying with the shin
+    or hand on the floor (collider_util.crossing_touching_states), every bank in use."""
     env = O.OracleEnv(cm.cmodel, cfg, n, seed=seed)
     env.reset()
-    q = np.concatenate([U.crossing_states(cm, n // 2, seed, air=True), U.crossing_states(cm, n - n // 2, seed + 1,
-                                                                                          air=False)])
+    if getattr(cm, "variant", "pair") == "limbs_pair":
+        q = U.crossing_touching_states(cm, n, seed)
+    else:
+        q = np.concatenate([U.crossing_states(cm, n // 2, seed, air=True),
+                            U.crossing_states(cm, n - n // 2, seed + 1, air=False)])
     env.state[:, :27] = q.astype(np.float32)
     env.state[:, 32:58] = 0.0
     env.state[:, cs.S_QACCW:cs.S_QACCW + 32] = 0.0
@@ -56,8 +68,9 @@ def test_debug_forward_matches_oracle(torch_gpu, pair_model, oracle_mod, solver)
     ctrl = (np.random.default_rng(2).normal(size=(n, 20)) * 0.5).astype(np.float32)
     eng = HipEngine(cm, cfg, n)
     g = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()
-    worst, npair = 0.0, 0
+    worst, npair, nfloor = 0.0, 0, 0
     for e in range(n):
+        nfloor += int(any(len(cc) for cc in U.contacts(cm, st[e, :27].astype(np.float64))[2:]))
         ref = oracle_mod.forward_debug(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
         assert int(g[e, DBG["misc"] + 1]) == ref["ncon"], e
         assert int(g[e, DBG["misc"]]) == ref["nefc"], e
@@ -70,9 +83,11 @@ def test_debug_forward_matches_oracle(torch_gpu, pair_model, oracle_mod, solver)
         # iterations along rounding-sensitive paths
         assert err <= (1e-3 if solver == "newton" else 5e-2), (e, err)
         np.testing.assert_allclose(g[e, DBG["misc"] + 2:DBG["misc"] + 4], ref["touch"], rtol=2e-3, atol=2e-3)
-    print(f"\n[sole pair {solver} debug forward] {npair} of {n} envs with pair contacts, max relative qacc "
-          f"error {worst:.2e}")
+    print(f"\n[sole pair {cm.variant} {solver} debug forward] {npair} of {n} envs with pair contacts, {nfloor} with "
+          f"floor contacts beyond the soles, max relative qacc error {worst:.2e}")
     assert npair >= n // 2
+    if cm.variant == "limbs_pair":
+        assert nfloor >= n // 8
 
 
 # One env-step from a crossing state at rest, fp32 engine vs fp32 oracle (the MaxErr contract of the
@@ -107,7 +122,7 @@ def test_one_step_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
     # envs per output and step within CG_LOOSE x beyond it (round 5 held CG to the flat COLLIDER_TOL_CG
     # with up to 12 envs at a discontinuity)
     kw = dict(budget=CG_BUDGET, loose=CG_LOOSE, max_ill=n, k_slack=CG_SLACK) if cg else {}
-    err = MaxErr(f"sole pair {solver} one-step", **kw)
+    err = MaxErr(f"sole pair {cm.variant} {solver} one-step", **kw)
     for t in range(2):
         st0, rd0 = env.state.copy(), env.rand.copy()
         eng.set_state(torch.from_numpy(st0.copy()))
@@ -197,7 +212,7 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, pair_model, oracle_mod, so
         done.append(o["done"].cpu().numpy().copy())
     rew, done = np.stack(rew), np.stack(done)
     np.testing.assert_array_equal(done[:GOLDEN_EXACT_STEPS], g["done"][:GOLDEN_EXACT_STEPS])
-    err = MaxErr(f"sole pair {solver} rollout from reset")
+    err = MaxErr(f"sole pair {cm.variant} {solver} rollout from reset")
     tol = GOLDEN_TOL_CG if solver == "cg" else GOLDEN_TOL
     # The box-box contact set switches (which clip candidates make the four manifold points, a face
     # or an edge axis) as the soles slide over each other: each is a discontinuity two fp32
@@ -206,10 +221,10 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, pair_model, oracle_mod, so
     # exact window is 3 steps and the ensemble contract covers the 48
     for t in range(3):
         err.add(f"reward[{t}]", rew[t], g["reward"][t], tol["reward"], ref64=r64s[t])
-    print(f"\n[sole pair {solver} rollout] oracle env-steps with pair contacts (every 4th env): {touching} of "
+    print(f"\n[sole pair {cm.variant} {solver} rollout] oracle env-steps with pair contacts (every 4th env): {touching} of "
           f"{steps * n // 4}")
     assert touching > 0
-    golden_ensemble_check(f"sole pair {solver}", rew, done, eng.get_state().cpu().numpy(), g)
+    golden_ensemble_check(f"sole pair {cm.variant} {solver}", rew, done, eng.get_state().cpu().numpy(), g)
     err.report()
 
 

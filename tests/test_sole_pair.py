@@ -40,7 +40,7 @@ def test_other_self_pairs_are_still_refused():
     d = U.sole_pair_desc()
     d["self_pairs"].append(["left_foot_sole", "torso_box"])
     m = compile_model(d).cmodel
-    assert m.npair == 0 and m.nskip_pair == 2
+    assert m.npair == 1 and m.nskip_pair == 1  # the soles' pair is simulated, the other one is not
     L = E.load_library()
     h = C.c_void_p()
     assert L.zb_create(C.byref(m), C.byref(default_config(solver="newton")), 4, 0, 0, 0, C.byref(h)) == -4
@@ -50,6 +50,34 @@ def test_other_self_pairs_are_still_refused():
     assert rc != -4, L.zb_last_error()
     if rc == 0:
         L.zb_destroy(h)
+
+
+def test_sole_pair_beside_floor_colliders_compiles(oracle_mod):
+    """Round 6: the sole pair beside other floor colliders (the limbs model's shin
+    box and hand capsule) compiles to npair 1 with all four colliders and passes zb_create's model
+    checks (the XG 4 kernels: the floor bank and a bank of its own for the pair); the oracle collides
+    both the pair and every floor collider."""
+    from zbot_amd import engine as E
+
+    cm = compile_model(U.limbs_pair_desc())
+    m = cm.cmodel
+    assert m.npair == 1 and m.nskip_pair == 0 and m.ngeom == 4
+    assert sorted([m.pair_geom[0], m.pair_geom[1]]) == [0, 1]
+    L = E.load_library()
+    h = C.c_void_p()
+    rc = L.zb_create(C.byref(m), C.byref(default_config()), 4, 0, 0, 0, C.byref(h))
+    assert rc != -4, L.zb_last_error()
+    if rc == 0:
+        L.zb_destroy(h)
+    # the crossing-and-touching states hold pair contacts and floor contacts of the shin / hand
+    q = U.crossing_touching_states(cm, 32, 3)
+    cfg = default_config()
+    npair = nfloor = 0
+    for e in range(32):
+        p = oracle_mod.constraint_problem(m, cfg, q[e], np.zeros(26), precision="f64")
+        npair += int(((p["type"] == 2) & (np.abs(p["J"][:, :6]).max(1) == 0)).any())
+        nfloor += int(len(U.contacts(cm, q[e])[2]) + len(U.contacts(cm, q[e])[3]) > 0)
+    assert npair >= 8 and nfloor >= 8, (npair, nfloor)
 
 
 def test_pair_rows_are_internal_and_repulsive(oracle_mod):
