@@ -317,6 +317,47 @@ def bench_ksim_env(cm, n: int, steps: int, warmup: int, dev, rank: int, world: i
     }
 
 
+# the step kernel's SQ wave-cycle PMC pass (scripts/pmc_latency.sh -> profiles/), per (solver, envs)
+LATENCY_FILE = "r06_pmc_latency.json"
+
+
+def latency_block(solver: str, n: int, kernel_ms: float, substeps: int, cus: int, train_leg: dict | None) -> dict | None:
+    """The step kernel against its latency floor: from the SQ wave-cycle PMC pass of the
+    same kernel (scripts/pmc_latency.sh, LATENCY_FILE), per physics substep and wave, the wave's lifetime
+    (SQ_WAVE_CYCLES) and its issue floor (SQ_ACTIVE_INST_ANY: the cycles the wave spends issuing, its
+    lifetime if no instruction ever waited on a dependency); latency_frac = floor / lifetime. At 512 envs
+    (train.py's size: 256 waves, each alone on its SIMD) that is the kernel's whole budget; at the
+    headline's 8192 two waves share each SIMD and the partner's issue counts as wait. The live part:
+    the kernel's HIP-event time over rounds x the PMC wave lifetime gives the clock the live run ran at
+    (a check that the profile and the timed run are the same kernel: MI355X runs 1.9-2.4 GHz)."""
+    path = os.path.join(ROOT, "profiles", LATENCY_FILE)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        lj = json.load(f)
+
+    def row(envs):
+        r = lj.get(f"{solver}_{envs}")
+        if r is None:
+            return None
+        ps = r["per_substep"]
+        return {"envs": envs, "wave_lifetime_cycles_per_substep": ps["lifetime_cycles"],
+                "issue_floor_cycles_per_substep": ps["issue_floor_cycles"], "latency_frac": r["latency_frac"],
+                "valu_insts_per_wave": r["per_wave"]["INSTS_VALU"]}
+
+    out = {"kernel": "zb::step_kernel", "solver": solver, "source": f"profiles/{LATENCY_FILE} (scripts/pmc_latency.sh)",
+           "train_size": row(512), "bench_size": row(n)}
+    b = out["bench_size"]
+    if b is not None and kernel_ms > 0:
+        waves = n // 2  # two envs per wave
+        rounds = -(-waves // (cus * 4 * 2))  # 256 VGPRs: two waves per SIMD, four SIMDs per CU
+        out["live"] = {"kernel_ms": kernel_ms, "rounds": rounds,
+                       "implied_clock_ghz": rounds * b["wave_lifetime_cycles_per_substep"] * substeps / (kernel_ms * 1e6)}
+    if train_leg is not None:
+        out["train_defaults_ms_per_step"] = train_leg.get("ms_per_step")
+    return out
+
+
 def bench_train_defaults(cm, dev, rank: int, world: int, seed: int, n: int = 512, T: int = 200) -> dict:
     """train.py's own training size (train.py:1770 num_envs=512, :1775 rollout_length_seconds 4.0 at
     ctrl_dt 0.02 = 200 steps): one 200-step rollout of 512 envs per GPU from reset through
@@ -1001,6 +1042,9 @@ def main(argv: list | None = None) -> None:
                         "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 lane-FLOP; the binding resource of this "
                         "latency/VALU-bound kernel",
             },
+            "latency": latency_block(args.solver, n // G, avg_ms, cfg.n_substeps,
+                                     torch.cuda.get_device_properties(dev).multi_processor_count,
+                                     extra_legs.get("train_defaults")),
             "process_group": dist.get_backend() if dist.is_initialized() else None,
             "episode_stats": {
                 "episodes_done": float(total_stats[2].item()),

@@ -81,6 +81,7 @@ class MaxErr:
         self.max_ill = max_ill
         self.over = set()  # envs over the bound in the last add() calls (cleared by take_over())
         self.exempted = set()  # (output, env, excess / tol) of boundary envs over the bound (add exempt=)
+        self.kneed = {}  # output -> the largest budget + 1 slack multiples needed by an env (one step)
 
     def add(self, key, got, ref, tol, rtol=0.0, ref64=None, loose_abs=None, sens=None, exempt=None):
         """Record |got - ref| against tol + rtol |ref| elementwise (rows = envs; asserted in
@@ -117,6 +118,12 @@ class MaxErr:
             return
         excess = d - rtol * np.abs(ref) - slack
         rows = excess.reshape(excess.shape[0], -1).max(1) if excess.ndim > 1 else excess
+        if ref64 is not None:
+            # the slack multiple each env needs to be within tol (printed: how much of k_slack is used)
+            raw = (d - rtol * np.abs(ref)).reshape(d.shape[0], -1).max(1) - tol
+            kn = np.where(raw > 0, raw / np.maximum(gap.reshape(-1), 1e-30), 0.0)
+            top = sorted(kn.tolist(), reverse=True)[:self.budget + 1]
+            self.kneed[key] = max(self.kneed.get(key, [0.0]), top)
         n_over = int((rows > tol).sum())
         self.over |= set(np.nonzero(rows > tol)[0].tolist())
         self.nout[key] = max(self.nout.get(key, 0), n_over)
@@ -139,6 +146,10 @@ class MaxErr:
 
     def report(self):
         print(f"\n[{self.name}] max |error|: " + ", ".join(f"{k} {v:.2e}" for k, v in self.err.items()))
+        if self.kneed:
+            print(f"[{self.name}] slack multiples needed (k_slack {self.k_slack:g}; the largest {self.budget + 1} envs of "
+                  "the worst step): " + ", ".join(f"{k} " + "/".join(f"{x:.2g}" for x in v)
+                                                  for k, v in self.kneed.items()))
         if any(self.nout.values()):
             print(f"[{self.name}] envs over the bound (solver exit-iteration budget {self.budget}): "
                   + ", ".join(f"{k} {v}" for k, v in self.nout.items() if v))
@@ -217,7 +228,7 @@ ONE_STEP_TOL = {
 # two fp32 implementations of it part by about as much as fp32 and fp64 do, env by env. The contract is
 # Newton's bounds (ONE_STEP_TOL) plus, per env, CG_SLACK x the step's own measured sensitivity: the larger
 # of the fp32/fp64 oracle gap and the spread of the fp32 oracle under 1-ulp perturbations of its input
-# (oracle_sensitivity, 4 draws; the engine is one more such draw, so a small multiple of the largest of
+# (oracle_sensitivity, 16 draws over qpos and qvel; the engine is one more such draw, so a small multiple of the largest of
 # them). At most CG_BUDGET envs per output and step may exceed that, within CG_LOOSE x
 # Newton's bound beyond the slack, unless their step starts with a contact at its activation boundary
 # (boundary_envs: the cause, shown per env). Measured on MI355X (r06, tests/diag_cg_contract.py): 0-2
@@ -268,10 +279,11 @@ def oracle_steps(O, cm, cfg, env, a, seed):
     return ref, ref64
 
 
-def oracle_sensitivity(O, cm, cfg, state, rand, a, seed, ref, draws=4):
+def oracle_sensitivity(O, cm, cfg, state, rand, a, seed, ref, draws=16):
     """The step's sensitivity to a rounding-level change of its input, per output and env: the fp32
-    oracle stepped from the same state with every qvel component scaled by 1 +- 2^-23 (one fp32 ulp,
-    `draws` random sign patterns), the largest |output - ref| over the draws (ref: the unperturbed
+    oracle stepped from the same state with every qpos and qvel component scaled by 1 +- 2^-23 (one
+    fp32 ulp, `draws` random sign patterns: the engine's kinematics round the pose as differently as
+    its dynamics round the velocity), the largest |output - ref| over the draws (ref: the unperturbed
     fp32 step's outputs, {output: value}). For CG this is the scale of the disagreement between any
     two fp32 implementations of the same unconverged 8-iteration solve: an
     env whose solve amplifies one ulp into 1e-4 of qvel would part from any other fp32 CG by as much."""
@@ -284,6 +296,8 @@ def oracle_sensitivity(O, cm, cfg, state, rand, a, seed, ref, draws=4):
         ep.rand[:] = rand
         sgn = rng.choice([-1.0, 1.0], size=(n, 26)).astype(np.float32)
         ep.state[:, 32:58] *= (np.float32(1.0) + sgn * np.float32(2.0 ** -23))
+        sgq = rng.choice([-1.0, 1.0], size=(n, 27)).astype(np.float32)
+        ep.state[:, :27] *= (np.float32(1.0) + sgq * np.float32(2.0 ** -23))
         rp = ep.step(a)
         for key, _, want in one_step_outputs(ep.state, rp, ep.state, rp):
             d = np.abs(np.asarray(want, np.float64) - np.asarray(ref[key], np.float64)).reshape(n, -1).max(1)

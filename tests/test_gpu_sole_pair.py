@@ -53,6 +53,18 @@ def crossing_env(O, cm, cfg, n, seed):
     return env
 
 
+def tie_member(O, cm, cfg, st, ctrl, got, draws=32):
+    """The fp32 oracle's forward pass from qpos scaled by 1 +- 2^-23 (random signs, `draws` draws):
+    the first member whose (ncon, nefc) is `got`, or None."""
+    rng = np.random.default_rng(12345)
+    for _ in range(draws):
+        q = st[:27] * (np.float32(1.0) + rng.choice([-1.0, 1.0], size=27).astype(np.float32) * np.float32(2.0 ** -23))
+        r = O.forward_debug(cm.cmodel, cfg, q, st[32:58], ctrl)
+        if (r["ncon"], r["nefc"]) == got:
+            return r
+    return None
+
+
 @pytest.mark.parametrize("solver", ["newton", "cg"])
 def test_debug_forward_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
     """One forward pass: contact and constraint counts exact (floor + pair), the constrained
@@ -68,12 +80,20 @@ def test_debug_forward_matches_oracle(torch_gpu, pair_model, oracle_mod, solver)
     ctrl = (np.random.default_rng(2).normal(size=(n, 20)) * 0.5).astype(np.float32)
     eng = HipEngine(cm, cfg, n)
     g = eng.debug_forward(torch.from_numpy(st), torch.from_numpy(ctrl)).cpu().numpy()
-    worst, npair, nfloor = 0.0, 0, 0
+    worst, npair, nfloor, ties = 0.0, 0, 0, []
     for e in range(n):
         nfloor += int(any(len(cc) for cc in U.contacts(cm, st[e, :27].astype(np.float64))[2:]))
         ref = oracle_mod.forward_debug(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
-        assert int(g[e, DBG["misc"] + 1]) == ref["ncon"], e
-        assert int(g[e, DBG["misc"]]) == ref["nefc"], e
+        got = (int(g[e, DBG["misc"] + 1]), int(g[e, DBG["misc"]]))
+        if got != (ref["ncon"], ref["nefc"]):
+            # a tie in the box-box manifold selection (the fourth point: the first maximum of two
+            # distances equal to rounding, or the deepest point again): the fp32 oracle from the state
+            # scaled by 1 +- 1 ulp takes either branch (r06 env 31 of limbs_pair: 5 contacts in 12 of
+            # 16 draws, 6 in 4); the engine must match a member of that ensemble, against which its
+            # qacc is then checked
+            ref = tie_member(oracle_mod, cm, cfg, st[e], ctrl[e], got)
+            assert ref is not None, (e, got)
+            ties.append(e)
         p = oracle_mod.constraint_problem(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
         npair += int(((p["type"] == 2) & (np.abs(p["J"][:, :6]).max(1) == 0)).sum() > 0)
         qa = g[e, DBG["qacc"]:DBG["qacc"] + 26]
@@ -84,7 +104,8 @@ def test_debug_forward_matches_oracle(torch_gpu, pair_model, oracle_mod, solver)
         assert err <= (1e-3 if solver == "newton" else 5e-2), (e, err)
         np.testing.assert_allclose(g[e, DBG["misc"] + 2:DBG["misc"] + 4], ref["touch"], rtol=2e-3, atol=2e-3)
     print(f"\n[sole pair {cm.variant} {solver} debug forward] {npair} of {n} envs with pair contacts, {nfloor} with "
-          f"floor contacts beyond the soles, max relative qacc error {worst:.2e}")
+          f"floor contacts beyond the soles, max relative qacc error {worst:.2e}, manifold ties {ties}")
+    assert len(ties) <= 2
     assert npair >= n // 2
     if cm.variant == "limbs_pair":
         assert nfloor >= n // 8
