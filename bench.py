@@ -349,6 +349,8 @@ def latency_block(solver: str, n: int, kernel_ms: float, substeps: int, cus: int
            "train_size": row(512), "bench_size": row(n)}
     b = out["bench_size"]
     if b is not None and kernel_ms > 0:
+        # the n envs' waves over all of the GPU's wave slots (the env groups' launches run concurrently,
+        # each lasting about as long as the rounds of the whole set)
         waves = n // 2  # two envs per wave
         rounds = -(-waves // (cus * 4 * 2))  # 256 VGPRs: two waves per SIMD, four SIMDs per CU
         out["live"] = {"kernel_ms": kernel_ms, "rounds": rounds,
@@ -1042,7 +1044,7 @@ def main(argv: list | None = None) -> None:
                         "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 lane-FLOP; the binding resource of this "
                         "latency/VALU-bound kernel",
             },
-            "latency": latency_block(args.solver, n // G, avg_ms, cfg.n_substeps,
+            "latency": latency_block(args.solver, n, avg_ms, cfg.n_substeps,
                                      torch.cuda.get_device_properties(dev).multi_processor_count,
                                      extra_legs.get("train_defaults")),
             "process_group": dist.get_backend() if dist.is_initialized() else None,

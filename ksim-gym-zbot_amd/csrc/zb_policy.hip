@@ -25,11 +25,6 @@
  *   The carry of layer l + 1 is loaded from HBM into registers while layer l
  *   runs (its latency hides behind the MFMAs) and layer l's new carry is
  *   written at its end ([n][5][128] fp32, 2.5 KB per env per step).
- *   One-step launches (round 6) take layer l + 1's W_hh h products, which
- *   need only its carry, beside layer l's GRU epilogue, so the matrix cores
- *   run while the epilogue's transcendental VALU work issues; the persistent
- *   T-step form keeps every layer's carry in registers and has no room for
- *   that second set of accumulators.
  *
  * Numerics (bit-identical to the oracle): every product is the matrix core's
  * k-ordered fp32 fmaf chain from 0, biases are added afterwards, elementwise
@@ -91,8 +86,11 @@ __device__ __forceinline__ void tile_gemm(const float* xs, const float4* wp, int
   }
 }
 
-/* PERSIST: the persistent T-step form (a0.T > 1), whose carries stay in registers between steps;
-   the one-step form (T = 1) keeps no such registers (190 VGPRs against 256 with spills) */
+/* PERSIST: the persistent T-step form (a0.T > 1), whose carries stay in registers between steps. The
+   one-step form (T = 1) is its own instantiation, so it keeps no such registers: round 5's one kernel
+   for both spilled in the one-step launches too (the critic 121 VGPRs; actor 19), round 6 splits it
+   (one-step actor 0.111 -> 0.107 ms, critic 0.134 -> 0.111 ms at 8192 envs, no spills, the same bits;
+   profiles/r06_p11_policy_ab.log). */
 template <int KIN, int NOUT, bool ACTOR, bool PERSIST>
 __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
 #pragma clang fp contract(off)
@@ -105,7 +103,7 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
   constexpr int UW = XIN > OUTW ? XIN : OUTW;
   __shared__ float su[UW];          /* observation tile [k][env]; then the actor output [env][c] */
   __shared__ float sx[2][H * LDA];  /* layer input / output [unit][env], ping-pong */
-  __shared__ float sh[PERSIST ? 1 : 2][H * LDA]; /* carries [unit][env]: layer l's in sh[l & 1] */
+  __shared__ float sh[H * LDA];     /* carry of the current layer [unit][env] */
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c16 = lane & 15, k4 = lane >> 4;
@@ -196,281 +194,127 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
       su[k * LDA + e] = 0.f;
     }
   }
+  __syncthreads();
+
+  /* 2. input projection (no activation: train.py:944): the wave's unit tile */
+  {
+    const int unit = 16 * w + c16;
+    f32x4 acc[NET];
+    tile_gemm(su, wp4 + (size_t)w * GIN * 64 + lane, GIN, lane, acc);
+    const float bu = a.bias[unit];
+#pragma unroll
+    for (int et = 0; et < NET; ++et)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) sx[0][unit * LDA + crow(et, v, lane)] = acc[et][v] + bu;
+  }
+
+  /* 3. GRU stack (train.py:945-948) */
   const size_t off_gru = (size_t)(H / 16) * GIN * 64;  /* float4 offset of layer 0's W_ih pack */
   constexpr size_t MAT = (size_t)(3 * H / 16) * GH * 64; /* one packed [3H][H] matrix, float4 */
   int cur = 0;
-  if constexpr (PERSIST) {
-    /* the persistent T-step form: each layer's W_ih x and W_hh h inside the layer, the carries of every
-       layer in registers between steps (round 5) */
-    __syncthreads();
-    /* 2. input projection (no activation: train.py:944): the wave's unit tile */
-    {
-      const int unit = 16 * w + c16;
-      f32x4 acc[NET];
-      tile_gemm(su, wp4 + (size_t)w * GIN * 64 + lane, GIN, lane, acc);
-      const float bu = a.bias[unit];
-#pragma unroll
-      for (int et = 0; et < NET; ++et)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) sx[0][unit * LDA + crow(et, v, lane)] = acc[et][v] + bu;
-    }
-
-    /* 3. GRU stack (train.py:945-948) */
-    for (int l = 0; l < D; ++l) {
-      if (t == 0) {
-        /* carry of layer l (prefetched during layer l - 1) -> sh */
-#pragma unroll
-        for (int j = 0; j < CPT; ++j) {
-          const int i = tid + j * NTHR;
-          const int e = i / (H / 4), q = i - e * (H / 4);
-          sh[0][(4 * q) * LDA + e] = cr[j].x;
-          sh[0][(4 * q + 1) * LDA + e] = cr[j].y;
-          sh[0][(4 * q + 2) * LDA + e] = cr[j].z;
-          sh[0][(4 * q + 3) * LDA + e] = cr[j].w;
-        }
-      } else {
-        /* persistent: the previous step's carry from registers (zero where the episode restarts) */
-        const int unit = 16 * w + c16;
-#pragma unroll
-        for (int et = 0; et < NET; ++et)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int e = crow(et, v, lane), ge = e0 + e;
-            float hv = hreg[0][et][v];
-#pragma unroll
-            for (int k = 1; k < D; ++k) hv = l == k ? hreg[k][et][v] : hv;
-            const bool rs = ge >= a.n || (a.reset && a.reset[ge]);
-            sh[0][unit * LDA + e] = rs ? 0.f : hv;
-          }
-      }
-      __syncthreads();
-      if (t == 0 && l + 1 < D) load_carry(l + 1);
-
-      const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
-      const float4* whh = wih + MAT;
-      const float* xs = sx[cur];
-      /* gate tiles of this wave's units: r = w, z = 8 + w, n = 16 + w */
-      size_t to[3];
-#pragma unroll
-      for (int gt = 0; gt < 3; ++gt) to[gt] = (size_t)(8 * gt + w) * GH * 64;
-      /* accumulators [gate][row tile] */
-      f32x4 ia[3][NET], ha[3][NET];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int et = 0; et < NET; ++et) ia[i][et] = ha[i][et] = f32x4{0.f, 0.f, 0.f, 0.f};
-      float4 bi[3], bh[3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        bi[i] = wih[to[i]];
-        bh[i] = whh[to[i]];
-      }
-      for (int g = 0; g < GH; ++g) {
-        const size_t gn = (size_t)(g + 1 < GH ? g + 1 : g) * 64;
-        float4 ni[3], nh[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          ni[i] = wih[to[i] + gn];
-          nh[i] = whh[to[i] + gn];
-        }
-        /* keep the next group's loads here, a whole group (48 MFMAs) ahead of their use */
-        __builtin_amdgcn_sched_barrier(0);
-        const float* xp = xs + (16 * g + k4) * LDA + c16;
-        const float* hp = sh[0] + (16 * g + k4) * LDA + c16;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int et = 0; et < NET; ++et) {
-            const float ax = xp[4 * u * LDA + MT * et], ah = hp[4 * u * LDA + MT * et];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) ia[i][et] = mma(ax, q4(bi[i], u), ia[i][et]);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) ha[i][et] = mma(ah, q4(bh[i], u), ha[i][et]);
-          }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          bi[i] = ni[i];
-          bh[i] = nh[i];
-        }
-      }
-      /* equinox GRUCell: r, z, n gates; h' = n + z (h - n) */
-      const float* bl = a.bias + H + (size_t)l * 4 * H;
-      float* xo = sx[cur ^ 1];
-      {
-        const int unit = 16 * w + c16;
-        const float br = bl[unit], bz = bl[H + unit], bni = bl[2 * H + unit], bnh = bl[3 * H + unit];
-#pragma unroll
-        for (int et = 0; et < NET; ++et)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int e = crow(et, v, lane);
-          const float r = zbf_sigmoid((ia[0][et][v] + br) + ha[0][et][v]);
-          const float z = zbf_sigmoid((ia[1][et][v] + bz) + ha[1][et][v]);
-          const float nn = zbf_tanh((ia[2][et][v] + bni) + r * (ha[2][et][v] + bnh));
-          const float ho = sh[0][unit * LDA + e];
-          const float hv = nn + z * (ho - nn);
-          xo[unit * LDA + e] = hv;
-          if (last && e0 + e < a.n) a.carry[((size_t)(e0 + e) * D + l) * H + unit] = hv;
-          if (TT > 1) {
-#pragma unroll
-            for (int k = 0; k < D; ++k) hreg[k][et][v] = l == k ? hv : hreg[k][et][v];
-          }
-        }
-      }
-      __syncthreads();
-      cur ^= 1;
-    }
-  } else {
-    /* 3. GRU stack (train.py:945-948). Layer l's W_hh h products depend only on its carry, known
-          before the layer starts, so they are taken out of the layer: layer 0's here, layer l + 1's
-          interleaved with layer l's GRU epilogue (one 4-step k group of the next layer's 24 MFMAs
-          beside each of the epilogue's 8 (row tile, env) items), so the matrix cores keep running
-          while the epilogue's transcendental VALU work issues. Every product is the same k-ordered
-          chain from 0 as before, only issued earlier: the same bits. The carries go through two
-          [unit][env] tiles, layer l's in sh[l & 1]. */
-    static_assert(GH == 4 * NET, "one epilogue item (row tile, accumulator register) per k group");
-    const int unit = 16 * w + c16;
-    size_t to[3]; /* gate tiles of this wave's units: r = w, z = 8 + w, n = 16 + w */
-#pragma unroll
-    for (int gt = 0; gt < 3; ++gt) to[gt] = (size_t)(8 * gt + w) * GH * 64;
-    /* carry of layer l (prefetched into registers, zero where the episode restarts) -> sh[l & 1] */
-    auto stage_carry = [&](int l) {
-      float* dst = sh[l & 1];
+  for (int l = 0; l < D; ++l) {
+    if (t == 0) {
+      /* carry of layer l (prefetched during layer l - 1) -> sh */
 #pragma unroll
       for (int j = 0; j < CPT; ++j) {
         const int i = tid + j * NTHR;
         const int e = i / (H / 4), q = i - e * (H / 4);
-        dst[(4 * q) * LDA + e] = cr[j].x;
-        dst[(4 * q + 1) * LDA + e] = cr[j].y;
-        dst[(4 * q + 2) * LDA + e] = cr[j].z;
-        dst[(4 * q + 3) * LDA + e] = cr[j].w;
+        sh[(4 * q) * LDA + e] = cr[j].x;
+        sh[(4 * q + 1) * LDA + e] = cr[j].y;
+        sh[(4 * q + 2) * LDA + e] = cr[j].z;
+        sh[(4 * q + 3) * LDA + e] = cr[j].w;
       }
-    };
-    /* k group g of a [3H][H] product for this wave's three gate tiles and both row tiles: A from the
-       [k][env] tile xs, B the fragments b (the next group's loaded into b, a group ahead) */
-    auto gate_group = [&](const float* xs, const float4* wm, int g, float4 (&b)[3], f32x4 (&acc)[3][NET]) {
-      float4 nb[3];
-      const size_t gn = (size_t)(g + 1 < GH ? g + 1 : g) * 64;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) nb[i] = wm[to[i] + gn];
-      const float* xp = xs + (16 * g + k4) * LDA + c16;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int et = 0; et < NET; ++et) {
-          const float ax = xp[4 * u * LDA + MT * et];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) acc[i][et] = mma(ax, q4(b[i], u), acc[i][et]);
-        }
-#pragma unroll
-      for (int i = 0; i < 3; ++i) b[i] = nb[i];
-    };
-    auto zero_acc = [](f32x4 (&acc)[3][NET]) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int et = 0; et < NET; ++et) acc[i][et] = f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-    auto first_frags = [&](const float4* wm, float4 (&b)[3]) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) b[i] = wm[to[i]];
-    };
-
-    stage_carry(0);
-    if (D > 1) load_carry(1); /* layer 1's carry loads overlap the input projection and layer 0 */
-    __syncthreads(); /* the observation tile and layer 0's carry */
-
-    /* 2. input projection (no activation: train.py:944): the wave's unit tile */
-    {
-      f32x4 acc[NET];
-      tile_gemm(su, wp4 + (size_t)w * GIN * 64 + lane, GIN, lane, acc);
-      const float bu = a.bias[unit];
-#pragma unroll
-      for (int et = 0; et < NET; ++et)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) sx[0][unit * LDA + crow(et, v, lane)] = acc[et][v] + bu;
-    }
-    /* layer 0's W_hh h */
-    f32x4 ha[3][NET];
-    {
-      const float4* whh = wp4 + off_gru + MAT + lane;
-      float4 bh[3];
-      zero_acc(ha);
-      first_frags(whh, bh);
-      for (int g = 0; g < GH; ++g) {
-        __builtin_amdgcn_sched_barrier(0); /* each group's fragment loads stay a group ahead */
-        gate_group(sh[0], whh, g, bh, ha);
-      }
-    }
-
-    for (int l = 0; l < D; ++l) {
-      __syncthreads(); /* layer l's input in sx[cur]; layer l - 1's readers of sh[(l + 1) & 1] are done */
-      if (l + 1 < D) stage_carry(l + 1);
-      if (l + 2 < D) load_carry(l + 2);
-
-      /* W_ih x (the layer's input), k-ordered chains from 0 */
-      const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
-      f32x4 ia[3][NET];
-      {
-        float4 bi[3];
-        zero_acc(ia);
-        first_frags(wih, bi);
-        for (int g = 0; g < GH; ++g) {
-          __builtin_amdgcn_sched_barrier(0);
-          gate_group(sx[cur], wih, g, bi, ia);
-        }
-      }
-      __syncthreads(); /* layer l + 1's carry staged in sh[(l + 1) & 1] */
-
-      /* equinox GRUCell: r, z, n gates; h' = n + z (h - n) */
-      const float* bl = a.bias + H + (size_t)l * 4 * H;
-      const float br = bl[unit], bz = bl[H + unit], bni = bl[2 * H + unit], bnh = bl[3 * H + unit];
-      const float* ho_t = sh[l & 1];
-      float* xo = sx[cur ^ 1];
-      float hvs[NET][4];
-      auto epilogue = [&](int et, int v) {
-        const int e = crow(et, v, lane);
-        const float r = zbf_sigmoid((ia[0][et][v] + br) + ha[0][et][v]);
-        const float z = zbf_sigmoid((ia[1][et][v] + bz) + ha[1][et][v]);
-        const float nn = zbf_tanh((ia[2][et][v] + bni) + r * (ha[2][et][v] + bnh));
-        const float ho = ho_t[unit * LDA + e];
-        const float hv = nn + z * (ho - nn);
-        xo[unit * LDA + e] = hv;
-        hvs[et][v] = hv;
-      };
-      if (l + 1 < D) {
-        /* layer l + 1's W_hh h beside this layer's epilogue */
-        const float4* whh = wp4 + off_gru + (size_t)(l + 1) * 2 * MAT + MAT + lane;
-        f32x4 hn[3][NET];
-        float4 bh[3];
-        zero_acc(hn);
-        first_frags(whh, bh);
-#pragma unroll
-        for (int g = 0; g < GH; ++g) {
-          __builtin_amdgcn_sched_barrier(0);
-          gate_group(sh[(l + 1) & 1], whh, g, bh, hn);
-          epilogue(g / 4, g % 4);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int et = 0; et < NET; ++et) ha[i][et] = hn[i][et];
-      } else {
-#pragma unroll
-        for (int et = 0; et < NET; ++et)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) epilogue(et, v);
-      }
+    } else {
+      /* persistent: the previous step's carry from registers (zero where the episode restarts) */
+      const int unit = 16 * w + c16;
 #pragma unroll
       for (int et = 0; et < NET; ++et)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int e = crow(et, v, lane);
-          if (e0 + e < a.n) a.carry[((size_t)(e0 + e) * D + l) * H + unit] = hvs[et][v];
+          const int e = crow(et, v, lane), ge = e0 + e;
+          float hv = hreg[0][et][v];
+#pragma unroll
+          for (int k = 1; k < D; ++k) hv = l == k ? hreg[k][et][v] : hv;
+          const bool rs = ge >= a.n || (a.reset && a.reset[ge]);
+          sh[unit * LDA + e] = rs ? 0.f : hv;
         }
-      cur ^= 1;
     }
-    __syncthreads(); /* the last layer's output tile */
+    __syncthreads();
+    if (t == 0 && l + 1 < D) load_carry(l + 1);
+
+    const float4* wih = wp4 + off_gru + (size_t)l * 2 * MAT + lane;
+    const float4* whh = wih + MAT;
+    const float* xs = sx[cur];
+    /* gate tiles of this wave's units: r = w, z = 8 + w, n = 16 + w */
+    size_t to[3];
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt) to[gt] = (size_t)(8 * gt + w) * GH * 64;
+    /* accumulators [gate][row tile] */
+    f32x4 ia[3][NET], ha[3][NET];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int et = 0; et < NET; ++et) ia[i][et] = ha[i][et] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 bi[3], bh[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      bi[i] = wih[to[i]];
+      bh[i] = whh[to[i]];
+    }
+    for (int g = 0; g < GH; ++g) {
+      const size_t gn = (size_t)(g + 1 < GH ? g + 1 : g) * 64;
+      float4 ni[3], nh[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        ni[i] = wih[to[i] + gn];
+        nh[i] = whh[to[i] + gn];
+      }
+      /* keep the next group's loads here, a whole group (48 MFMAs) ahead of their use */
+      __builtin_amdgcn_sched_barrier(0);
+      const float* xp = xs + (16 * g + k4) * LDA + c16;
+      const float* hp = sh + (16 * g + k4) * LDA + c16;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int et = 0; et < NET; ++et) {
+          const float ax = xp[4 * u * LDA + MT * et], ah = hp[4 * u * LDA + MT * et];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ia[i][et] = mma(ax, q4(bi[i], u), ia[i][et]);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) ha[i][et] = mma(ah, q4(bh[i], u), ha[i][et]);
+        }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        bi[i] = ni[i];
+        bh[i] = nh[i];
+      }
+    }
+    /* equinox GRUCell: r, z, n gates; h' = n + z (h - n) */
+    const float* bl = a.bias + H + (size_t)l * 4 * H;
+    float* xo = sx[cur ^ 1];
+    {
+      const int unit = 16 * w + c16;
+      const float br = bl[unit], bz = bl[H + unit], bni = bl[2 * H + unit], bnh = bl[3 * H + unit];
+#pragma unroll
+      for (int et = 0; et < NET; ++et)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int e = crow(et, v, lane);
+        const float r = zbf_sigmoid((ia[0][et][v] + br) + ha[0][et][v]);
+        const float z = zbf_sigmoid((ia[1][et][v] + bz) + ha[1][et][v]);
+        const float nn = zbf_tanh((ia[2][et][v] + bni) + r * (ha[2][et][v] + bnh));
+        const float ho = sh[unit * LDA + e];
+        const float hv = nn + z * (ho - nn);
+        xo[unit * LDA + e] = hv;
+        if (last && e0 + e < a.n) a.carry[((size_t)(e0 + e) * D + l) * H + unit] = hv;
+        if (TT > 1) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) hreg[k][et][v] = l == k ? hv : hreg[k][et][v];
+        }
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
   }
 
   /* 4. heads */
