@@ -2002,10 +2002,6 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   EnvL* L = c.L;
   int g, gb;
   const bool gvalid = lane_geom<XG>(c, bank, g, gb);
-  int kd = gvalid ? m->body_lastdof[gb] : 0;
-  if (kd < 0) kd = 0;
-  r.chd = tshi(c.chd, kd);
-  r.kdep = tshi(c.ddep, kd);
   r.ex = false;
   r.act = 0;
   r.f = 0.f;
@@ -2015,11 +2011,18 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   r.aref = 0.f;
   if (XFLOOR<XG> && bank == 1 && __ballot(gvalid) == 0ull) {
     /* no geom of the second bank within reach of the floor in either env of the wave (select_bank2):
-       no row, the same state as the full test finds, without its shuffles and rotations */
+       no row, the same state as the full test finds, without its shuffles and rotations (the row's
+       chain is read only while the bank has a row: r.x.any) */
+    r.chd = -1;
+    r.kdep = 0;
     r.nrow = 0;
     r.exmask = 0u;
     return;
   }
+  int kd = gvalid ? m->body_lastdof[gb] : 0;
+  if (kd < 0) kd = 0;
+  r.chd = tshi(c.chd, kd);
+  r.kdep = tshi(c.ddep, kd);
   float Jc[CAP];
 #pragma unroll
   for (int e = 0; e < CAP; e++) Jc[e] = 0.f;
