@@ -74,8 +74,10 @@ void zb_default_config(ZbEnvConfig* cfg);
  * second bank of 32 contact-row lanes (Jacobian rows in per-env global scratch),
  * which holds, each substep, the first two of the other colliders within reach
  * of the floor; a substep with more than two within reach sets bit 1 of the
- * state's flag word (ZB_S_NAN; bit 0: non-finite). npair = 1 (the two box soles
- * against each other, geom-geom) holds the pair's contacts in that second bank.
+ * state's flag word (ZB_S_NAN; bit 0: non-finite; bit 2: the same, for the
+ * current control step only). npair = 1 (the two box soles against each other,
+ * geom-geom) holds the pair's contacts in that second bank when the soles are the
+ * only colliders, and in a third bank beside the floor colliders' otherwise.
  *
  * Create a handle simulating `n_envs` environments whose global ids are
  * [env_offset, env_offset + n_envs) — RNG streams are keyed by global id, so

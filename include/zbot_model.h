@@ -18,8 +18,8 @@
  *     capsules, cylinders, spheres, ellipsoids or convex meshes (<= ZB_MAX_MESHV hull
  *     vertices each; the two foot soles first by
  *     convention); of the robot's own pairs only the two box soles against each
- *     other (npair <= 1, box-box, with no other floor collider); any other
- *     self pair is counted in nskip_pair and refused;
+ *     other (npair <= 1, box-box, alone or beside other floor colliders); any
+ *     other self pair is counted in nskip_pair and refused;
  *   - actuators = motors on hinge joints (joint transmission, gear).
  * All floats are fp32; all vectors are padded to 4 so rows are 16-B aligned.
  */
