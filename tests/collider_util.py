@@ -444,6 +444,14 @@ def limbs_pair_desc() -> dict:
     return d
 
 
+def many_pair_desc() -> dict:
+    """The nine-collider model (many_desc) whose two soles also collide with each other (round 6: the
+    XG 4 kernels with the second bank picked per substep)."""
+    d = many_desc()
+    d["self_pairs"] = [["left_foot_sole", "right_foot_sole"]]
+    return d
+
+
 def crossing_touching_states(cm, n: int, seed: int, depth=0.003) -> np.ndarray:
     """qpos [n, 27] with the legs crossed as in crossing_states (the soles interpenetrate) and the
     robot on the floor: even envs standing at the reset height, odd envs lying (a random heading,

@@ -25,8 +25,9 @@ def torch_gpu():
 
 # "pair": the soles alone (the XG 3 kernels); "limbs_pair" (round 6): the pair beside
 # the limbs model's shin box and hand capsule (the XG 4 kernels: the floor colliders in the second bank,
-# the pair in a third)
-PAIR_MODELS = {"pair": U.sole_pair_desc, "limbs_pair": U.limbs_pair_desc}
+# the pair in a third); "many_pair": beside the nine-collider model's seven others (XG 4 with the second
+# bank picked per substep, a mesh among them)
+PAIR_MODELS = {"pair": U.sole_pair_desc, "limbs_pair": U.limbs_pair_desc, "many_pair": U.many_pair_desc}
 
 
 @pytest.fixture(scope="module", params=list(PAIR_MODELS))
@@ -205,6 +206,10 @@ def test_rollout_from_reset_matches_oracle(torch_gpu, pair_model, oracle_mod, so
     from zbot_amd.engine import HipEngine
 
     cm = pair_model
+    if cm.variant == "many_pair":
+        pytest.skip("robots that fall from crossed legs can put more than two of the nine colliders within "
+                    "reach of the floor (the second bank's cap, DESIGN.md §4j): the rollout is compared on "
+                    "the limbs + pair model")
     cfg = default_config(solver=solver)
     n, steps, seed = 64, 48, 13
     acts = crossing_actions(oracle_mod, cm, seed, n, steps)
