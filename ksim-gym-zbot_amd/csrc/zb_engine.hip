@@ -2995,12 +2995,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
       eval(alpha, d1, d2);
       if (fabsf(d1) <= gtol) break;
       if (d1 < 0.f) lo = alpha; else hi = alpha;
-      const float an = alpha - d1 / d2;
-      /* the bracket safeguard as selects: the two teams of a wave take it independently, and a
-         branch around it costs the wave an exec-mask split every evaluation */
-      const bool out = !(an > lo) || (hi >= 0.f && !(an < hi));
-      const float bisect = 0.5f * (lo + (hi >= 0.f ? hi : 2.f * alpha));
-      alpha = out ? bisect : an;
+      float an = alpha - d1 / d2;
+      if (!(an > lo) || (hi >= 0.f && !(an < hi))) an = 0.5f * (lo + (hi >= 0.f ? hi : 2.f * alpha));
+      alpha = an;
     }
     return alpha;
   };
