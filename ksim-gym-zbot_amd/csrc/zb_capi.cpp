@@ -139,7 +139,7 @@ int zb_create(const ZbModel* model, const ZbEnvConfig* cfg, int n_envs, int env_
   if (e == hipSuccess) e = hipMemset(h->itpart, 0, n * sizeof(int32_t));
   h->xg = zb::needs_xg(model);
   /* XG 4: two banks in global scratch per env (the floor selection, the sole pair) */
-  if (e == hipSuccess && h->xg) e = hipMalloc(&h->xj, (n + 1) * ZB_XJ_STRIDE * (h->xg == 4 ? 2 : 1) * sizeof(float));
+  if (e == hipSuccess && h->xg) e = hipMalloc(&h->xj, (n + 1) * ZB_XJ_STRIDE * (h->xg == 4 || h->xg == 5 ? 2 : 1) * sizeof(float));
   h->nchunk = choose_chunks(n_envs, cfg->n_substeps, zb::step_resident_blocks(device, h->xg, cfg->solver, (cfg->flags & ZB_F_EULERDAMP) ? 1 : 0));
 #if defined(ZB_STAMPS) || defined(ZB_WAVETIME)
   {

@@ -77,6 +77,8 @@ struct EnvS {
   /* XG 1 / 2: the geoms in the second contact-row bank this substep (half 0, half 1; -1: none):
      the first two of geoms 2.. within reach of the floor (select_bank2) */
   int32_t xsel[2];
+  /* XG 5: the third bank's geoms (the third and fourth within reach) */
+  int32_t ysel[2];
 };
 struct Sensors {
   float fq[4], gyro[3], acc[3], touch[2], force[6];
@@ -519,11 +521,11 @@ typedef __attribute__((address_space(1))) xv4f gfloat4_t;
 __device__ __forceinline__ gfloat_t* xrows(const EnvL* L) {
   return (gfloat_t*)(((uint64_t)L->s.xj_hi << 32) | (uint64_t)L->s.xj_lo);
 }
-/* XG 4: the third bank's rows follow the second bank's in the env's block */
+/* XG 4 / 5: the third bank's rows follow the second bank's in the env's block */
 __device__ __forceinline__ gfloat_t* yrows(const EnvL* L) { return xrows(L) + 32 * CAP; }
 /* floats of StepArgs::xj per env: one [32][CAP] block per extra bank */
 template <int XG>
-constexpr int XJ_STRIDE = ZB_XJ_STRIDE * (XG == 4 ? 2 : 1);
+constexpr int XJ_STRIDE = ZB_XJ_STRIDE * (XG == 4 || XG == 5 ? 2 : 1);
 __device__ __forceinline__ void set_xrows(EnvL* L, float* base) {
   L->s.xj_lo = (uint32_t)(uint64_t)base;
   L->s.xj_hi = (uint32_t)((uint64_t)base >> 32);
@@ -1704,15 +1706,21 @@ __device__ __forceinline__ void row_params(PR solref, PS solimp, float pos, floa
    (Rows::x) holds the general floor colliders (the first two beyond the soles within reach, select_bank2;
    XG 2 compiles cylinders, ellipsoids and meshes), XG 3 the sole pair (the two box soles against each
    other, pair_rows), XG 4 both: the floor colliders in the second bank and the sole pair in a third
-   (Rows::y, round 6). XG 0: the two soles alone. */
+   (Rows::y, round 6), XG 5 (models with more than two colliders beyond the soles) floor colliders in
+   the second and third banks: the first four within reach of the floor each substep. XG 0: the two
+   soles alone. */
 template <int XG>
-constexpr bool XFLOOR = XG == 1 || XG == 2 || XG == 4;
+constexpr bool XFLOOR = XG == 1 || XG == 2 || XG == 4 || XG == 5;
 template <int XG>
 constexpr bool XPAIR = XG == 3; /* the pair in the second bank */
 template <int XG>
 constexpr bool YPAIR = XG == 4; /* the pair in the third bank */
 template <int XG>
-constexpr bool XRICH = XG == 2 || XG == 4; /* cylinder / ellipsoid / mesh rules compiled */
+constexpr bool YFLOOR = XG == 5; /* floor colliders in the third bank too */
+template <int XG>
+constexpr bool YBANK = YPAIR<XG> || YFLOOR<XG>; /* the third bank exists */
+template <int XG>
+constexpr bool XRICH = XG == 2 || XG == 4 || XG == 5; /* cylinder / ellipsoid / mesh rules compiled */
 template <int XG>
 constexpr bool ANYPAIR = XPAIR<XG> || YPAIR<XG>;
 
@@ -1722,9 +1730,9 @@ template <int XG>
 __device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& gb) {
   MP m = c.m;
   const int gl = c.l >> 4;
-  if (XFLOOR<XG> && bank == 1) {
-    /* the second bank's geoms of this substep (select_bank2) */
-    const int sg = c.L->s.xsel[gl];
+  if (XFLOOR<XG> && bank >= 1) {
+    /* the second (third: XG 5) bank's geoms of this substep (select_bank2) */
+    const int sg = bank == 1 ? c.L->s.xsel[gl] : c.L->s.ysel[gl];
     const bool sv = sg >= 0;
     g = sv ? sg : 0;
     gb = sv ? m->geom_body[g] : 0;
@@ -2009,7 +2017,7 @@ __device__ __forceinline__ void contact_rows(const Ctx& c, const EnvS& s, const 
   r.Jv = 0.f;
   r.D = 0.f;
   r.aref = 0.f;
-  if (XFLOOR<XG> && bank == 1 && __ballot(gvalid) == 0ull) {
+  if (XFLOOR<XG> && bank >= 1 && __ballot(gvalid) == 0ull) {
     /* no geom of the second bank within reach of the floor in either env of the wave (select_bank2):
        no row, the same state as the full test finds, without its shuffles and rotations (the row's
        chain is read only while the bank has a row: r.x.any) */
@@ -2441,6 +2449,15 @@ __device__ __forceinline__ void select_bank2(const Ctx& c, const BodyK& B) {
     sel1 = mk ? 1 + __ffs(mk) : -1;
     mk &= mk - 1u;
   }
+  if constexpr (YFLOOR<XG>) {
+    /* XG 5: the third and fourth geoms within reach take the third bank's halves */
+    const int sel2 = mk ? 1 + __ffs(mk) : -1;
+    mk &= mk - 1u;
+    const int sel3 = mk ? 1 + __ffs(mk) : -1;
+    mk &= mk - 1u;
+    c.L->s.ysel[0] = sel2;
+    c.L->s.ysel[1] = sel3;
+  }
   /* team-uniform values, written by every lane of the team */
   c.L->s.xsel[0] = sel0;
   c.L->s.xsel[1] = sel1;
@@ -2484,6 +2501,22 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
     bool yany = false;
     if constexpr (YPAIR<XG>) {
       pair_rows(c, s, B, cm, r.y, yrows(c.L) + l * CAP);
+      r.y.any = yany = __ballot(r.y.ex) != 0ull;
+    }
+    if constexpr (YFLOOR<XG>) {
+      /* XG 5: the third and fourth geoms within reach in the third bank, row masks as the second's */
+      contact_rows<XG>(c, s, B, cm, 2, r.y, yrows(c.L) + l * CAP);
+      uint32_t rm = 0u;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int sg = c.L->s.ysel[h];
+        const int kd = sg >= 0 ? m->body_lastdof[m->geom_body[sg]] : -1;
+        const int kdc = kd >= 0 ? kd : 0;
+        const int hkd = tshi(c.chd, kdc);
+        const bool on = l < NV && kd >= 0 && l <= kd && (l < NROOT || c.chd == hkd);
+        rm |= on ? (0xFFFFu << (16 * h)) : 0u;
+      }
+      r.y.rowmask = rm;
       r.y.any = yany = __ballot(r.y.ex) != 0ull;
     }
     if (r.x.any || yany) {
@@ -2589,9 +2622,9 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const Rows& r, float jc
     /* the sole pair's row is held by two lanes (its halves): counted once */
     cost += (r.x.ex && (!XPAIR<XG> || c.l < 16)) ? k3 : 0.f;
   }
-  if constexpr (YPAIR<XG> && XA) {
+  if constexpr (YBANK<XG> && XA) {
     const float k4 = eval_one(jy, r.y.D, f, a);
-    cost += (r.y.ex && c.l < 16) ? k4 : 0.f; /* the pair's halves: once */
+    cost += (r.y.ex && (YFLOOR<XG> || c.l < 16)) ? k4 : 0.f; /* the pair's halves: once */
   }
   return cost;
 }
@@ -2682,12 +2715,12 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
     sx1 = tsh(cx, 16 + ddep);
   }
   float sy0 = 0.f, sy1 = 0.f;
-  if constexpr (YPAIR<XG> && XA) {
+  if constexpr (YBANK<XG> && XA) {
     if (r.y.any) {
       float f4;
       int a4;
       const float k4 = eval_one(r.y.jar, r.y.D, f4, a4);
-      cost += (r.y.ex && c.l < 16) ? k4 : 0.f; /* the pair's halves: once */
+      cost += (r.y.ex && (YFLOOR<XG> || c.l < 16)) ? k4 : 0.f; /* the pair's halves: once */
       r.y.f = r.y.ex ? f4 : r.y.f;
       r.y.act = r.y.ex ? a4 : r.y.act;
       const float cy = colsum16((const gfloat_t*)yrows(c.L) + c.l * CAP, r.y.ex ? r.y.f : 0.f);
@@ -2708,8 +2741,10 @@ __device__ __forceinline__ float update_constraint_lane(const Ctx& c, Rows& r, c
       const bool f2 = (rm2 & 0xFFFFu) != 0u, f3 = (rm2 >> 16) != 0u;
       qc += (f2 ? sx0 : 0.f) + (f3 ? sx1 : 0.f);
     }
-    if constexpr (YPAIR<XG> && XA) {
-      const bool f4 = (c.rmb & 16u) != 0u, f5 = (c.rmb & 32u) != 0u; /* the pair's static row masks */
+    if constexpr (YBANK<XG> && XA) {
+      /* the pair's static row masks (XG 4), the third floor bank's of this substep (XG 5) */
+      const bool f4 = YFLOOR<XG> ? (r.y.rowmask & 0xFFFFu) != 0u : (c.rmb & 16u) != 0u;
+      const bool f5 = YFLOOR<XG> ? (r.y.rowmask >> 16) != 0u : (c.rmb & 32u) != 0u;
       qc += (f4 ? sy0 : 0.f) + (f5 ? sy1 : 0.f);
     }
     if (r.hf) qc += r.ff;
@@ -2730,9 +2765,9 @@ __device__ __forceinline__ float update_constraint(const Ctx& c, Rows& r, const 
  * lane l supplies row 4*chunk + l/16, entry l%16). Staged in the env's L[][]
  * as [foot][12][12]; L[][] is free until factor_ldl writes it. D is rowDA
  * (0 for absent / inactive rows). Wave-uniform: call with every lane active.
- * BANK2: the same for the second bank's geoms (xrows J, rowDA holding that bank's D), staged in
- * the Hessian rows Hs[][], free until hessian_factor stores the assembled rows. */
-template <bool BANK2>
+ * BANK 1 / 2: the same for the second / third bank's geoms (xrows / yrows J, rowDA holding that bank's
+ * D), staged in the Hessian rows Hs[][], free until hessian_factor stores the assembled rows. */
+template <int BANK>
 __device__ __forceinline__ void jdj_mfma() {
   const int l = threadIdx.x & 63;
   const int e = l & 15, k = l >> 4;
@@ -2751,8 +2786,10 @@ __device__ __forceinline__ void jdj_mfma() {
         const int r = 16 * f + 4 * ch + k;
         /* no masks: rowDA is zero for absent / inactive rows, and output rows or
            columns e >= CAP (lanes reading entry CAP-1) are never stored */
-        const float jv = BANK2 ? xrows(&g_lds[t])[r * CAP + ec] : g_lds[t].u.J[r][ec];
-        const float dv = g_lds[t].rowDA[r]; /* BANK2: the second bank's, written by hessian_factor */
+        const float jv = BANK == 2   ? yrows(&g_lds[t])[r * CAP + ec]
+                         : BANK == 1 ? xrows(&g_lds[t])[r * CAP + ec]
+                                     : g_lds[t].u.J[r][ec];
+        const float dv = g_lds[t].rowDA[r]; /* BANK >= 1: that bank's, written by hessian_factor */
         acc[t][f] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv * jv, jv, acc[t][f], 0, 0, 0);
       }
   /* lane l holds G[4*(l/16) + v][l%16], v = 0..3: G is symmetric (to rounding), so the
@@ -2763,7 +2800,7 @@ __device__ __forceinline__ void jdj_mfma() {
     for (int t = 0; t < NTEAM; t++)
 #pragma unroll
       for (int f = 0; f < NGEOM; f++)
-        *reinterpret_cast<v4f*>((BANK2 ? &g_lds[t].Hs[0][0] : &g_lds[t].L[0][0]) + f * CAP * CAP + e * CAP + 4 * k) =
+        *reinterpret_cast<v4f*>((BANK ? &g_lds[t].Hs[0][0] : &g_lds[t].L[0][0]) + f * CAP * CAP + e * CAP + 4 * k) =
             acc[t][f];
 }
 
@@ -2799,22 +2836,22 @@ __device__ __forceinline__ void add_rows(uint32_t tb, JP J, const float* da, int
  * the active set, and the change is usually a handful of rows. XG: both banks. */
 template <int XG, bool XA = true>
 __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, bool full, int pa, int pf, int plo,
-                                                int pa2) {
+                                                int pa2, int pa3) {
   const int ddep = vopq(c.ddep);
   EnvL* L = c.L;
   float H[CAP], Hd;
-  uint32_t tb, tb2 = 0u, ch2 = 0u;
-  float dl2 = 0.f;
+  uint32_t tb, tb2 = 0u, ch2 = 0u, tb3 = 0u, ch3 = 0u;
+  float dl2 = 0.f, dl3 = 0.f;
   if (full) {
     Hd = load_mrow(c, H);
     tb = 0u;
-    jdj_mfma<false>();
+    jdj_mfma<0>();
     if (XFLOOR<XG> && XA && r.x.any) {
       /* the second bank's D (rowDA is free once the first bank's J'DJ has read it) */
       tsync();
       L->rowDA[c.l] = (r.x.ex && r.x.act) ? r.x.D : 0.f;
       tsync();
-      jdj_mfma<true>();
+      jdj_mfma<1>();
     }
     tsync();
     if (c.l < NV) {
@@ -2847,6 +2884,27 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
         Hd += d2 + d3;
       }
     }
+    if (YFLOOR<XG> && XA && r.y.any) {
+      /* XG 5: the third bank's J'DJ through the same staging rows, once the second's are read */
+      tsync();
+      L->rowDA[c.l] = (r.y.ex && r.y.act) ? r.y.D : 0.f;
+      tsync();
+      jdj_mfma<2>();
+      tsync();
+      if (c.l < NV) {
+        const float* GY = &L->Hs[0][0] + ddep * CAP;
+        const bool f4 = (r.y.rowmask & 0xFFFFu) != 0u, f5 = (r.y.rowmask >> 16) != 0u;
+        const float* G4 = f4 ? GY : &L->L[31][0];
+        const float* G5 = f5 ? GY + CAP * CAP : &L->L[31][0];
+        float g4[CAP], g5[CAP];
+        ld_row(G4, g4);
+        ld_row(G5, g5);
+        const float d4 = G4[f4 ? ddep : 0], d5 = G5[f5 ? ddep : 0];
+#pragma unroll
+        for (int e = 0; e < CAP; e++) H[e] += g4[e] + g5[e];
+        Hd += d4 + d5;
+      }
+    }
   } else {
     ld_row(&L->Hs[c.l][0], H);
     Hd = L->Hsd[c.l];
@@ -2857,6 +2915,11 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
       dl2 = r.x.ex ? ((r.x.act ? r.x.D : 0.f) - (pa2 ? r.x.D : 0.f)) : 0.f;
       ch2 = team_ballot(dl2 != 0.f); /* team-uniform: some row of the bank changed */
       tb2 = ch2 & r.x.rowmask;       /* per dof lane: the changed rows on its chain */
+    }
+    if (YFLOOR<XG> && XA && r.y.any) {
+      dl3 = r.y.ex ? ((r.y.act ? r.y.D : 0.f) - (pa3 ? r.y.D : 0.f)) : 0.f;
+      ch3 = team_ballot(dl3 != 0.f);
+      tb3 = ch3 & r.y.rowmask;
     }
     tsync();
   }
@@ -2880,7 +2943,15 @@ __device__ __forceinline__ float hessian_factor(const Ctx& c, const Rows& r, boo
     tsync();
     if (c.l < NV) add_rows(tb2, (const gfloat_t*)xrows(L), L->rowF, ddep, H, Hd);
   }
-  if (XFLOOR<XG> && XA && full && r.x.any) tsync(); /* the second bank's G rows in Hs[] are read before H is stored there */
+  if (YFLOOR<XG> && ch3 != 0u) {
+    /* XG 5: the third bank's changed rows, the same way after the second's */
+    tsync();
+    L->rowF[c.l] = dl3;
+    tsync();
+    if (c.l < NV) add_rows(tb3, (const gfloat_t*)yrows(L), L->rowF, ddep, H, Hd);
+  }
+  /* the second / third bank's G rows in Hs[] are read before H is stored there */
+  if (XA && full && ((XFLOOR<XG> && r.x.any) || (YFLOOR<XG> && r.y.any))) tsync();
   st_row(&L->Hs[c.l][0], H);
   L->Hsd[c.l] = Hd;
   tsync();
@@ -2903,9 +2974,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
     if constexpr (XPAIR<XG>) jx += xor16f(jx); /* the pair's row: both halves */
     r.x.Jv = jx;
   }
-  if constexpr (YPAIR<XG> && XA) {
+  if constexpr (YBANK<XG> && XA) {
     float jy = r.y.any ? row_dot_y(c, r, V_TMP) : 0.f;
-    jy += xor16f(jy);
+    if constexpr (YPAIR<XG>) jy += xor16f(jy); /* the pair's row: both halves */
     r.y.Jv = jy;
   }
   tsync();
@@ -2921,7 +2992,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
   /* XA: the second bank has rows in the wave; without, its terms are exact zeros and its row state is
      not carried through the loop (fewer live registers in the common copy) */
   if constexpr (XG && XA) g20 += (r.x.ex && r.x.act && xprim) ? r.x.D * r.x.Jv * r.x.Jv : 0.f;
-  if constexpr (YPAIR<XG> && XA) g20 += (r.y.ex && r.y.act && c.l < 16) ? r.y.D * r.y.Jv * r.y.Jv : 0.f;
+  if constexpr (YBANK<XG> && XA)
+    g20 += (r.y.ex && r.y.act && (YFLOOR<XG> || c.l < 16)) ? r.y.D * r.y.Jv * r.y.Jv : 0.f;
   float cc[4] = {isd ? search * (Ma - fs) : 0.f, isd ? search * Mv : 0.f, isd ? search * grad : 0.f, g20};
   tsum_n<4>(cc);
   const float c1 = cc[0], c2 = cc[1];
@@ -2938,8 +3010,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
     DlJ2 = DlJ * sv;
   }
   const float DXJ = (XG && XA && r.x.ex && xprim) ? r.x.D * r.x.Jv : 0.f, DXJ2 = (XG && XA) ? DXJ * r.x.Jv : 0.f;
-  const float DYJ = (YPAIR<XG> && XA && r.y.ex && c.l < 16) ? r.y.D * r.y.Jv : 0.f,
-              DYJ2 = (YPAIR<XG> && XA) ? DYJ * r.y.Jv : 0.f;
+  const float DYJ = (YBANK<XG> && XA && r.y.ex && (YFLOOR<XG> || c.l < 16)) ? r.y.D * r.y.Jv : 0.f,
+              DYJ2 = (YBANK<XG> && XA) ? DYJ * r.y.Jv : 0.f;
   float d1 = cc[2], d2 = c2 + cc[3];
   if (!(d1 < 0.f) || !(d2 > 0.f)) return 0.f;
   const float gtol = cfg->ls_tolerance * (-d1);
@@ -2978,7 +3050,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, Rows& r, const float 
         const float x = r.x.jar + alpha * r.x.Jv;
         g1 += DXJ * fminf(x, 0.f);
         g2 += x < 0.f ? DXJ2 : 0.f;
-        if constexpr (YPAIR<XG>) {
+        if constexpr (YBANK<XG>) {
           const float xy = r.y.jar + alpha * r.y.Jv;
           g1 += DYJ * fminf(xy, 0.f);
           g2 += xy < 0.f ? DYJ2 : 0.f;
@@ -3118,12 +3190,14 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     jsx -= r.x.aref;
   }
   float jwy = 0.f, jsy = 0.f;
-  if constexpr (YPAIR<XG> && XA) {
+  if constexpr (YBANK<XG> && XA) {
     if (r.y.any) {
       jwy = row_dot_y(c, r, V_TMP);
       jsy = row_dot_y(c, r, V_TMP2);
-      jwy += xor16f(jwy);
-      jsy += xor16f(jsy);
+      if constexpr (YPAIR<XG>) {
+        jwy += xor16f(jwy);
+        jsy += xor16f(jsy);
+      }
       jwy -= r.y.aref;
       jsy -= r.y.aref;
     }
@@ -3151,7 +3225,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
   float grad;
   float cost = update_constraint<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
   STAMP(S_UPD0);
-  float Dinv = hessian_factor<XG, XA>(c, r, true, 0, 0, 0, 0);
+  float Dinv = hessian_factor<XG, XA>(c, r, true, 0, 0, 0, 0, 0);
   STAMP(S_HESS0);
   float search;
   if constexpr (ANYPAIR<XG> && XA) search = -hsolve_pair<XG>(c, r, jr, grad, Dinv);
@@ -3168,17 +3242,19 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
     if constexpr (XG && XA) r.x.jar += alpha * r.x.Jv;
-    if constexpr (YPAIR<XG> && XA) r.y.jar += alpha * r.y.Jv;
+    if constexpr (YBANK<XG> && XA) r.y.jar += alpha * r.y.Jv;
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     float oldcost = cost;
-    const int pa = r.act, pf = r.actf, plo = r.actl, pa2 = (XG && XA) ? r.x.act : 0;
+    const int pa = r.act, pf = r.actf, plo = r.actl, pa2 = (XG && XA) ? r.x.act : 0,
+              pa3 = (YFLOOR<XG> && XA) ? r.y.act : 0;
     /* the iteration's three team sums in one interleaved reduction (the same DPP sequence per
        value, so the bits of separate tsum calls): cost, |grad|^2 and the active-set change */
     float red[3];
     red[0] = update_constraint_lane<XG, XA>(c, r, jr, x, qs, fs, Ma, grad);
     red[1] = c.l < NV ? grad * grad : 0.f;
-    red[2] = (r.act != pa || r.actf != pf || (XFLOOR<XG> && XA && r.x.act != pa2)) ? 1.f : 0.f;
+    red[2] = (r.act != pa || r.actf != pf || (XFLOOR<XG> && XA && r.x.act != pa2) ||
+              (YFLOOR<XG> && XA && r.y.act != pa3)) ? 1.f : 0.f;
     if (r.anyl && r.actl != plo) red[2] = 1.f;
     tsum_n<3>(red);
     cost = red[0];
@@ -3193,7 +3269,7 @@ __device__ __forceinline__ float solve_newton(const Ctx& c, Rows& r, float qs, f
     /* H depends only on the active set (M, D fixed within a substep):
        refactor only when it changed (MuJoCo's Newton does the same) */
     const bool changed = red[2] > 0.f;
-    if (changed) Dinv = hessian_factor<XG, XA>(c, r, false, pa, pf, plo, pa2);
+    if (changed) Dinv = hessian_factor<XG, XA>(c, r, false, pa, pf, plo, pa2, pa3);
     STAMP(S_HESS);
     float mg;
     if constexpr (ANYPAIR<XG> && XA) mg = hsolve_pair<XG>(c, r, jr, grad, Dinv);
@@ -3243,12 +3319,14 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     jsx -= r.x.aref;
   }
   float jwy = 0.f, jsy = 0.f;
-  if constexpr (YPAIR<XG> && XA) {
+  if constexpr (YBANK<XG> && XA) {
     if (r.y.any) {
       jwy = row_dot_y(c, r, V_TMP);
       jsy = row_dot_y(c, r, V_TMP2);
-      jwy += xor16f(jwy);
-      jsy += xor16f(jsy);
+      if constexpr (YPAIR<XG>) {
+        jwy += xor16f(jwy);
+        jsy += xor16f(jsy);
+      }
       jwy -= r.y.aref;
       jsy -= r.y.aref;
     }
@@ -3290,7 +3368,7 @@ __device__ __forceinline__ float solve_cg(const Ctx& c, Rows& r, float qs, float
     Ma += alpha * Mv;
     r.jar += alpha * r.Jv;
     if constexpr (XG && XA) r.x.jar += alpha * r.x.Jv;
-    if constexpr (YPAIR<XG> && XA) r.y.jar += alpha * r.y.Jv;
+    if constexpr (YBANK<XG> && XA) r.y.jar += alpha * r.y.Jv;
     r.jf += alpha * search;
     if (r.anyl) r.jl += alpha * (r.sl * search);
     const float oldcost = cost, gold = grad, mgold = mg;
@@ -3408,7 +3486,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   /* constraints */
   make_constraints<XG>(c, s, ls, B, cm, r);
   STAMP(S_CON);
-  int nrows = tmaxi(r.nrow + (XG ? r.x.nrow : 0) + (YPAIR<XG> ? r.y.nrow : 0) + (r.hf || r.hl ? 1 : 0));
+  int nrows = tmaxi(r.nrow + (XG ? r.x.nrow : 0) + (YBANK<XG> ? r.y.nrow : 0) + (r.hf || r.hl ? 1 : 0));
   float qacc;
   /* entered by the whole wave when either env has rows (the full Hessian
      build runs on the matrix cores and needs every lane); an env without
@@ -3425,7 +3503,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
       return SOLVER == ZB_SOLVER_CG ? solve_cg<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, DinvM, ft)
                                     : solve_newton<XG, XA>(c, r, qs, fs, ls.w, it2, nrows > 0, ft);
     };
-    const bool xa = XG != 0 && (r.x.any || (YPAIR<XG> && r.y.any)); /* wave-uniform */
+    const bool xa = XG != 0 && (r.x.any || (YBANK<XG> && r.y.any)); /* wave-uniform */
     const float qn = xa ? solve(BoolC<true>{}) : solve(BoolC<false>{});
     if (nrows > 0) {
       qacc = qn;
@@ -3461,12 +3539,14 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
   }
   if constexpr (YPAIR<XG>) {
     if (r.y.any) pair_dir(ypos, ydir);
+  } else if (YFLOOR<XG> && r.y.any) {
+    (void)contact_point<XG>(c, s, B, 2, ypos, ydir, cmu);
   }
   const int rgeom = c.l >> 4;
   float tch0 = 0.f, tch1 = 0.f;
-  for (int g = 0; g < (YPAIR<XG> ? 3 * NGEOM : XG ? 2 * NGEOM : NGEOM); g++) {
+  for (int g = 0; g < (YBANK<XG> ? 3 * NGEOM : XG ? 2 * NGEOM : NGEOM); g++) {
     /* geom g: bank g / 2, lanes 16 (g % 2) .. + 15 (XG 4: bank 2 = the pair's halves) */
-    const bool b1 = XG && g >= NGEOM && g < 2 * NGEOM, b2 = YPAIR<XG> && g >= 2 * NGEOM;
+    const bool b1 = XG && g >= NGEOM && g < 2 * NGEOM, b2 = YBANK<XG> && g >= 2 * NGEOM;
     if (b1 && !r.x.any) continue; /* wave-uniform */
     if (b2 && !r.y.any) continue;
     const bool mine = (b2 ? r.y.ex : b1 ? r.x.ex : r.ex) && rgeom == (g & 1);
@@ -3487,7 +3567,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     float fnt = ex7[6];
     /* the pair's halves: g = 2 geom2's body (+F), g = 3 geom1's (-F, in xdir); each foot's touch
        sensor takes the pair's normal force (its geom is in the contact) */
-    const int gg = b2 ? m->pair_geom[g == 2 * NGEOM ? 1 : 0]
+    const int gg = (YFLOOR<XG> && b2) ? c.L->s.ysel[g - 2 * NGEOM]
+                   : b2 ? m->pair_geom[g == 2 * NGEOM ? 1 : 0]
                    : (XPAIR<XG> && b1) ? m->pair_geom[g == NGEOM ? 1 : 0]
                    : (XFLOOR<XG> && b1) ? c.L->s.xsel[g - NGEOM] : g;
     if (gg >= 0 && gg < m->ngeom && c.l == m->geom_body[gg]) {
@@ -4385,10 +4466,11 @@ __global__ __launch_bounds__(64) void debug_forward_kernel(StepArgs a) {
     for (int k = 0; k < 6; k++) d[ZB_DBG_CVEL + 6 * l + k] = B.cv[k];
   }
   int nefc = (int)tsum((float)((r.ex ? 1 : 0) + (XG && r.x.ex && (!XPAIR<XG> || l < 16) ? 1 : 0) +
-                               (YPAIR<XG> && r.y.ex && l < 16 ? 1 : 0) + (r.hf ? 1 : 0) + (r.hl ? 1 : 0)));
+                               (YBANK<XG> && r.y.ex && (YFLOOR<XG> || l < 16) ? 1 : 0) + (r.hf ? 1 : 0) +
+                               (r.hl ? 1 : 0)));
   if (l == 0) {
     d[ZB_DBG_MISC + 0] = (float)nefc;
-    d[ZB_DBG_MISC + 1] = (float)((r.nrow + (XG ? r.x.nrow / (XPAIR<XG> ? 2 : 1) : 0) + (YPAIR<XG> ? r.y.nrow / 2 : 0)) / 4);
+    d[ZB_DBG_MISC + 1] = (float)((r.nrow + (XG ? r.x.nrow / (XPAIR<XG> ? 2 : 1) : 0) + (YBANK<XG> ? r.y.nrow / (YPAIR<XG> ? 2 : 1) : 0)) / 4);
     d[ZB_DBG_MISC + 2] = sen.touch[0];
     d[ZB_DBG_MISC + 3] = sen.touch[1];
     for (int k = 0; k < 4; k++) d[ZB_DBG_MISC + 4 + k] = sen.fq[k];
@@ -4426,6 +4508,7 @@ __host__ void with_variant(int solver, int xg, int ed, F&& f) {
   using std::integral_constant;
   auto by_xg = [&](auto S, auto D) {
     switch (xg) {
+      case 5: f(S, integral_constant<int, 5>{}, D); break;
       case 4: f(S, integral_constant<int, 4>{}, D); break;
       case 3: f(S, integral_constant<int, 3>{}, D); break;
       case 2: f(S, integral_constant<int, 2>{}, D); break;

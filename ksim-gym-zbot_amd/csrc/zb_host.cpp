@@ -203,6 +203,9 @@ int needs_xg(const ZbModel* m) {
   const char* fx = getenv("ZB_FORCE_XG");
   if (m->ngeom == 2 && m->geom_type[0] == ZB_GEOM_BOX && m->geom_type[1] == ZB_GEOM_BOX)
     return (fx && fx[0] == '1') ? 1 : 0;
+  /* more than two colliders beyond the soles: the second and third banks both hold floor colliders,
+     the first four within reach of the floor each substep (XG 5, every collider type compiled) */
+  if (m->ngeom > 4) return 5;
   for (int g = 0; g < m->ngeom; g++)
     if (m->geom_type[g] == ZB_GEOM_CYLINDER || m->geom_type[g] == ZB_GEOM_ELLIPSOID || m->geom_type[g] == ZB_GEOM_MESH)
       return 2;

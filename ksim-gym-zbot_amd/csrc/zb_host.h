@@ -31,7 +31,7 @@ int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int check_model(const ZbModel* m);
 int check_cfg(const ZbEnvConfig* c);
 /* the model needs the general-collider kernels (anything but exactly two box soles) */
-int needs_xg(const ZbModel* m); /* 0 two-sole, 1 general colliders, 2 with cylinders / ellipsoids / meshes, 3 the sole pair alone, 4 the sole pair beside other colliders */
+int needs_xg(const ZbModel* m); /* 0 two-sole, 1 general colliders, 2 with cylinders / ellipsoids / meshes, 3 the sole pair alone, 4 the sole pair beside other colliders, 5 more than two colliders beyond the soles (two floor banks) */
 /* requires check_model(m) == ZB_OK */
 void build_topology(const ZbModel* m, int32_t t[TP_NF][TOPO_LANES]);
 

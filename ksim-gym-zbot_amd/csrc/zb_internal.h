@@ -58,7 +58,7 @@ struct StepArgs {
   int32_t* itpart;          /* [n] Newton iterations of the chunks so far */
   int air_mark;             /* first step of a rollout: save its contacts + causal airtime term */
   int solver;               /* ZB_SOLVER_NEWTON / ZB_SOLVER_CG: which kernel instantiation runs */
-  int xg;                   /* general colliders (zb_host.h needs_xg): 0 two-sole, 1 two banks, 2 two banks + cylinders / ellipsoids */
+  int xg;                   /* general colliders (zb_host.h needs_xg): 0 two-sole, 1 two banks, 2 two banks + cylinders / ellipsoids / meshes, 3 / 4 the sole pair, 5 three banks of floor colliders */
   float* xj;                /* xg: [n + 1, ZB_XJ_STRIDE] second-bank Jacobian rows (the last block: ghost teams) */
   int ed;                   /* ZB_F_EULERDAMP: the step kernel integrates the joint damping implicitly */
 };
