@@ -77,8 +77,6 @@ struct EnvS {
   /* XG 1 / 2: the geoms in the second contact-row bank this substep (half 0, half 1; -1: none):
      the first two of geoms 2.. within reach of the floor (select_bank2) */
   int32_t xsel[2];
-  /* XG 5: the third bank's geoms (the third and fourth within reach) */
-  int32_t ysel[2];
 };
 struct Sensors {
   float fq[4], gyro[3], acc[3], touch[2], force[6];
@@ -110,6 +108,10 @@ struct __align__(16) EnvL {
                         scratch at the head of every substep) */
   EnvS s;
   Sensors sen;
+  /* XG 5: the third bank's geoms this substep (the third and fourth within reach; -1: none). Kept
+     behind the sensors rather than in EnvS so every field the other kernels address keeps its offset
+     and alignment (it fills the struct's tail padding) */
+  int32_t ysel[2];
 #ifdef ZB_STAMPS
   unsigned long long stamp[NSTAMP];
   unsigned long long stamp_last;
@@ -1732,7 +1734,7 @@ __device__ __forceinline__ bool lane_geom(const Ctx& c, int bank, int& g, int& g
   const int gl = c.l >> 4;
   if (XFLOOR<XG> && bank >= 1) {
     /* the second (third: XG 5) bank's geoms of this substep (select_bank2) */
-    const int sg = bank == 1 ? c.L->s.xsel[gl] : c.L->s.ysel[gl];
+    const int sg = bank == 1 ? c.L->s.xsel[gl] : c.L->ysel[gl];
     const bool sv = sg >= 0;
     g = sv ? sg : 0;
     gb = sv ? m->geom_body[g] : 0;
@@ -2455,8 +2457,8 @@ __device__ __forceinline__ void select_bank2(const Ctx& c, const BodyK& B) {
     mk &= mk - 1u;
     const int sel3 = mk ? 1 + __ffs(mk) : -1;
     mk &= mk - 1u;
-    c.L->s.ysel[0] = sel2;
-    c.L->s.ysel[1] = sel3;
+    c.L->ysel[0] = sel2;
+    c.L->ysel[1] = sel3;
   }
   /* team-uniform values, written by every lane of the team */
   c.L->s.xsel[0] = sel0;
@@ -2509,7 +2511,7 @@ __device__ __forceinline__ void make_constraints(const Ctx& c, const EnvS& s, co
       uint32_t rm = 0u;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        const int sg = c.L->s.ysel[h];
+        const int sg = c.L->ysel[h];
         const int kd = sg >= 0 ? m->body_lastdof[m->geom_body[sg]] : -1;
         const int kdc = kd >= 0 ? kd : 0;
         const int hkd = tshi(c.chd, kdc);
@@ -3567,7 +3569,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const EnvS& s, LaneS& ls, 
     float fnt = ex7[6];
     /* the pair's halves: g = 2 geom2's body (+F), g = 3 geom1's (-F, in xdir); each foot's touch
        sensor takes the pair's normal force (its geom is in the contact) */
-    const int gg = (YFLOOR<XG> && b2) ? c.L->s.ysel[g - 2 * NGEOM]
+    const int gg = (YFLOOR<XG> && b2) ? c.L->ysel[g - 2 * NGEOM]
                    : b2 ? m->pair_geom[g == 2 * NGEOM ? 1 : 0]
                    : (XPAIR<XG> && b1) ? m->pair_geom[g == NGEOM ? 1 : 0]
                    : (XFLOOR<XG> && b1) ? c.L->s.xsel[g - NGEOM] : g;
