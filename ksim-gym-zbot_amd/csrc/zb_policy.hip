@@ -44,16 +44,28 @@ namespace pol {
 
 constexpr int H = ZB_POL_HIDDEN;
 constexpr int D = ZB_POL_DEPTH;
-constexpr int M = ZB_POL_ENVS_PER_BLOCK; /* envs per workgroup */
+#ifndef ZB_POL_NET
+#define ZB_POL_NET 2
+#endif
 constexpr int MT = 16;                   /* envs per MFMA row tile */
+constexpr int M = MT * ZB_POL_NET;       /* envs per workgroup */
 constexpr int NET = M / MT;              /* row tiles per workgroup */
 constexpr int NWAVE = H / 16;            /* one wave per 16-unit tile */
 constexpr int NTHR = 64 * NWAVE;
-constexpr int LDA = M + 1;  /* row stride of the [k][env] activation tiles */
+#ifndef ZB_POL_LDA
+#define ZB_POL_LDA (M + 1)
+#endif
+constexpr int LDA = ZB_POL_LDA;  /* row stride of the [unit][env] layer tiles */
+constexpr int LDU = M + 1;       /* row stride of the [k][env] observation tile */
 constexpr int GH = H / 16;  /* 4-step (16-k) groups over K = H */
 constexpr int NJ = ZB_POL_JOINTS;
 constexpr int NMIX = ZB_POL_MIX;
-static_assert(M == 32 && NET == 2, "two 16-env row tiles of v_mfma_f32_16x16x4_f32");
+#if ZB_POL_NET == 1
+#define ZB_POL_OCC __attribute__((amdgpu_waves_per_eu(4, 4))) /* two workgroups per CU */
+#else
+#define ZB_POL_OCC
+#endif
+static_assert(NET == 1 || NET == 2, "one or two 16-env row tiles of v_mfma_f32_16x16x4_f32");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -69,6 +81,7 @@ __device__ __forceinline__ float q4(const float4& v, int u) {
 
 /* one output tile (16 columns) of X[32][K] W^T over K = 16 * G for both row tiles, A from
    LDS; each weight fragment feeds both row tiles */
+template <int LD>
 __device__ __forceinline__ void tile_gemm(const float* xs, const float4* wp, int G, int lane, f32x4 acc[NET]) {
   const int c16 = lane & 15, k4 = lane >> 4;
 #pragma unroll
@@ -77,11 +90,11 @@ __device__ __forceinline__ void tile_gemm(const float* xs, const float4* wp, int
   for (int g = 0; g < G; ++g) {
     const float4 bn = wp[(size_t)(g + 1 < G ? g + 1 : g) * 64];
     __builtin_amdgcn_sched_barrier(0); /* next group's load stays a group ahead */
-    const float* xp = xs + (16 * g + k4) * LDA + c16;
+    const float* xp = xs + (16 * g + k4) * LD + c16;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int et = 0; et < NET; ++et) acc[et] = mma(xp[4 * u * LDA + MT * et], q4(b, u), acc[et]);
+      for (int et = 0; et < NET; ++et) acc[et] = mma(xp[4 * u * LD + MT * et], q4(b, u), acc[et]);
     b = bn;
   }
 }
@@ -92,13 +105,13 @@ __device__ __forceinline__ void tile_gemm(const float* xs, const float4* wp, int
    (one-step actor 0.111 -> 0.107 ms, critic 0.134 -> 0.111 ms at 8192 envs, no spills, the same bits;
    profiles/r06_p11_policy_ab.log). */
 template <int KIN, int NOUT, bool ACTOR, bool PERSIST>
-__global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
+__global__ __launch_bounds__(NTHR) ZB_POL_OCC void policy_kernel(PolicyArgs a0) {
 #pragma clang fp contract(off)
   constexpr int KPAD = (KIN + 15) / 16 * 16;
   constexpr int GIN = KPAD / 16;
   constexpr int NTO = (NOUT + 15) / 16;
   constexpr int OUTS = NOUT + 1;
-  constexpr int XIN = KPAD * LDA;
+  constexpr int XIN = KPAD * LDU;
   constexpr int OUTW = ACTOR ? M * OUTS : 1;
   constexpr int UW = XIN > OUTW ? XIN : OUTW;
   __shared__ float su[UW];          /* observation tile [k][env]; then the actor output [env][c] */
@@ -179,19 +192,19 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
           const int f = 4 * i4 + c;
           if (f < FL) {
             const int e = f / KIN, k = f - e * KIN;
-            su[k * LDA + e] = c4[c]; /* zero past the last env */
+            su[k * LDU + e] = c4[c]; /* zero past the last env */
           }
         }
       }
     } else {
       for (int i = tid; i < FL; i += NTHR) {
         const int e = i / KIN, k = i - e * KIN;
-        su[k * LDA + e] = i < lim ? src[i] : 0.f;
+        su[k * LDU + e] = i < lim ? src[i] : 0.f;
       }
     }
     for (int i = tid; i < M * (KPAD - KIN); i += NTHR) { /* padding rows k = KIN .. KPAD - 1 */
       const int k = KIN + i / M, e = i - (i / M) * M;
-      su[k * LDA + e] = 0.f;
+      su[k * LDU + e] = 0.f;
     }
   }
   __syncthreads();
@@ -200,7 +213,7 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
   {
     const int unit = 16 * w + c16;
     f32x4 acc[NET];
-    tile_gemm(su, wp4 + (size_t)w * GIN * 64 + lane, GIN, lane, acc);
+    tile_gemm<LDU>(su, wp4 + (size_t)w * GIN * 64 + lane, GIN, lane, acc);
     const float bu = a.bias[unit];
 #pragma unroll
     for (int et = 0; et < NET; ++et)
@@ -325,7 +338,7 @@ __global__ __launch_bounds__(NTHR) void policy_kernel(PolicyArgs a0) {
     const float4* wo = wp4 + off_gru + (size_t)D * 2 * MAT + lane;
     for (int nt = w; nt < NTO; nt += NWAVE) {
       f32x4 acc[NET];
-      tile_gemm(xs, wo + (size_t)nt * GH * 64, GH, lane, acc);
+      tile_gemm<LDA>(xs, wo + (size_t)nt * GH * 64, GH, lane, acc);
       const int c = nt * 16 + c16;
       if (c < NOUT) {
         const float bc = tail[c];
