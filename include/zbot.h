@@ -73,11 +73,14 @@ void zb_default_config(ZbEnvConfig* cfg);
  * kernels; any other collider set runs a general-collider instantiation with a
  * second bank of 32 contact-row lanes (Jacobian rows in per-env global scratch),
  * which holds, each substep, the first two of the other colliders within reach
- * of the floor; a substep with more than two within reach sets bit 1 of the
- * state's flag word (ZB_S_NAN; bit 0: non-finite; bit 2: the same, for the
- * current control step only). npair = 1 (the two box soles against each other,
+ * of the floor. A model with more than two colliders beyond the soles (and no
+ * self pair) adds a third bank of floor colliders: the first four within reach.
+ * A substep with more within reach than the banks hold sets bit 1 of the state's
+ * flag word (ZB_S_NAN; bit 0: non-finite; bit 2: the same, for the current
+ * control step only). npair = 1 (the two box soles against each other,
  * geom-geom) holds the pair's contacts in that second bank when the soles are the
- * only colliders, and in a third bank beside the floor colliders' otherwise.
+ * only colliders, and in a third bank beside the floor colliders' otherwise (the
+ * floor colliders beyond the soles then keep the two of the second bank).
  *
  * Create a handle simulating `n_envs` environments whose global ids are
  * [env_offset, env_offset + n_envs) — RNG streams are keyed by global id, so

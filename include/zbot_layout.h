@@ -53,7 +53,7 @@ extern "C" {
 #define ZB_S_RNG_STEP    169  /* u32   global per-env step counter (RNG counter) */
 #define ZB_S_PREV_CONT   170  /* [2]   contact flags of the previous step (touchdown) */
 #define ZB_S_EPISODE     172  /* u32   episode index of this env (RNG counter) */
-#define ZB_S_NAN         173  /* u32   flags (diagnostic): bit 0 non-finite state (sticky); bit 1 more than two colliders beyond the soles within reach of the floor in a substep, their contacts not simulated (zb_engine.hip select_bank2; sticky); bit 2 the same in the last control step (cleared at the start of each) */
+#define ZB_S_NAN         173  /* u32   flags (diagnostic): bit 0 non-finite state (sticky); bit 1 more colliders beyond the soles within reach of the floor in a substep than its banks hold (four; two beside the sole pair), their contacts not simulated (zb_engine.hip select_bank2; sticky); bit 2 the same in the last control step (cleared at the start of each) */
 #define ZB_S_AIR0_CONT   174  /* u32   first step of a marked rollout: contact bits (1 left, 2 right) */
 #define ZB_S_AIR0_TERM   175  /*       ... and its causal FeetAirtime term (zb_feet_airtime_exact) */
 #define ZB_S_END         176

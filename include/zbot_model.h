@@ -40,7 +40,8 @@ extern "C" {
 #define ZB_MAX_QPOS  40
 #define ZB_MAX_DEPTH 12
 #define ZB_MAX_GEOM  16  /* floor colliders (model v9; the engine collides the two soles and, per substep,
-                            the first two others within reach of the floor: DESIGN.md §4j) */
+                            the first four others within reach of the floor, two beside the sole pair:
+                            DESIGN.md §4j) */
 #define ZB_MAX_MESHV 64  /* convex hull vertices of one mesh collider */
 #define ZB_MAX_MESHVERT 512 /* the mesh vertex pool (all mesh colliders together) */
 #define ZB_MAX_SITE  8

@@ -120,8 +120,9 @@ DBG = dict(qM=0, bias=1024, qacc_smooth=1056, qacc=1088, xpos=1120, cinert=1216,
 def state_flags(state) -> dict:
     """The sticky diagnostic flags of a [n, ZB_STATE_STRIDE] state (get_state()), as boolean [n]
     tensors (include/zbot_layout.h ZB_S_NAN): `nonfinite` - the env's state went non-finite;
-    `bank_overflow` - in some substep more than two colliders beyond the soles were within reach of
-    the floor, and the extra ones' contacts were not simulated (zb_engine.hip select_bank2).
+    `bank_overflow` - in some substep more colliders beyond the soles were within reach of the floor
+    than the contact-row banks hold (four; two beside the sole pair), and the extra ones' contacts were
+    not simulated (zb_engine.hip select_bank2).
     Both are sticky for the life of the env's state row (resets keep them; set_state() can clear
     them). `bank_overflow_step`: the same overflow in the last control step alone (the kernel clears
     it at the start of every step), so the step that ends an episode still shows it. Works on CPU or

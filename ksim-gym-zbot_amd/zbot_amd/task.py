@@ -212,8 +212,8 @@ class ZbotWalkingEnv:
         return self.curriculum_level
 
     def check_bank_overflow(self, state=None) -> int:
-        """Envs whose second contact-row bank overflowed at some substep (more than two colliders beyond
-        the soles within reach of the floor; the extra ones' contacts were not simulated: zb_engine.hip
+        """Envs whose second contact-row bank overflowed at some substep (more colliders beyond the soles
+        within reach of the floor than the banks hold: four, two beside the sole pair; the extra ones' contacts were not simulated: zb_engine.hip
         select_bank2, engine.state_flags). Warns once per env object the first time any env has; called
         by update_curriculum() after every rollout. Returns the count."""
         from .engine import state_flags  # noqa: PLC0415
@@ -222,8 +222,8 @@ class ZbotWalkingEnv:
         if n and not getattr(self, "_overflow_warned", False):
             import warnings  # noqa: PLC0415
 
-            warnings.warn(f"{n} env(s) had more than two colliders beyond the soles within reach of the floor in one "
-                          "substep; the contacts beyond the first two were not simulated (DESIGN.md §4j)", RuntimeWarning,
+            warnings.warn(f"{n} env(s) had more colliders beyond the soles within reach of the floor in one "
+                          "substep than the contact-row banks hold; the extra contacts were not simulated (DESIGN.md §4j)", RuntimeWarning,
                           stacklevel=2)
             self._overflow_warned = True
         return n
