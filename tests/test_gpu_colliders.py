@@ -106,8 +106,11 @@ NO_FP64_SLACK = {"cyl"}
 ENSEMBLE_ONLY = {"mjxbox"}
 
 
+@pytest.mark.parametrize("eulerdamp", [False, True], ids=["explicit", "eulerdamp"])
 @pytest.mark.parametrize("solver", ["newton", "cg"])
-def test_one_step_matches_oracle(torch_gpu, variant, oracle_mod, solver):
+def test_one_step_matches_oracle(torch_gpu, variant, oracle_mod, solver, eulerdamp):
+    """eulerdamp: mj_Euler's implicit damping (the ED instantiations of the general-collider kernels)
+    under the same contract as the explicit form, as tests/test_gpu_parity.py holds the two-sole model."""
     torch = torch_gpu
     from test_gpu_parity import (CG_BUDGET, CG_LOOSE, CG_SLACK, MaxErr, boundary_envs, one_step_outputs, oracle_sensitivity,
                                  oracle_steps)
@@ -115,13 +118,13 @@ def test_one_step_matches_oracle(torch_gpu, variant, oracle_mod, solver):
     from zbot_amd.engine import HipEngine
 
     name, cm = variant
-    cfg = default_config(solver=solver)
+    cfg = default_config(solver=solver, eulerdamp=eulerdamp)
     n = 64
     cg = solver == "cg"
     env = contact_env(oracle_mod, cm, cfg, n, seed=11)
     eng = HipEngine(cm, cfg, n, seed=11)
     kw = dict(budget=CG_BUDGET, loose=CG_LOOSE, max_ill=n, k_slack=CG_SLACK) if cg else {}
-    err = MaxErr(f"colliders {name} {solver} one-step", exempt_ill=name in ENSEMBLE_ONLY, **kw)
+    err = MaxErr(f"colliders {name} {solver}{' eulerdamp' if eulerdamp else ''} one-step", exempt_ill=name in ENSEMBLE_ONLY, **kw)
     # the second step starts from the oracle's first, where the lying robots (56 of 64) have been
     # reset onto flat soles: for ENSEMBLE_ONLY variants that is the flat-face tie of their rollouts
     for t in range(1 if name in ENSEMBLE_ONLY else 2):
@@ -299,8 +302,9 @@ def test_many_colliders_match_oracle_within_the_cap(torch_gpu, oracle_mod):
 
     cm = compile_model(U.many_desc())
     n = 64
-    for solver in ("newton", "cg"):
-        cfg = default_config(solver=solver)
+    for solver, ed in (("newton", False), ("cg", False), ("newton", True), ("cg", True)):
+        cfg = default_config(solver=solver, eulerdamp=ed)
+        tag = solver + (" eulerdamp" if ed else "")
         env = contact_env(oracle_mod, cm, cfg, n, seed=5)
         st = env.state.copy()
         cand = np.array([len(U.bank2_candidates(cm, st[e, :27].astype(np.float64))) for e in range(n)])
@@ -312,13 +316,13 @@ def test_many_colliders_match_oracle_within_the_cap(torch_gpu, oracle_mod):
             if cand[e] > BANK_CAP:
                 continue
             ref = oracle_mod.forward_debug(cm.cmodel, cfg, st[e, :27], st[e, 32:58], ctrl[e], precision="f64")
-            assert int(g[e, DBG["misc"] + 1]) == ref["ncon"], (solver, e)
-            assert int(g[e, DBG["misc"]]) == ref["nefc"], (solver, e)
+            assert int(g[e, DBG["misc"] + 1]) == ref["ncon"], (tag, e)
+            assert int(g[e, DBG["misc"]]) == ref["nefc"], (tag, e)
             qa = g[e, DBG["qacc"]:DBG["qacc"] + 26]
             tol = 1e-3 if solver == "newton" else 5e-2  # CG: 8 unconverged iterations (test_gpu_sole_pair)
-            assert np.abs(qa - ref["qacc"]).max() / max(1.0, np.abs(ref["qacc"]).max()) <= tol, (solver, e)
+            assert np.abs(qa - ref["qacc"]).max() / max(1.0, np.abs(ref["qacc"]).max()) <= tol, (tag, e)
             checked += 1
-        print(f"\n[many colliders {solver}] forward pass: {checked} of {n} envs within {BANK_CAP} candidates beyond "
+        print(f"\n[many colliders {tag}] forward pass: {checked} of {n} envs within {BANK_CAP} candidates beyond "
               f"the soles (candidates per env {np.bincount(cand).tolist()}), {int((cand > 2).sum())} of them "
               "beyond round 5's two")
         assert checked >= n // 2
@@ -342,12 +346,12 @@ def test_many_colliders_match_oracle_within_the_cap(torch_gpu, oracle_mod):
         kw = dict(budget=CG_BUDGET, loose=CG_LOOSE, max_ill=n, k_slack=CG_SLACK) if cg else {}
         ref32 = {k: want for k, _, want in one_step_outputs(env.state, ref, env.state, ref)}
         sens = oracle_sensitivity(oracle_mod, cm, cfg, st0, rd0, a, 5, ref32) if cg else {}
-        err = MaxErr(f"many colliders {solver} one-step (unflagged envs)", **kw)
+        err = MaxErr(f"many colliders {tag} one-step (unflagged envs)", **kw)
         for key, got, want in one_step_outputs(gs, out, env.state, ref):
             sk = sens.get(key)
             err.add(key, got[keep], want[keep], *COLLIDER_TOL[key], ref64=ref64[key][keep],
                     sens=None if sk is None else np.asarray(sk)[keep])
-        print(f"[many colliders {solver}] one step: {int(keep.sum())} of {n} envs without the overflow flag")
+        print(f"[many colliders {tag}] one step: {int(keep.sum())} of {n} envs without the overflow flag")
         err.report()
 
 

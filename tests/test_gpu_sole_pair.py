@@ -126,8 +126,10 @@ PAIR_TOL = {
 }
 
 
+@pytest.mark.parametrize("eulerdamp", [False, True], ids=["explicit", "eulerdamp"])
 @pytest.mark.parametrize("solver", ["newton", "cg"])
-def test_one_step_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
+def test_one_step_matches_oracle(torch_gpu, pair_model, oracle_mod, solver, eulerdamp):
+    """eulerdamp: the XG 3 / 4 kernels' ED instantiations under the explicit form's contract."""
     torch = torch_gpu
     from test_gpu_parity import (CG_BUDGET, CG_LOOSE, CG_SLACK, MaxErr, boundary_envs, one_step_outputs, oracle_sensitivity,
                                  oracle_steps)
@@ -135,7 +137,7 @@ def test_one_step_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
     from zbot_amd.engine import HipEngine
 
     cm = pair_model
-    cfg = default_config(solver=solver)
+    cfg = default_config(solver=solver, eulerdamp=eulerdamp)
     n = 64
     cg = solver == "cg"
     env = crossing_env(oracle_mod, cm, cfg, n, seed=11)
@@ -144,7 +146,7 @@ def test_one_step_matches_oracle(torch_gpu, pair_model, oracle_mod, solver):
     # envs per output and step within CG_LOOSE x beyond it (round 5 held CG to the flat COLLIDER_TOL_CG
     # with up to 12 envs at a discontinuity)
     kw = dict(budget=CG_BUDGET, loose=CG_LOOSE, max_ill=n, k_slack=CG_SLACK) if cg else {}
-    err = MaxErr(f"sole pair {cm.variant} {solver} one-step", **kw)
+    err = MaxErr(f"sole pair {cm.variant} {solver}{' eulerdamp' if eulerdamp else ''} one-step", **kw)
     for t in range(2):
         st0, rd0 = env.state.copy(), env.rand.copy()
         eng.set_state(torch.from_numpy(st0.copy()))
