@@ -183,11 +183,21 @@ __device__ __forceinline__ void tsum_n(float v[N]) {
   for (int i = 0; i < N; i++) v[i] += dppf<0x141>(v[i]);
 #pragma unroll
   for (int i = 0; i < N; i++) v[i] += dppf<0x140>(v[i]);
+  /* the row exchange two values at a time: one swap of (v[i], v[i + 1]) puts value i's two row sums
+     side by side in rows 0 / 2 and value i + 1's in rows 1 / 3; their sum, swapped with itself, sends
+     each value's team total to all 32 lanes. The same additions in the same order as rows2 + add */
 #pragma unroll
-  for (int i = 0; i < N; i++) {
+  for (int i = 0; i + 1 < N; i += 2) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 1]), false, false);
+    const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+    v[i] = __uint_as_float(q[0]);
+    v[i + 1] = __uint_as_float(q[1]);
+  }
+  if constexpr ((N & 1) != 0) {
     float a, b;
-    rows2(v[i], a, b);
-    v[i] = a + b;
+    rows2(v[N - 1], a, b);
+    v[N - 1] = a + b;
   }
 }
 /* 21 team sums (the root Schur complement), written to out[0..20] in LDS: a
