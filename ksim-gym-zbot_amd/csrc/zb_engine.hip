@@ -33,7 +33,44 @@
 
 #include "zb_internal.h"
 
+/* The product library compiles this file twice (Makefile): once for the collider sets (XG) whose step
+   kernels run fastest under the iterative-ILP machine scheduler, once, with ZB_ENGINE_TU_B, for the
+   others under the default one (the scheduler is chosen per compilation unit). ZB_XG_MASK: the XG
+   values whose kernels this unit compiles; the entry points of the first unit hand the others' to the
+   second unit's (*_tu_b). Without the defines (diagnostic builds) one unit holds every XG. */
+#ifndef ZB_XG_MASK
+#define ZB_XG_MASK 0x3F
+#endif
+#ifdef ZB_ENGINE_TU_B
+#define ZB_EP(f) f##_tu_b
+#else
+#define ZB_EP(f) f
+#endif
+
 namespace zb {
+constexpr int XG_MASK = ZB_XG_MASK;
+__host__ __device__ constexpr bool xg_here(int xg) { return ((XG_MASK >> xg) & 1) != 0; }
+#if !defined(ZB_ENGINE_TU_B) && ZB_XG_MASK != 0x3F
+int step_resident_blocks_tu_b(int device, int xg, int solver, int ed);
+hipError_t launch_step_tu_b(const StepArgs& a, hipStream_t s);
+hipError_t launch_reset_tu_b(const StepArgs& a, hipStream_t s);
+hipError_t launch_debug_forward_tu_b(const StepArgs& a, hipStream_t s);
+#define ZB_HANDOFF(xg, fn, ...)                 \
+  do {                                          \
+    if (!xg_here(xg)) return fn##_tu_b(__VA_ARGS__); \
+  } while (0)
+#else
+/* an XG this unit does not hold never reaches it (the first unit hands it off): fail loudly */
+template <typename T>
+constexpr T not_here() {
+  if constexpr (std::is_same<T, hipError_t>::value) return hipErrorInvalidValue;
+  else return T{};
+}
+#define ZB_HANDOFF(xg, fn, ...)                                          \
+  do {                                                                   \
+    if (!xg_here(xg)) return not_here<decltype(ZB_EP(fn)(__VA_ARGS__))>(); \
+  } while (0)
+#endif
 
 constexpr int TEAM = 32;
 constexpr int NTEAM = 64 / TEAM;
@@ -4520,12 +4557,13 @@ __host__ void with_variant(int solver, int xg, int ed, F&& f) {
   using std::integral_constant;
   auto by_xg = [&](auto S, auto D) {
     switch (xg) {
-      case 5: f(S, integral_constant<int, 5>{}, D); break;
-      case 4: f(S, integral_constant<int, 4>{}, D); break;
-      case 3: f(S, integral_constant<int, 3>{}, D); break;
-      case 2: f(S, integral_constant<int, 2>{}, D); break;
-      case 1: f(S, integral_constant<int, 1>{}, D); break;
-      default: f(S, integral_constant<int, 0>{}, D); break;
+      /* only this unit's XG values are instantiated (ZB_XG_MASK); the entry points hand the others off */
+      case 5: if constexpr (xg_here(5)) f(S, integral_constant<int, 5>{}, D); break;
+      case 4: if constexpr (xg_here(4)) f(S, integral_constant<int, 4>{}, D); break;
+      case 3: if constexpr (xg_here(3)) f(S, integral_constant<int, 3>{}, D); break;
+      case 2: if constexpr (xg_here(2)) f(S, integral_constant<int, 2>{}, D); break;
+      case 1: if constexpr (xg_here(1)) f(S, integral_constant<int, 1>{}, D); break;
+      default: if constexpr (xg_here(0)) f(S, integral_constant<int, 0>{}, D); break;
     }
   };
   auto by_ed = [&](auto S) {
@@ -4536,7 +4574,8 @@ __host__ void with_variant(int solver, int xg, int ed, F&& f) {
   else by_ed(integral_constant<int, ZB_SOLVER_NEWTON>{});
 }
 
-int step_resident_blocks(int device, int xg, int solver, int ed) {
+int ZB_EP(step_resident_blocks)(int device, int xg, int solver, int ed) {
+  ZB_HANDOFF(xg, step_resident_blocks, device, xg, solver, ed);
   int per_cu = 0, cus = 0;
   /* the instantiation the handle launches: CG and Newton differ in registers and LDS */
   hipError_t e = hipSuccess;
@@ -4549,8 +4588,9 @@ int step_resident_blocks(int device, int xg, int solver, int ed) {
   return per_cu * cus;
 }
 
-hipError_t launch_step(const StepArgs& a, hipStream_t s) {
+hipError_t ZB_EP(launch_step)(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
+  ZB_HANDOFF(a.xg, launch_step, a, s);
   if (a.nchunk < 1 || (a.nchunk > 1 && (a.nsteps != 1 || !a.sched || !a.itpart))) return hipErrorInvalidValue;
 #ifdef ZB_STAMPS
   StepArgs b = a;
@@ -4575,6 +4615,7 @@ hipError_t launch_step(const StepArgs& a, hipStream_t s) {
    written over reward_terms0's FeetAirtime slot. The episode statistics' reward sum (ZB_ST_REWARD)
    gets the same delta, so it stays the sum of the rollout's patched rows; episode returns
    (ZB_ST_RETURN, the state row's running return) keep the causal row 0 (include/zbot.h). */
+#ifndef ZB_ENGINE_TU_B
 __global__ __launch_bounds__(256) void airtime_exact_kernel(const float* __restrict__ state, const ZbEnvConfig* cfg,
                                                             int n, float curriculum, float* reward0, float* terms0,
                                                             float* stats) {
@@ -4601,17 +4642,20 @@ hipError_t launch_airtime_exact(const StepArgs& a, hipStream_t s) {
                      a.reward, a.reward_terms, a.stats);
   return hipGetLastError();
 }
+#endif
 
-hipError_t launch_reset(const StepArgs& a, hipStream_t s) {
+hipError_t ZB_EP(launch_reset)(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
+  ZB_HANDOFF(a.xg, launch_reset, a, s);
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
   with_variant(a.solver, a.xg, 0, [&](auto S, auto X, auto) {
     hipLaunchKernelGGL((reset_kernel<decltype(S)::value, decltype(X)::value>), grid, block, 0, s, a);
   });
   return hipGetLastError();
 }
-hipError_t launch_debug_forward(const StepArgs& a, hipStream_t s) {
+hipError_t ZB_EP(launch_debug_forward)(const StepArgs& a, hipStream_t s) {
   if (a.n_envs <= 0) return hipSuccess;
+  ZB_HANDOFF(a.xg, launch_debug_forward, a, s);
   dim3 grid((a.n_envs + NTEAM - 1) / NTEAM), block(64);
   with_variant(a.solver, a.xg, 0, [&](auto S, auto X, auto) {
     hipLaunchKernelGGL((debug_forward_kernel<decltype(S)::value, decltype(X)::value>), grid, block, 0, s, a);
